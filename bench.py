@@ -1,0 +1,225 @@
+#!/usr/bin/env python3
+"""Benchmark: GiB/s of Merkle leaf-hash + tree-reduce over device-resident record values.
+
+One step = the Merkle step of one SSTable build on each GPU: SHA-1 of every value
+(NewLeaf, merklenode.go:27-34) + the full tree (build, merkletree.go:31-64) over
+BASELINE config 2 -- 1 Mi values x 4 KiB, resident in HBM when timing starts.
+With N > 1 ranks each GPU builds its own table (one run per GPU, as in
+lsmtree compaction) and the 20-byte roots are all-gathered over RCCL every step.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+Rank 0 prints one JSON line (see DESIGN.md "Measurement").
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md (chip table)
+SEED = 0x6E616B65
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--leaves", type=int, default=1 << 20)
+    ap.add_argument("--value-bytes", type=int, default=4096)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-leaves", type=int, default=1 << 20)
+    ap.add_argument("--verify", action="store_true", help="check the root against the C oracle")
+    ap.add_argument("--no-kernel-timing", action="store_true",
+                    help="do not record per-kernel HIP events inside the timed loop")
+    return ap.parse_args()
+
+
+def cpu_baseline(n_leaves: int, vlen: int) -> dict:
+    """The oracle (C restatement of ds/merkletree, one thread, like the Go reference)."""
+    import numpy as np
+    from oracle import oracle_c as oc
+    oc.build()
+    data = oc.splitmix64_bytes(n_leaves * vlen, SEED)
+    t0 = time.perf_counter()
+    leaves = oc.leaf_hashes_strided(data, vlen, vlen, n_leaves, threads=1)
+    nodes = oc.tree_from_digests(leaves)
+    dt = time.perf_counter() - t0
+    # informational: OpenSSL SHA-1 (hashlib) on one core over a 256 MiB slice
+    k = min(n_leaves, (256 << 20) // vlen)
+    t1 = time.perf_counter()
+    for i in range(k):
+        hashlib.sha1(memoryview(data)[i * vlen:(i + 1) * vlen]).digest()
+    dt2 = time.perf_counter() - t1
+    del data
+    return {
+        "value": round(n_leaves * vlen / dt / 2**30, 4),
+        "unit": "GiB/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"{n_leaves} x {vlen} B values (splitmix64 seed {SEED:#x}), leaf hash + full tree, "
+                  f"oracle/merkle_oracle.c single thread, {dt:.2f} s",
+        "root": nodes[-1].tobytes().hex(),
+        "openssl_leaf_hash_1core_GiBps": round(k * vlen / dt2 / 2**30, 4),
+    }
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+
+    from nakevaleng_amd import build as nb
+    if rank == 0 or not os.path.exists(nb.SO):
+        nb.build()
+    if world > 1:
+        dist.barrier()
+    from nakevaleng_amd import _lib
+
+    L = _lib.lib()
+    dev = torch.cuda.current_device()
+    ctx = _lib.Context(dev)
+    stream = torch.cuda.current_stream()
+    ctx.set_stream(stream.cuda_stream)
+
+    n, vlen = args.leaves, args.value_bytes
+    nbytes = n * vlen
+    data = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    _lib.check(L.nkv_fill_splitmix64_dev(ctx.h, data.data_ptr(), nbytes, SEED + rank))
+    total_nodes = L.nkv_total_nodes(n)
+    nodes = torch.empty(total_nodes * 20, dtype=torch.uint8, device="cuda")
+    roots = torch.empty(world * 20, dtype=torch.uint8, device="cuda")
+
+    def step():
+        _lib.check(L.nkv_tree_from_strided_dev(ctx.h, data.data_ptr(), vlen, vlen, n, nodes.data_ptr()))
+        if world > 1:  # C1: gather the per-table roots
+            dist.all_gather_into_tensor(roots, nodes[-20:])
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ctx.set_timing(not args.no_kernel_timing)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    calls, leaf_ms_tot, reduce_ms_tot = ctx.timing_summary()
+    ctx.set_timing(False)
+    if calls == 0:  # kernel split measured in a separate loop of the same steps
+        ctx.set_timing(True)
+        for _ in range(args.steps):
+            step()
+        calls, leaf_ms_tot, reduce_ms_tot = ctx.timing_summary()
+        ctx.set_timing(False)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    root = nodes[-20:].cpu().numpy().tobytes().hex()
+    leaf_ms = leaf_ms_tot / max(calls, 1)
+    reduce_ms = reduce_ms_tot / max(calls, 1)
+
+    # K3 (Serialize image) timed separately: not part of the metric
+    img = torch.empty(L.nkv_bfs_size(n), dtype=torch.uint8, device="cuda")
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    _lib.check(L.nkv_bfs_image_dev(ctx.h, nodes.data_ptr(), n, img.data_ptr()))
+    e0.record(stream)
+    for _ in range(5):
+        _lib.check(L.nkv_bfs_image_dev(ctx.h, nodes.data_ptr(), n, img.data_ptr()))
+    e1.record(stream)
+    torch.cuda.synchronize()
+    bfs_ms = e0.elapsed_time(e1) / 5
+
+    verified = None
+    if args.verify and rank == 0:
+        from oracle import oracle_c as oc
+        host = oc.splitmix64_bytes(nbytes, SEED)
+        want = oc.tree_from_digests(oc.leaf_hashes_strided(host, vlen, vlen, n, threads=16))
+        verified = want[-1].tobytes().hex() == root
+        del host
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(min(args.cpu_sample_leaves, n), vlen)
+
+    if rank == 0:
+        total_bytes = nbytes * world * args.steps
+        value = total_bytes / elapsed / 2**30
+        achieved = nbytes / (leaf_ms * 1e-3) / 1e9  # algorithmic payload bytes per K1 launch
+        traffic = None
+        pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(pmc_path):
+            with open(pmc_path) as f:
+                pmc = json.load(f)
+            if pmc.get("leaves") == n and pmc.get("value_bytes") == vlen:
+                traffic = pmc.get("hbm_bytes_per_launch")
+        out = {
+            "metric": "GiB/s Merkle leaf-hash + tree-reduce over device-resident record blocks",
+            "value": round(value, 2),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": f"synthetic: splitmix64 bytes (seed {SEED:#x} + rank) generated in HBM",
+            "config": {
+                "workload": "BASELINE configs[1]: single SSTable flush, 1 Mi x 4 KiB values, "
+                            "leaf SHA-1 + full tree reduce (one table per GPU; roots all-gathered over RCCL when N>1)",
+                "leaves_per_gpu": n,
+                "value_bytes": vlen,
+                "parallelism": f"{world} independent tables" + (" + RCCL all_gather of roots" if world > 1 else ""),
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "k_leaf<strided,fused,aligned> (leaf SHA-1 + first 8 levels)",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+            },
+            "kernel_ms": {"leaf_fused": round(leaf_ms, 4), "tree_reduce_rest": round(reduce_ms, 4),
+                          "bfs_image": round(bfs_ms, 4)},
+            "root": root,
+            "cpu_baseline": cpu,
+        }
+        if verified is not None:
+            out["verified_vs_oracle"] = verified
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

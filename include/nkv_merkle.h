@@ -1,0 +1,171 @@
+/*
+ * nkv_merkle.h -- C-ABI of libnkvmerkle.so, the MI355X (gfx950) Merkle step of
+ * nakevaleng's SSTable build.
+ *
+ * This is the drop-in boundary for the reference's ds/merkletree package
+ * (magley/nakevaleng, Go).  A Go cgo shim keeps the exact Go
+ * API -- NewLeaf / New / (*MerkleTree).Serialize / Deserialize / Validate --
+ * and calls the entry points below; the C++ header nkv_merkletree.hpp is the
+ * same shim for C++ hosts.  Paths in the citations are relative to the
+ * reference root.
+ *
+ *   reference symbol                                   replaced by
+ *   ------------------------------------------------   -------------------------------
+ *   merkletree.NewLeaf      ds/merkletree/merklenode.go:27-34   nkv_leaf_hash (batched)
+ *   merkletree.New / build  ds/merkletree/merkletree.go:18-64   nkv_tree_build, nkv_tree_generic
+ *   NewLeaf loop + New      core/sstable/sstable.go:58-71       nkv_tree_from_values
+ *   (*MerkleTree).Serialize ds/merkletree/merkletree.go:67-92   image from the calls above +
+ *                           ds/merkletree/merklenode.go:37-63   nkv_write_file
+ *   MakeTableSecondaries    core/sstable/sstable.go:35-47       nkv_tree_from_values /
+ *     (Merkle part) + lsmtree.merge leaf collection               nkv_tree_from_records
+ *                           core/lsmtree/lsmtree.go:146,211
+ *   (*MerkleTree).Validate  ds/merkletree/merkletree.go:162-171 nkv_tree_build / nkv_tree_generic
+ *                           ds/merkletree/merklenode.go:99-108    + 20-byte root compare
+ *   record value location   core/record/record.go:191-199       nkv_locate_values_dev
+ *
+ * Conventions
+ *   - Every function returns an nkv_status (0 = NKV_OK) unless noted; nothing
+ *     aborts.  nkv_strerror() gives the message; NKV_ERR_EMPTY's message is
+ *     the reference's exact error text (merkletree.go:20).
+ *   - Digests are 20 bytes in Go's byte order (sha1.Sum output).
+ *   - "nodes" buffers hold every tree level bottom-up, level-major: level L
+ *     has nkv_level_count(n, L) digests starting at digest index
+ *     nkv_level_start(n, L); level 0 is the leaves, the root is the last
+ *     digest (index nkv_total_nodes(n) - 1).  Pads are not stored.
+ *   - "img" buffers receive the exact byte image Serialize() writes
+ *     (nkv_bfs_size(n) bytes for 20-byte leaves).
+ *   - Host-pointer functions are synchronous: outputs are written before
+ *     return, and no caller pointer is retained (cgo rule).  Inputs are
+ *     staged through library-owned pinned memory.
+ *   - *_dev functions take device pointers and are asynchronous on the
+ *     context's stream (nkv_ctx_set_stream); nkv_ctx_sync() waits.
+ *   - Thread safety: distinct contexts may be used concurrently; one context
+ *     must not be used by two threads at once.  Every call re-binds the
+ *     context's device (cgo calls may land on any OS thread).
+ */
+#ifndef NKV_MERKLE_H
+#define NKV_MERKLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NKV_DIGEST_SIZE 20
+#define NKV_MERKLE_NODE_EMPTY 1 /* merklenode.go:11 */
+
+typedef enum nkv_status {
+    NKV_OK = 0,
+    NKV_ERR_EMPTY = 1,   /* "cannot build Merkle Tree from 0 nodes" (merkletree.go:20) */
+    NKV_ERR_INVALID = 2, /* bad argument (null pointer, size overflow, bad record) */
+    NKV_ERR_DEVICE = 3,  /* HIP runtime / kernel launch failure, or no such device */
+    NKV_ERR_NOMEM = 4,   /* device or pinned-host allocation failed */
+    NKV_ERR_IO = 5       /* file open/write failed (nkv_write_file) */
+} nkv_status;
+
+typedef struct nkv_ctx nkv_ctx;
+
+/* ---- errors, devices, contexts ---- */
+const char *nkv_strerror(int status);
+int nkv_device_count(int *count);
+int nkv_ctx_create(int device, nkv_ctx **out);
+void nkv_ctx_destroy(nkv_ctx *ctx);
+/* Work is issued on the context's own (non-blocking) stream until
+ * nkv_ctx_set_stream() selects a hipStream_t of the context's device; NULL
+ * selects the device's null stream.  nkv_ctx_use_own_stream() switches back. */
+int nkv_ctx_set_stream(nkv_ctx *ctx, void *hip_stream);
+int nkv_ctx_use_own_stream(nkv_ctx *ctx);
+int nkv_ctx_sync(nkv_ctx *ctx);
+/* When enabled, the device-resident tree calls record HIP events around the
+ * leaf kernel and the tree reduce on the context's stream. */
+int nkv_ctx_set_timing(nkv_ctx *ctx, int enable);
+int nkv_ctx_last_timing(nkv_ctx *ctx, float *leaf_ms, float *reduce_ms);
+/* Sum over every tree call since timing was (re-)enabled: synchronizes on the
+ * last call's events only, so a timed loop is not perturbed. */
+int nkv_ctx_timing_summary(nkv_ctx *ctx, int *calls, float *leaf_ms_total, float *reduce_ms_total);
+
+/* ---- tree shape (pure, no device) ---- */
+int nkv_num_levels(uint64_t n); /* incl. the leaf level; 0 for n == 0 */
+uint64_t nkv_level_count(uint64_t n, int level);
+uint64_t nkv_level_start(uint64_t n, int level);
+uint64_t nkv_total_nodes(uint64_t n);
+uint64_t nkv_bfs_size(uint64_t n); /* Serialize() bytes for 20-byte leaves */
+
+/* ---- pinned host arena (for the deferred-NewLeaf shim) ---- */
+int nkv_host_alloc(nkv_ctx *ctx, uint64_t bytes, void **out);
+int nkv_host_free(nkv_ctx *ctx, void *p);
+
+/* ---- host-buffer API (synchronous) ---- */
+
+/* NewLeaf over n values: value i = base[off[i] .. off[i]+len[i]).
+ * out20: n * 20 bytes. */
+int nkv_leaf_hash(nkv_ctx *ctx, const uint8_t *base, const uint64_t *off, const uint64_t *len,
+                  uint64_t n, uint8_t *out20);
+
+/* New() over n NewLeaf digests (leaf20: n * 20 bytes).  Outputs are
+ * optional (NULL to skip): root20 (20 B), nodes_out (nkv_total_nodes(n) * 20 B),
+ * img_out (nkv_bfs_size(n) B). */
+int nkv_tree_build(nkv_ctx *ctx, const uint8_t *leaf20, uint64_t n, uint8_t *root20,
+                   uint8_t *nodes_out, uint8_t *img_out);
+
+/* makeMetadata: NewLeaf(value_i) for all i, then New, then the Serialize
+ * image -- in one call. */
+int nkv_tree_from_values(nkv_ctx *ctx, const uint8_t *base, const uint64_t *off,
+                         const uint64_t *len, uint64_t n, uint8_t *root20, uint8_t *nodes_out,
+                         uint8_t *img_out);
+
+/* New() over leaves with arbitrary Data (leaf i = data[off[i] .. +len[i]),
+ * README example ds/merkletree/README.md:44-57).  upper_out receives levels
+ * 1..top ((nkv_total_nodes(n) - n) * 20 B).  img_out receives the Serialize
+ * image (length nkv_generic_bfs_size()). */
+uint64_t nkv_generic_bfs_size(const uint64_t *len, uint64_t n);
+int nkv_tree_generic(nkv_ctx *ctx, const uint8_t *data, const uint64_t *off, const uint64_t *len,
+                     uint64_t n, uint8_t *root20, uint8_t *upper_out, uint8_t *img_out);
+
+/* Merkle step straight from a serialized Data-table stream (the records
+ * written by record.Serialize, record.go:191-199) and the RecSize of each
+ * record (record.KeyContext, record.go:38-41).  Leaves are the record Values
+ * (sstable.go:62, lsmtree.go:211), hashed in place on the device. */
+int nkv_tree_from_records(nkv_ctx *ctx, const uint8_t *stream, uint64_t stream_len,
+                          const uint64_t *rec_size, uint64_t n, uint8_t *root20,
+                          uint8_t *nodes_out, uint8_t *img_out);
+
+/* Serialize()'s file semantics: open O_WRONLY|O_CREAT (mode 0666) WITHOUT
+ * O_TRUNC (merkletree.go:68), write len bytes at offset 0, close. */
+int nkv_write_file(const char *fname, const uint8_t *data, uint64_t len);
+
+/* ---- device-resident API (asynchronous on the context stream) ---- */
+
+/* level 0 of d_nodes from n values at d_base + d_off[i], d_len[i] (any alignment) */
+int nkv_leaf_hash_dev(nkv_ctx *ctx, const void *d_base, const uint64_t *d_off,
+                      const uint64_t *d_len, uint64_t n, void *d_nodes);
+/* level 0 of d_nodes from n values of len bytes at d_base + i * stride */
+int nkv_leaf_hash_strided_dev(nkv_ctx *ctx, const void *d_base, uint64_t stride, uint64_t len,
+                              uint64_t n, void *d_nodes);
+/* levels 1..top of d_nodes from its level 0 */
+int nkv_tree_reduce_dev(nkv_ctx *ctx, void *d_nodes, uint64_t n);
+/* leaf hash fused with the first tree levels, then the rest of the reduce */
+int nkv_tree_from_values_dev(nkv_ctx *ctx, const void *d_base, const uint64_t *d_off,
+                             const uint64_t *d_len, uint64_t n, void *d_nodes);
+int nkv_tree_from_strided_dev(nkv_ctx *ctx, const void *d_base, uint64_t stride, uint64_t len,
+                              uint64_t n, void *d_nodes);
+/* Serialize() image of a 20-byte-leaf tree (nkv_bfs_size(n) bytes) */
+int nkv_bfs_image_dev(nkv_ctx *ctx, const void *d_nodes, uint64_t n, void *d_img);
+/* d_rec_off[i] = sum of d_rec_size[0..i) (exclusive scan of KeyContext.RecSize) */
+int nkv_record_offsets_dev(nkv_ctx *ctx, const uint64_t *d_rec_size, uint64_t n,
+                           uint64_t *d_rec_off);
+/* value offset/length of each record; NKV_ERR_INVALID (after a sync) if a
+ * header points outside the stream */
+int nkv_locate_values_dev(nkv_ctx *ctx, const void *d_stream, uint64_t stream_len,
+                          const uint64_t *d_rec_off, uint64_t n, uint64_t *d_voff,
+                          uint64_t *d_vlen);
+/* synthetic input: byte j = byte (j % 8) of splitmix64(seed, j / 8) */
+int nkv_fill_splitmix64_dev(nkv_ctx *ctx, void *d_buf, uint64_t nbytes, uint64_t seed);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NKV_MERKLE_H */

@@ -1,0 +1,180 @@
+"""ctypes binding of libnkvmerkle.so (the C-ABI in include/nkv_merkle.h).
+
+The product path has no CPU fallback: if the HIP library is missing, or no
+device is usable, every call raises.  Loading the library does not touch the GPU.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+import numpy as np
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+SO_PATH = os.path.join(_PKG, "libnkvmerkle.so")
+
+NKV_OK = 0
+NKV_ERR_EMPTY = 1
+NKV_ERR_INVALID = 2
+NKV_ERR_DEVICE = 3
+NKV_ERR_NOMEM = 4
+NKV_ERR_IO = 5
+
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+_vp = ctypes.c_void_p
+_u64 = ctypes.c_uint64
+_int = ctypes.c_int
+
+# name -> (restype, argtypes); every symbol include/nkv_merkle.h declares
+SIGNATURES = {
+    "nkv_strerror": (ctypes.c_char_p, [_int]),
+    "nkv_device_count": (_int, [ctypes.POINTER(_int)]),
+    "nkv_ctx_create": (_int, [_int, ctypes.POINTER(_vp)]),
+    "nkv_ctx_destroy": (None, [_vp]),
+    "nkv_ctx_set_stream": (_int, [_vp, _vp]),
+    "nkv_ctx_use_own_stream": (_int, [_vp]),
+    "nkv_ctx_sync": (_int, [_vp]),
+    "nkv_ctx_set_timing": (_int, [_vp, _int]),
+    "nkv_ctx_last_timing": (_int, [_vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
+    "nkv_ctx_timing_summary": (_int, [_vp, ctypes.POINTER(_int), ctypes.POINTER(ctypes.c_float),
+                                      ctypes.POINTER(ctypes.c_float)]),
+    "nkv_num_levels": (_int, [_u64]),
+    "nkv_level_count": (_u64, [_u64, _int]),
+    "nkv_level_start": (_u64, [_u64, _int]),
+    "nkv_total_nodes": (_u64, [_u64]),
+    "nkv_bfs_size": (_u64, [_u64]),
+    "nkv_host_alloc": (_int, [_vp, _u64, ctypes.POINTER(_vp)]),
+    "nkv_host_free": (_int, [_vp, _vp]),
+    "nkv_leaf_hash": (_int, [_vp, _u8p, _u64p, _u64p, _u64, _u8p]),
+    "nkv_tree_build": (_int, [_vp, _u8p, _u64, _u8p, _u8p, _u8p]),
+    "nkv_tree_from_values": (_int, [_vp, _u8p, _u64p, _u64p, _u64, _u8p, _u8p, _u8p]),
+    "nkv_generic_bfs_size": (_u64, [_u64p, _u64]),
+    "nkv_tree_generic": (_int, [_vp, _u8p, _u64p, _u64p, _u64, _u8p, _u8p, _u8p]),
+    "nkv_tree_from_records": (_int, [_vp, _u8p, _u64, _u64p, _u64, _u8p, _u8p, _u8p]),
+    "nkv_write_file": (_int, [ctypes.c_char_p, _u8p, _u64]),
+    "nkv_leaf_hash_dev": (_int, [_vp, _vp, _vp, _vp, _u64, _vp]),
+    "nkv_leaf_hash_strided_dev": (_int, [_vp, _vp, _u64, _u64, _u64, _vp]),
+    "nkv_tree_reduce_dev": (_int, [_vp, _vp, _u64]),
+    "nkv_tree_from_values_dev": (_int, [_vp, _vp, _vp, _vp, _u64, _vp]),
+    "nkv_tree_from_strided_dev": (_int, [_vp, _vp, _u64, _u64, _u64, _vp]),
+    "nkv_bfs_image_dev": (_int, [_vp, _vp, _u64, _vp]),
+    "nkv_record_offsets_dev": (_int, [_vp, _vp, _u64, _vp]),
+    "nkv_locate_values_dev": (_int, [_vp, _vp, _u64, _vp, _u64, _vp, _vp]),
+    "nkv_fill_splitmix64_dev": (_int, [_vp, _vp, _u64, _u64]),
+}
+
+_lib = None
+
+
+class NkvError(RuntimeError):
+    def __init__(self, code: int, what: str = ""):
+        self.code = code
+        msg = lib().nkv_strerror(code).decode()
+        super().__init__(f"{what}: {msg}" if what else msg)
+
+
+def lib():
+    """Load libnkvmerkle.so; raise loudly if it has not been built."""
+    global _lib
+    if _lib is None:
+        # One HIP runtime per process: torch wheels bundle their own
+        # libamdhip64.so.7.  Importing torch first makes our DT_NEEDED
+        # libamdhip64.so.7 bind to that already-loaded copy (same SONAME), so
+        # device pointers and streams are shared with torch.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
+        if not os.path.exists(SO_PATH):
+            raise ImportError(
+                f"{SO_PATH} is missing: build the HIP extension first "
+                "(python -c 'import __graft_entry__ as g; g.build()')")
+        L = ctypes.CDLL(SO_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != NKV_OK:
+        raise NkvError(rc, what)
+
+
+def p8(a: Optional[np.ndarray]):
+    if a is None:
+        return None
+    assert a.dtype == np.uint8 and a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(_u8p)
+
+
+def p64(a: np.ndarray):
+    assert a.dtype == np.uint64 and a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(_u64p)
+
+
+def device_count() -> int:
+    c = _int(0)
+    rc = lib().nkv_device_count(ctypes.byref(c))
+    return c.value if rc == NKV_OK else 0
+
+
+class Context:
+    """One nkv_ctx: a device, a stream, device scratch and pinned staging."""
+
+    def __init__(self, device: int = 0):
+        h = _vp()
+        check(lib().nkv_ctx_create(device, ctypes.byref(h)), f"nkv_ctx_create(device={device})")
+        self.h = h
+        self.device = device
+
+    def close(self) -> None:
+        if getattr(self, "h", None):
+            lib().nkv_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def set_stream(self, stream_handle: Optional[int]) -> None:
+        check(lib().nkv_ctx_set_stream(self.h, stream_handle))
+
+    def sync(self) -> None:
+        check(lib().nkv_ctx_sync(self.h))
+
+    def set_timing(self, on: bool) -> None:
+        check(lib().nkv_ctx_set_timing(self.h, 1 if on else 0))
+
+    def timing_summary(self):
+        """(calls, leaf_ms_total, reduce_ms_total) since set_timing(True)."""
+        k, a, b = _int(), ctypes.c_float(), ctypes.c_float()
+        check(lib().nkv_ctx_timing_summary(self.h, ctypes.byref(k), ctypes.byref(a), ctypes.byref(b)))
+        return k.value, a.value, b.value
+
+    def last_timing(self):
+        a, b = ctypes.c_float(), ctypes.c_float()
+        check(lib().nkv_ctx_last_timing(self.h, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
+
+
+_default: dict = {}
+
+
+def default_context(device: int = 0) -> Context:
+    ctx = _default.get(device)
+    if ctx is None:
+        ctx = _default[device] = Context(device)
+    return ctx

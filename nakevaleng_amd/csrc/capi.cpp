@@ -1,0 +1,660 @@
+// capi.cpp -- host side of libnkvmerkle.so: contexts, staging, launches and
+// the C-ABI declared in include/nkv_merkle.h.
+//
+// There is deliberately no CPU compute path here: every digest is produced by
+// the gfx950 kernels in kernels.hip.  A missing/unusable device is reported as
+// NKV_ERR_DEVICE.
+#include <fcntl.h>
+#include <hip/hip_runtime.h>
+#include <string.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "internal.hpp"
+#include "nkv_merkle.h"
+
+using namespace nkv;
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// tree shape (merkletree.go:31-64): n_0 = n, n_{L+1} = ceil(n_L / 2), until a
+// level of one node that is not the leaf level.
+
+int levels_of(uint64_t n) {
+    if (n == 0) return 0;
+    int lv = 1;
+    uint64_t c = n;
+    do {
+        c = (c + 1) / 2;
+        ++lv;
+    } while (c > 1);
+    return lv;
+}
+
+uint64_t count_of(uint64_t n, int L) { return L == 0 ? n : ((n - 1) >> L) + 1; }
+
+uint64_t start_of(uint64_t n, int L) {
+    uint64_t s = 0;
+    for (int j = 0; j < L; ++j) s += count_of(n, j);
+    return s;
+}
+
+uint64_t total_of(uint64_t n) {
+    const int lv = levels_of(n);
+    uint64_t s = 0;
+    for (int j = 0; j < lv; ++j) s += count_of(n, j);
+    return s;
+}
+
+// Image layout (merkletree.go:67-92) of levels given bottom-up counts[0..nlev)
+// of 20-byte nodes stored level-major from node index 0: top level first, 21
+// bytes per node, one 0x01 pad byte after every odd level below the top.
+BfsLayout layout_of(const std::vector<uint64_t>& counts, uint64_t img_base = 0) {
+    BfsLayout lay{};
+    const int nlev = int(counts.size());
+    lay.nlev = nlev;
+    std::vector<uint64_t> start(nlev);
+    uint64_t s = 0;
+    for (int L = 0; L < nlev; ++L) {
+        start[L] = s;
+        s += counts[L];
+    }
+    uint64_t p = img_base;
+    for (int i = 0; i < nlev; ++i) {  // image order: top first
+        const int L = nlev - 1 - i;
+        lay.img_start[i] = p;
+        lay.node_start[i] = start[L];
+        lay.count[i] = counts[L];
+        p += 21 * counts[L];
+        if (L < nlev - 1 && (counts[L] & 1)) p += 1;
+    }
+    lay.total = p;
+    return lay;
+}
+
+std::vector<uint64_t> counts_of(uint64_t n) {
+    std::vector<uint64_t> c(levels_of(n));
+    for (size_t L = 0; L < c.size(); ++L) c[L] = count_of(n, int(L));
+    return c;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// context
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+};
+
+struct nkv_ctx {
+    int device = 0;
+    hipStream_t own = nullptr;
+    hipStream_t stream = nullptr;
+    bool timing = false;
+    bool timed = false;
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    // per-call event triples (leaf start, leaf end / reduce start, reduce end)
+    std::vector<hipEvent_t> ring;
+    size_t ring_used = 0;
+    DevBuf d_data, d_off, d_len, d_nodes, d_img, d_tmp, d_err, d_aux;
+    void* h_stage = nullptr;
+    size_t h_cap = 0;
+};
+
+namespace {
+
+int st(hipError_t e) {
+    if (e == hipSuccess) return NKV_OK;
+    if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) return NKV_ERR_NOMEM;
+    return NKV_ERR_DEVICE;
+}
+
+#define TRY(x)                         \
+    do {                               \
+        int _rc = (x);                 \
+        if (_rc != NKV_OK) return _rc; \
+    } while (0)
+#define HIPTRY(x) TRY(st(x))
+
+int bind(nkv_ctx* c) {
+    if (!c) return NKV_ERR_INVALID;
+    return st(hipSetDevice(c->device));
+}
+
+int grow(DevBuf& b, size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    if (b.cap >= bytes) return NKV_OK;
+    const size_t old = b.cap;
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.cap = 0;
+    size_t want = std::max(bytes, old + old / 2);
+    if (hipMalloc(&b.p, want) != hipSuccess) {
+        (void)hipGetLastError();
+        if (hipMalloc(&b.p, bytes) != hipSuccess) {
+            (void)hipGetLastError();
+            b.p = nullptr;
+            return NKV_ERR_NOMEM;
+        }
+        want = bytes;
+    }
+    b.cap = want;
+    return NKV_OK;
+}
+
+int grow_host(nkv_ctx* c, size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    if (c->h_cap >= bytes) return NKV_OK;
+    if (c->h_stage) (void)hipHostFree(c->h_stage);
+    c->h_stage = nullptr;
+    c->h_cap = 0;
+    if (hipHostMalloc(&c->h_stage, bytes, hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        c->h_stage = nullptr;
+        return NKV_ERR_NOMEM;
+    }
+    c->h_cap = bytes;
+    return NKV_OK;
+}
+
+uint64_t align16(uint64_t x) { return (x + 15) & ~uint64_t(15); }
+
+// Pack n host values into the pinned stage at 16-byte aligned offsets
+// (lib-owned copy: no caller pointer is kept) and upload them with their
+// packed offsets/lengths to d_data / d_off / d_len.
+int stage_values(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint64_t* len,
+                 uint64_t n) {
+    uint64_t total = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        if (len[i] > (uint64_t(1) << 62) || total > (uint64_t(1) << 62)) return NKV_ERR_INVALID;
+        total += align16(len[i]);
+    }
+    const uint64_t meta = 16 * n;
+    TRY(grow_host(c, total + meta));
+    TRY(grow(c->d_data, total));
+    TRY(grow(c->d_off, 8 * n));
+    TRY(grow(c->d_len, 8 * n));
+    uint8_t* h = static_cast<uint8_t*>(c->h_stage);
+    uint64_t* hoff = reinterpret_cast<uint64_t*>(h + total);
+    uint64_t* hlen = hoff + n;
+    uint64_t p = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        if (len[i]) memcpy(h + p, base + off[i], len[i]);
+        hoff[i] = p;
+        hlen[i] = len[i];
+        p += align16(len[i]);
+    }
+    HIPTRY(hipMemcpyAsync(c->d_data.p, h, total, hipMemcpyHostToDevice, c->stream));
+    HIPTRY(hipMemcpyAsync(c->d_off.p, hoff, 8 * n, hipMemcpyHostToDevice, c->stream));
+    HIPTRY(hipMemcpyAsync(c->d_len.p, hlen, 8 * n, hipMemcpyHostToDevice, c->stream));
+    return NKV_OK;
+}
+
+int finish_tree(nkv_ctx* c, uint8_t* nodes, uint64_t n, uint8_t* root20, uint8_t* nodes_out,
+                uint8_t* img_out) {
+    const uint64_t tot = total_of(n);
+    if (img_out) {
+        BfsLayout lay = layout_of(counts_of(n));
+        TRY(grow(c->d_img, lay.total));
+        HIPTRY(launch_bfs_image(nodes, lay, static_cast<uint8_t*>(c->d_img.p), c->stream));
+        HIPTRY(hipMemcpyAsync(img_out, c->d_img.p, lay.total, hipMemcpyDeviceToHost, c->stream));
+    }
+    if (nodes_out)
+        HIPTRY(hipMemcpyAsync(nodes_out, nodes, 20 * tot, hipMemcpyDeviceToHost, c->stream));
+    if (root20)
+        HIPTRY(hipMemcpyAsync(root20, nodes + 20 * (tot - 1), 20, hipMemcpyDeviceToHost, c->stream));
+    HIPTRY(hipStreamSynchronize(c->stream));
+    return NKV_OK;
+}
+
+// Events around the leaf kernel and the reduce of one tree call; kept per
+// call (no host sync) so a timed loop can be summarised afterwards.
+int mark(nkv_ctx* c, int which) {
+    if (!c->timing) return NKV_OK;
+    if (which == 0) {
+        if (c->ring_used + 3 > c->ring.size()) {
+            for (int i = 0; i < 3; ++i) {
+                hipEvent_t e;
+                HIPTRY(hipEventCreate(&e));
+                c->ring.push_back(e);
+            }
+        }
+        c->ring_used += 3;
+    }
+    hipEvent_t e = c->ring[c->ring_used - 3 + which];
+    HIPTRY(hipEventRecord(e, c->stream));
+    HIPTRY(hipEventRecord(c->ev[which], c->stream));
+    if (which == 2) c->timed = true;
+    return NKV_OK;
+}
+
+int tree_from_device_values(nkv_ctx* c, const uint8_t* base, const uint64_t* off,
+                            const uint64_t* len, uint64_t n, bool aligned, uint8_t* nodes) {
+    const int top = levels_of(n) - 1;
+    TRY(mark(c, 0));
+    HIPTRY(launch_leaf_offsets(base, off, len, nullptr, n, top, true, aligned, nodes, c->stream));
+    TRY(mark(c, 1));
+    HIPTRY(launch_reduce(nodes, n, std::min(top, kFuseLevels), top, c->stream));
+    return mark(c, 2);
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* nkv_strerror(int s) {
+    switch (s) {
+        case NKV_OK: return "ok";
+        case NKV_ERR_EMPTY: return "cannot build Merkle Tree from 0 nodes";
+        case NKV_ERR_INVALID: return "invalid argument";
+        case NKV_ERR_DEVICE: return "HIP device error";
+        case NKV_ERR_NOMEM: return "out of memory";
+        case NKV_ERR_IO: return "file I/O error";
+        default: return "unknown error";
+    }
+}
+
+int nkv_device_count(int* count) {
+    if (!count) return NKV_ERR_INVALID;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        *count = 0;
+        return NKV_ERR_DEVICE;
+    }
+    *count = n;
+    return NKV_OK;
+}
+
+int nkv_ctx_create(int device, nkv_ctx** out) {
+    if (!out) return NKV_ERR_INVALID;
+    *out = nullptr;
+    int cnt = 0;
+    if (nkv_device_count(&cnt) != NKV_OK || device < 0 || device >= cnt) return NKV_ERR_DEVICE;
+    nkv_ctx* c = new nkv_ctx();
+    c->device = device;
+    int rc = st(hipSetDevice(device));
+    if (rc == NKV_OK) rc = st(hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking));
+    for (int i = 0; i < 3 && rc == NKV_OK; ++i) rc = st(hipEventCreate(&c->ev[i]));
+    if (rc != NKV_OK) {
+        nkv_ctx_destroy(c);
+        return rc;
+    }
+    c->stream = c->own;
+    *out = c;
+    return NKV_OK;
+}
+
+void nkv_ctx_destroy(nkv_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (DevBuf* b : {&c->d_data, &c->d_off, &c->d_len, &c->d_nodes, &c->d_img, &c->d_tmp,
+                      &c->d_err, &c->d_aux})
+        if (b->p) (void)hipFree(b->p);
+    if (c->h_stage) (void)hipHostFree(c->h_stage);
+    for (hipEvent_t e : c->ev)
+        if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->ring) (void)hipEventDestroy(e);
+    if (c->own) (void)hipStreamDestroy(c->own);
+    delete c;
+}
+
+int nkv_ctx_set_stream(nkv_ctx* c, void* s) {
+    TRY(bind(c));
+    c->stream = static_cast<hipStream_t>(s);  // NULL = the device's null stream
+    return NKV_OK;
+}
+
+int nkv_ctx_use_own_stream(nkv_ctx* c) {
+    TRY(bind(c));
+    c->stream = c->own;
+    return NKV_OK;
+}
+
+int nkv_ctx_sync(nkv_ctx* c) {
+    TRY(bind(c));
+    return st(hipStreamSynchronize(c->stream));
+}
+
+int nkv_ctx_set_timing(nkv_ctx* c, int enable) {
+    TRY(bind(c));
+    c->timing = enable != 0;
+    c->timed = false;
+    c->ring_used = 0;
+    return NKV_OK;
+}
+
+int nkv_ctx_timing_summary(nkv_ctx* c, int* calls, float* leaf_ms_total, float* reduce_ms_total) {
+    TRY(bind(c));
+    if (!calls || !leaf_ms_total || !reduce_ms_total) return NKV_ERR_INVALID;
+    const size_t k = c->ring_used / 3;
+    if (k) HIPTRY(hipEventSynchronize(c->ring[c->ring_used - 1]));
+    double a = 0, b = 0;
+    for (size_t i = 0; i < k; ++i) {
+        float x = 0.f, y = 0.f;
+        HIPTRY(hipEventElapsedTime(&x, c->ring[3 * i], c->ring[3 * i + 1]));
+        HIPTRY(hipEventElapsedTime(&y, c->ring[3 * i + 1], c->ring[3 * i + 2]));
+        a += x;
+        b += y;
+    }
+    *calls = int(k);
+    *leaf_ms_total = float(a);
+    *reduce_ms_total = float(b);
+    return NKV_OK;
+}
+
+int nkv_ctx_last_timing(nkv_ctx* c, float* leaf_ms, float* reduce_ms) {
+    TRY(bind(c));
+    if (!c->timed) return NKV_ERR_INVALID;
+    HIPTRY(hipEventSynchronize(c->ev[2]));
+    float a = 0.f, b = 0.f;
+    HIPTRY(hipEventElapsedTime(&a, c->ev[0], c->ev[1]));
+    HIPTRY(hipEventElapsedTime(&b, c->ev[1], c->ev[2]));
+    if (leaf_ms) *leaf_ms = a;
+    if (reduce_ms) *reduce_ms = b;
+    return NKV_OK;
+}
+
+// ---- shape ----
+int nkv_num_levels(uint64_t n) { return levels_of(n); }
+uint64_t nkv_level_count(uint64_t n, int L) {
+    return (n == 0 || L < 0 || L >= levels_of(n)) ? 0 : count_of(n, L);
+}
+uint64_t nkv_level_start(uint64_t n, int L) {
+    return (n == 0 || L < 0 || L >= levels_of(n)) ? 0 : start_of(n, L);
+}
+uint64_t nkv_total_nodes(uint64_t n) { return total_of(n); }
+uint64_t nkv_bfs_size(uint64_t n) { return n == 0 ? 0 : layout_of(counts_of(n)).total; }
+
+// ---- pinned arena ----
+int nkv_host_alloc(nkv_ctx* c, uint64_t bytes, void** out) {
+    if (!out) return NKV_ERR_INVALID;
+    TRY(bind(c));
+    if (hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        *out = nullptr;
+        return NKV_ERR_NOMEM;
+    }
+    return NKV_OK;
+}
+
+int nkv_host_free(nkv_ctx* c, void* p) {
+    TRY(bind(c));
+    return p ? st(hipHostFree(p)) : NKV_OK;
+}
+
+// ---- host-buffer API ----
+int nkv_leaf_hash(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint64_t* len,
+                  uint64_t n, uint8_t* out20) {
+    TRY(bind(c));
+    if (n == 0) return NKV_OK;
+    if (!base || !off || !len || !out20) return NKV_ERR_INVALID;
+    TRY(stage_values(c, base, off, len, n));
+    TRY(grow(c->d_nodes, 20 * n));
+    uint8_t* nodes = static_cast<uint8_t*>(c->d_nodes.p);
+    HIPTRY(launch_leaf_offsets(static_cast<const uint8_t*>(c->d_data.p),
+                               static_cast<const uint64_t*>(c->d_off.p),
+                               static_cast<const uint64_t*>(c->d_len.p), nullptr, n, 0, false, true,
+                               nodes, c->stream));
+    HIPTRY(hipMemcpyAsync(out20, nodes, 20 * n, hipMemcpyDeviceToHost, c->stream));
+    return st(hipStreamSynchronize(c->stream));
+}
+
+int nkv_tree_build(nkv_ctx* c, const uint8_t* leaf20, uint64_t n, uint8_t* root20,
+                   uint8_t* nodes_out, uint8_t* img_out) {
+    TRY(bind(c));
+    if (n == 0) return NKV_ERR_EMPTY;
+    if (!leaf20) return NKV_ERR_INVALID;
+    TRY(grow(c->d_nodes, 20 * total_of(n)));
+    uint8_t* nodes = static_cast<uint8_t*>(c->d_nodes.p);
+    TRY(grow_host(c, 20 * n));
+    memcpy(c->h_stage, leaf20, 20 * n);
+    HIPTRY(hipMemcpyAsync(nodes, c->h_stage, 20 * n, hipMemcpyHostToDevice, c->stream));
+    HIPTRY(launch_reduce(nodes, n, 0, levels_of(n) - 1, c->stream));
+    return finish_tree(c, nodes, n, root20, nodes_out, img_out);
+}
+
+int nkv_tree_from_values(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint64_t* len,
+                         uint64_t n, uint8_t* root20, uint8_t* nodes_out, uint8_t* img_out) {
+    TRY(bind(c));
+    if (n == 0) return NKV_ERR_EMPTY;
+    if (!base || !off || !len) return NKV_ERR_INVALID;
+    TRY(stage_values(c, base, off, len, n));
+    TRY(grow(c->d_nodes, 20 * total_of(n)));
+    uint8_t* nodes = static_cast<uint8_t*>(c->d_nodes.p);
+    TRY(tree_from_device_values(c, static_cast<const uint8_t*>(c->d_data.p),
+                                static_cast<const uint64_t*>(c->d_off.p),
+                                static_cast<const uint64_t*>(c->d_len.p), n, true, nodes));
+    return finish_tree(c, nodes, n, root20, nodes_out, img_out);
+}
+
+uint64_t nkv_generic_bfs_size(const uint64_t* len, uint64_t n) {
+    if (n == 0 || !len) return 0;
+    // levels 1..top are 20-byte nodes; level 0 is the raw leaves
+    uint64_t s = nkv_bfs_size(n) - 21 * n;
+    for (uint64_t i = 0; i < n; ++i) s += len[i] ? 1 + len[i] : 1;
+    return s;
+}
+
+int nkv_tree_generic(nkv_ctx* c, const uint8_t* data, const uint64_t* off, const uint64_t* len,
+                     uint64_t n, uint8_t* root20, uint8_t* upper_out, uint8_t* img_out) {
+    TRY(bind(c));
+    if (n == 0) return NKV_ERR_EMPTY;
+    if (!data || !off || !len) return NKV_ERR_INVALID;
+    // Level 1 node i = SHA-1(leaf[2i].Data || leaf[2i+1].Data) (merkletree.go:44-46;
+    // the pad of an odd level contributes no bytes).  Stage each parent's
+    // message contiguously and hash the messages with the leaf kernel; the
+    // rest of the tree is the 20-byte reduce over the n1 level-1 nodes.
+    const uint64_t n1 = (n + 1) / 2;
+    std::vector<uint64_t> moff(n1), mlen(n1);
+    std::vector<uint8_t> tmp;
+    uint64_t total = 0;
+    for (uint64_t i = 0; i < n1; ++i) {
+        mlen[i] = len[2 * i] + (2 * i + 1 < n ? len[2 * i + 1] : 0);
+        total += mlen[i];
+    }
+    tmp.resize(total ? total : 1);
+    uint64_t p = 0;
+    for (uint64_t i = 0; i < n1; ++i) {
+        moff[i] = p;
+        memcpy(tmp.data() + p, data + off[2 * i], len[2 * i]);
+        p += len[2 * i];
+        if (2 * i + 1 < n) {
+            memcpy(tmp.data() + p, data + off[2 * i + 1], len[2 * i + 1]);
+            p += len[2 * i + 1];
+        }
+    }
+    TRY(stage_values(c, tmp.data(), moff.data(), mlen.data(), n1));
+    const uint64_t up_total = n1 == 1 ? 1 : total_of(n1);
+    TRY(grow(c->d_nodes, 20 * up_total));
+    uint8_t* up = static_cast<uint8_t*>(c->d_nodes.p);
+    HIPTRY(launch_leaf_offsets(static_cast<const uint8_t*>(c->d_data.p),
+                               static_cast<const uint64_t*>(c->d_off.p),
+                               static_cast<const uint64_t*>(c->d_len.p), nullptr, n1, 0, false,
+                               true, up, c->stream));
+    if (n1 > 1) HIPTRY(launch_reduce(up, n1, 0, levels_of(n1) - 1, c->stream));
+    if (upper_out)
+        HIPTRY(hipMemcpyAsync(upper_out, up, 20 * up_total, hipMemcpyDeviceToHost, c->stream));
+    if (root20)
+        HIPTRY(hipMemcpyAsync(root20, up + 20 * (up_total - 1), 20, hipMemcpyDeviceToHost,
+                              c->stream));
+    uint64_t upper_img = 0;
+    if (img_out) {
+        // levels top..1 from the device, level 0 (raw leaf Data) appended here
+        std::vector<uint64_t> cnt = n1 == 1 ? std::vector<uint64_t>{1} : counts_of(n1);
+        BfsLayout lay = layout_of(cnt);
+        // the bottom of this sub-image is level 1 of the whole tree, which is
+        // never the top when n1 > 1; its pad is already handled by layout_of
+        upper_img = lay.total;
+        TRY(grow(c->d_img, lay.total));
+        HIPTRY(launch_bfs_image(up, lay, static_cast<uint8_t*>(c->d_img.p), c->stream));
+        HIPTRY(hipMemcpyAsync(img_out, c->d_img.p, lay.total, hipMemcpyDeviceToHost, c->stream));
+    }
+    HIPTRY(hipStreamSynchronize(c->stream));
+    if (img_out) {
+        uint8_t* q = img_out + upper_img;
+        for (uint64_t i = 0; i < n; ++i) {
+            if (len[i] == 0) {
+                *q++ = NKV_MERKLE_NODE_EMPTY;
+            } else {
+                *q++ = 0;
+                memcpy(q, data + off[i], len[i]);
+                q += len[i];
+            }
+        }
+        if (n & 1) *q++ = NKV_MERKLE_NODE_EMPTY;
+    }
+    return NKV_OK;
+}
+
+int nkv_tree_from_records(nkv_ctx* c, const uint8_t* stream, uint64_t stream_len,
+                          const uint64_t* rec_size, uint64_t n, uint8_t* root20,
+                          uint8_t* nodes_out, uint8_t* img_out) {
+    TRY(bind(c));
+    if (n == 0) return NKV_ERR_EMPTY;
+    if (!stream || !rec_size) return NKV_ERR_INVALID;
+    uint64_t sum = 0;
+    for (uint64_t i = 0; i < n; ++i) sum += rec_size[i];
+    if (sum > stream_len) return NKV_ERR_INVALID;
+    TRY(grow_host(c, stream_len + 8 * n));
+    TRY(grow(c->d_data, stream_len));
+    TRY(grow(c->d_aux, 8 * n));
+    uint8_t* h = static_cast<uint8_t*>(c->h_stage);
+    memcpy(h, stream, stream_len);
+    memcpy(h + stream_len, rec_size, 8 * n);
+    HIPTRY(hipMemcpyAsync(c->d_data.p, h, stream_len, hipMemcpyHostToDevice, c->stream));
+    HIPTRY(hipMemcpyAsync(c->d_aux.p, h + stream_len, 8 * n, hipMemcpyHostToDevice, c->stream));
+    TRY(grow(c->d_off, 8 * n));
+    TRY(grow(c->d_len, 8 * n));
+    // d_len doubles as the record-offset scratch before it receives lengths
+    uint64_t* rec_off = static_cast<uint64_t*>(c->d_len.p);
+    TRY(nkv_record_offsets_dev(c, static_cast<const uint64_t*>(c->d_aux.p), n, rec_off));
+    // values land in d_off (offsets) and d_aux (lengths; RecSize no longer needed)
+    uint64_t* voff = static_cast<uint64_t*>(c->d_off.p);
+    uint64_t* vlen = static_cast<uint64_t*>(c->d_aux.p);
+    TRY(nkv_locate_values_dev(c, c->d_data.p, stream_len, rec_off, n, voff, vlen));
+    TRY(grow(c->d_nodes, 20 * total_of(n)));
+    uint8_t* nodes = static_cast<uint8_t*>(c->d_nodes.p);
+    TRY(tree_from_device_values(c, static_cast<const uint8_t*>(c->d_data.p), voff, vlen, n, false,
+                                nodes));
+    return finish_tree(c, nodes, n, root20, nodes_out, img_out);
+}
+
+int nkv_write_file(const char* fname, const uint8_t* data, uint64_t len) {
+    if (!fname || (!data && len)) return NKV_ERR_INVALID;
+    int fd = open(fname, O_WRONLY | O_CREAT, 0666);  // no O_TRUNC: merkletree.go:68
+    if (fd < 0) return NKV_ERR_IO;
+    uint64_t done = 0;
+    while (done < len) {
+        ssize_t w = write(fd, data + done, size_t(std::min<uint64_t>(len - done, 1ull << 30)));
+        if (w <= 0) {
+            close(fd);
+            return NKV_ERR_IO;
+        }
+        done += uint64_t(w);
+    }
+    return close(fd) == 0 ? NKV_OK : NKV_ERR_IO;
+}
+
+// ---- device-resident API ----
+int nkv_leaf_hash_dev(nkv_ctx* c, const void* d_base, const uint64_t* d_off,
+                      const uint64_t* d_len, uint64_t n, void* d_nodes) {
+    TRY(bind(c));
+    if (n == 0) return NKV_OK;
+    if (!d_base || !d_off || !d_len || !d_nodes) return NKV_ERR_INVALID;
+    return st(launch_leaf_offsets(static_cast<const uint8_t*>(d_base), d_off, d_len, nullptr, n, 0,
+                                  false, false, static_cast<uint8_t*>(d_nodes), c->stream));
+}
+
+int nkv_leaf_hash_strided_dev(nkv_ctx* c, const void* d_base, uint64_t stride, uint64_t len,
+                              uint64_t n, void* d_nodes) {
+    TRY(bind(c));
+    if (n == 0) return NKV_OK;
+    if (!d_base || !d_nodes) return NKV_ERR_INVALID;
+    return st(launch_leaf_strided(static_cast<const uint8_t*>(d_base), stride, len, n, 0, false,
+                                  static_cast<uint8_t*>(d_nodes), c->stream));
+}
+
+int nkv_tree_reduce_dev(nkv_ctx* c, void* d_nodes, uint64_t n) {
+    TRY(bind(c));
+    if (n == 0) return NKV_ERR_EMPTY;
+    if (!d_nodes) return NKV_ERR_INVALID;
+    return st(launch_reduce(static_cast<uint8_t*>(d_nodes), n, 0, levels_of(n) - 1, c->stream));
+}
+
+int nkv_tree_from_values_dev(nkv_ctx* c, const void* d_base, const uint64_t* d_off,
+                             const uint64_t* d_len, uint64_t n, void* d_nodes) {
+    TRY(bind(c));
+    if (n == 0) return NKV_ERR_EMPTY;
+    if (!d_base || !d_off || !d_len || !d_nodes) return NKV_ERR_INVALID;
+    return tree_from_device_values(c, static_cast<const uint8_t*>(d_base), d_off, d_len, n, false,
+                                   static_cast<uint8_t*>(d_nodes));
+}
+
+int nkv_tree_from_strided_dev(nkv_ctx* c, const void* d_base, uint64_t stride, uint64_t len,
+                              uint64_t n, void* d_nodes) {
+    TRY(bind(c));
+    if (n == 0) return NKV_ERR_EMPTY;
+    if (!d_base || !d_nodes) return NKV_ERR_INVALID;
+    uint8_t* nodes = static_cast<uint8_t*>(d_nodes);
+    const int top = levels_of(n) - 1;
+    TRY(mark(c, 0));
+    HIPTRY(launch_leaf_strided(static_cast<const uint8_t*>(d_base), stride, len, n, top, true,
+                               nodes, c->stream));
+    TRY(mark(c, 1));
+    HIPTRY(launch_reduce(nodes, n, std::min(top, kFuseLevels), top, c->stream));
+    return mark(c, 2);
+}
+
+int nkv_bfs_image_dev(nkv_ctx* c, const void* d_nodes, uint64_t n, void* d_img) {
+    TRY(bind(c));
+    if (n == 0) return NKV_ERR_EMPTY;
+    if (!d_nodes || !d_img) return NKV_ERR_INVALID;
+    BfsLayout lay = layout_of(counts_of(n));
+    return st(launch_bfs_image(static_cast<const uint8_t*>(d_nodes), lay,
+                               static_cast<uint8_t*>(d_img), c->stream));
+}
+
+int nkv_record_offsets_dev(nkv_ctx* c, const uint64_t* d_rec_size, uint64_t n,
+                           uint64_t* d_rec_off) {
+    TRY(bind(c));
+    if (n == 0) return NKV_OK;
+    if (!d_rec_size || !d_rec_off || n > 0x7fffffffull) return NKV_ERR_INVALID;
+    size_t tb = 0;
+    HIPTRY(scan_exclusive_u64(d_rec_size, d_rec_off, n, nullptr, &tb, c->stream));
+    TRY(grow(c->d_tmp, tb));
+    return st(scan_exclusive_u64(d_rec_size, d_rec_off, n, c->d_tmp.p, &tb, c->stream));
+}
+
+int nkv_locate_values_dev(nkv_ctx* c, const void* d_stream, uint64_t stream_len,
+                          const uint64_t* d_rec_off, uint64_t n, uint64_t* d_voff,
+                          uint64_t* d_vlen) {
+    TRY(bind(c));
+    if (n == 0) return NKV_OK;
+    if (!d_stream || !d_rec_off || !d_voff || !d_vlen) return NKV_ERR_INVALID;
+    TRY(grow(c->d_err, 4));
+    unsigned int* err = static_cast<unsigned int*>(c->d_err.p);
+    HIPTRY(hipMemsetAsync(err, 0, 4, c->stream));
+    HIPTRY(launch_locate(static_cast<const uint8_t*>(d_stream), stream_len, d_rec_off, n, d_voff,
+                         d_vlen, err, c->stream));
+    unsigned int h = 0;
+    HIPTRY(hipMemcpyAsync(&h, err, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPTRY(hipStreamSynchronize(c->stream));
+    return h ? NKV_ERR_INVALID : NKV_OK;
+}
+
+int nkv_fill_splitmix64_dev(nkv_ctx* c, void* d_buf, uint64_t nbytes, uint64_t seed) {
+    TRY(bind(c));
+    if (nbytes == 0) return NKV_OK;
+    if (!d_buf) return NKV_ERR_INVALID;
+    return st(launch_fill(static_cast<uint8_t*>(d_buf), nbytes, seed, c->stream));
+}
+
+}  // extern "C"

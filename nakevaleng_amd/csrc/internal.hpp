@@ -1,0 +1,42 @@
+// internal.hpp -- launcher declarations shared by kernels.hip and capi.cpp.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace nkv {
+
+constexpr int kBlock = 256;       // threads per workgroup = leaves per K1 block
+constexpr int kFuseLevels = 8;    // log2(kBlock): levels one workgroup reduces in LDS
+constexpr int kMaxLevels = 64;
+#ifndef NKV_LEAF_WAVES
+#define NKV_LEAF_WAVES 8
+#endif
+constexpr int kLeafWavesPerSimd = NKV_LEAF_WAVES;  // 8 waves/SIMD <=> <= 64 VGPRs
+
+// BFS image layout in image order (index 0 = top level).
+struct BfsLayout {
+    int nlev;
+    uint64_t total;
+    uint64_t img_start[kMaxLevels];   // first image byte of the level
+    uint64_t node_start[kMaxLevels];  // first node of the level in the nodes buffer
+    uint64_t count[kMaxLevels];       // real nodes in the level
+};
+
+hipError_t launch_leaf_strided(const uint8_t* base, uint64_t stride, uint64_t L, uint64_t n,
+                               int top, bool fuse, uint8_t* nodes, hipStream_t s);
+hipError_t launch_leaf_offsets(const uint8_t* base, const uint64_t* off, const uint64_t* len,
+                               const uint32_t* perm, uint64_t n, int top, bool fuse, bool aligned,
+                               uint8_t* nodes, hipStream_t s);
+hipError_t launch_reduce(uint8_t* nodes, uint64_t n, int from_level, int top, hipStream_t s);
+hipError_t launch_hash_messages(const uint8_t* base, const uint64_t* off, const uint64_t* len,
+                                uint64_t n, uint8_t* out, hipStream_t s);
+hipError_t launch_bfs_image(const uint8_t* nodes, const BfsLayout& lay, uint8_t* img,
+                            hipStream_t s);
+hipError_t launch_locate(const uint8_t* stream, uint64_t stream_len, const uint64_t* rec_off,
+                         uint64_t n, uint64_t* voff, uint64_t* vlen, unsigned int* err,
+                         hipStream_t s);
+hipError_t scan_exclusive_u64(const uint64_t* in, uint64_t* out, uint64_t n, void* tmp,
+                              size_t* tmp_bytes, hipStream_t s);
+hipError_t launch_fill(uint8_t* buf, uint64_t nbytes, uint64_t seed, hipStream_t s);
+
+}  // namespace nkv

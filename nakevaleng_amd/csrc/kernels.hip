@@ -1,0 +1,576 @@
+// kernels.hip -- gfx950 kernels of the Merkle step of SSTable build.
+//
+//   K1  k_leaf        NewLeaf over many values (merklenode.go:27-34), one lane
+//                     per leaf, 64 leaves per wavefront; optionally fused with
+//                     the first 8 tree levels of its 256-leaf block (K2a).
+//   K2  k_reduce      build() levels (merkletree.go:31-64): a 256-node slab of
+//                     one level reduced up to 8 levels in LDS per launch.
+//   K3  k_bfs_image   Serialize() byte image (merkletree.go:67-92,
+//                     merklenode.go:37-63) at closed-form offsets.
+//   K0  k_locate      value offset/length of each serialized core/record
+//                     (record.go:191-199): value = rec + 30 + KeySize.
+//       k_fill        splitmix64 synthetic bytes (bench/test input only).
+//
+// Node storage ("nodes" buffer): every level, bottom-up, level-major; level L
+// holds ceil(n / 2^L) 20-byte digests in Go byte order (big-endian words);
+// level 0 is the leaves, the last digest is the root.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+#include <stdint.h>
+
+#include "internal.hpp"
+#include "sha1_dev.hpp"
+
+namespace nkv {
+
+// ---------------------------------------------------------------------------
+// tree shape helpers (device side; host side mirrors them in capi.cpp)
+
+__device__ __forceinline__ uint64_t lvl_count(uint64_t n, int L) {
+    return L == 0 ? n : ((n - 1) >> L) + 1;  // ceil(n / 2^L), n >= 1
+}
+
+__device__ __forceinline__ uint64_t lvl_start(uint64_t n, int L) {
+    uint64_t s = 0;
+    for (int j = 0; j < L; ++j) s += lvl_count(n, j);
+    return s;
+}
+
+__device__ __forceinline__ void store_digest(uint8_t* nodes, uint64_t idx, const uint32_t h[5]) {
+    uint32_t* p = reinterpret_cast<uint32_t*>(nodes + 20ull * idx);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) p[k] = bswap32(h[k]);
+}
+
+__device__ __forceinline__ void load_digest(const uint8_t* nodes, uint64_t idx, uint32_t h[5]) {
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(nodes + 20ull * idx);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) h[k] = bswap32(p[k]);
+}
+
+// ---------------------------------------------------------------------------
+// Subtree reduce inside one 256-thread workgroup.
+//
+// lds[k][t] holds word k of the node at index lo + t of level j0 (t < 256).
+// Levels j0+1 .. jmax are computed; each level's nodes are written to the
+// global nodes buffer.  Node i of level j is SHA-1(c[2i] || c[2i+1]) when
+// 2i+1 < n_{j-1}, else SHA-1(c[2i]) (the empty pad, merkletree.go:32-34).
+__device__ __forceinline__ void subtree_reduce(uint32_t (*lds)[kBlock], uint64_t n, int j0, int jmax, uint64_t lo,
+                               uint8_t* nodes) {
+    const int tid = threadIdx.x;
+    uint64_t nprev = lvl_count(n, j0);
+    uint64_t start_cur = lvl_start(n, j0) + nprev;
+    uint64_t lo_prev = lo;
+    int span = kBlock;
+    for (int j = j0 + 1; j <= jmax; ++j) {
+        const uint64_t ncur = ((nprev - 1) >> 1) + 1;
+        const uint64_t lo_cur = lo_prev >> 1;
+        span >>= 1;
+        const bool act = tid < span && lo_cur + tid < ncur;
+        uint32_t out[5];
+        __syncthreads();
+        if (act) {
+            uint32_t l[5], r[5];
+            const bool lone = (2 * (lo_cur + tid) + 1) >= nprev;
+#pragma unroll
+            for (int k = 0; k < 5; ++k) {
+                l[k] = lds[k][2 * tid];
+                r[k] = lone ? 0u : lds[k][2 * tid + 1];
+            }
+            sha1_parent(l, r, lone, out);
+        }
+        __syncthreads();
+        if (act) {
+#pragma unroll
+            for (int k = 0; k < 5; ++k) lds[k][tid] = out[k];
+            store_digest(nodes, start_cur + lo_cur + tid, out);
+        }
+        nprev = ncur;
+        start_cur += ncur;
+        lo_prev = lo_cur;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K1: leaf SHA-1.
+//
+// Each lane hashes the value p[0 .. len).  Full 64-byte blocks are streamed
+// with a one-block register prefetch; the 1-2 padding blocks are built from
+// the remaining 0..63 bytes (FIPS 180-4 5.1.1).  A 16-byte aligned wave takes
+// 4 x global_load_dwordx4 per block; otherwise each lane reads the five
+// aligned 16-byte chunks that cover its 64 bytes and funnels them with
+// v_perm_b32 (never touching an aligned chunk that holds no value byte, so it
+// cannot step onto an unmapped page).
+
+__device__ __forceinline__ void be16_from_raw(const uint4 c[4], uint32_t w[16]) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        w[4 * q + 0] = bswap32(c[q].x);
+        w[4 * q + 1] = bswap32(c[q].y);
+        w[4 * q + 2] = bswap32(c[q].z);
+        w[4 * q + 3] = bswap32(c[q].w);
+    }
+}
+
+// d[0..19]: 20 little-endian dwords of the aligned 80-byte window; s = byte
+// shift 0..15 of the stream start inside it.  Produces 16 big-endian words.
+__device__ __forceinline__ void be16_funnel(const uint32_t d[20], uint32_t s, uint32_t w[16]) {
+    // Dword select by k = s >> 2 in two v_perm_b32 steps (a plain ?: on the
+    // array would be folded into a dynamically indexed private array).
+    const uint32_t k = s >> 2;
+    const uint32_t sel = be_sel(s & 3u);
+    const uint32_t sel1 = (k & 1u) ? 0x07060504u : 0x03020100u;
+    const uint32_t sel2 = (k & 2u) ? 0x07060504u : 0x03020100u;
+    uint32_t m1[19];
+#pragma unroll
+    for (int j = 0; j < 19; ++j) m1[j] = __builtin_amdgcn_perm(d[j + 1], d[j], sel1);
+    uint32_t m2[17];
+#pragma unroll
+    for (int j = 0; j < 17; ++j) m2[j] = __builtin_amdgcn_perm(m1[j + 2], m1[j], sel2);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) w[j] = be_word(m2[j + 1], m2[j], sel);
+}
+
+__device__ __forceinline__ void load_window(const uint8_t* p, uint32_t avail, uint32_t d[20]) {
+    // p: stream start; avail: value bytes available from p (>= 1 unless empty).
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    const uint4* q = reinterpret_cast<const uint4*>(a & ~uintptr_t(15));
+    const uint32_t s = uint32_t(a & 15);
+#pragma unroll
+    for (int c = 0; c < 5; ++c) {
+        uint4 v = make_uint4(0u, 0u, 0u, 0u);
+        if (avail > 0 && uint32_t(16 * c) < s + avail) v = q[c];
+        d[4 * c + 0] = v.x;
+        d[4 * c + 1] = v.y;
+        d[4 * c + 2] = v.z;
+        d[4 * c + 3] = v.w;
+    }
+}
+
+// ALIGNED: the caller guarantees p is 16-byte aligned (host-checked base and
+// stride, or host-packed values); otherwise a wave-uniform test picks the path.
+template <bool ALIGNED>
+__device__ __forceinline__ void sha1_tail(const uint8_t* p, uint64_t len, uint32_t h[5]);
+
+// Whole message in registers: full blocks with a one-block register prefetch
+// (aligned) or the 80-byte funnel window (unaligned), then the padding blocks.
+template <bool ALIGNED>
+__device__ __forceinline__ void sha1_value(const uint8_t* p, uint64_t len, uint32_t h[5]) {
+    sha1_init(h);
+    const uint64_t nfull = len >> 6;
+    uint32_t w[16];
+    const bool aligned = ALIGNED || __all((reinterpret_cast<uintptr_t>(p) & 15) == 0);
+    if (aligned) {
+        const uint4* q = reinterpret_cast<const uint4*>(p);
+        uint4 c[4];
+        if (nfull > 0) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) c[i] = q[i];
+        }
+        for (uint64_t b = 0; b < nfull; ++b) {
+            be16_from_raw(c, w);
+            if (b + 1 < nfull) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) c[i] = q[4 * (b + 1) + i];
+            }
+            sha1_compress(h, w);
+        }
+    } else {
+        const uint32_t s = uint32_t(reinterpret_cast<uintptr_t>(p) & 15);
+        for (uint64_t b = 0; b < nfull; ++b) {
+            uint32_t d[20];
+            load_window(p + 64 * b, 64u, d);
+            be16_funnel(d, s, w);
+            sha1_compress(h, w);
+        }
+    }
+    sha1_tail<ALIGNED>(p, len, h);
+}
+
+// The 1-2 padding blocks: rem = len % 64 value bytes, 0x80, zeros, 64-bit
+// big-endian bit length (FIPS 180-4 5.1.1).  h holds the state after the full
+// blocks.
+template <bool ALIGNED>
+__device__ __forceinline__ void sha1_tail(const uint8_t* p, uint64_t len, uint32_t h[5]) {
+    uint32_t w[16];
+    const uint64_t nfull = len >> 6;
+    const uint32_t rem = uint32_t(len & 63);
+    const uint8_t* pt = p + 64 * nfull;
+    if (ALIGNED) {
+        const uint4* q = reinterpret_cast<const uint4*>(pt);
+        uint4 c[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) c[i] = (uint32_t(16 * i) < rem) ? q[i] : make_uint4(0u, 0u, 0u, 0u);
+        be16_from_raw(c, w);
+    } else {
+        uint32_t d[20];
+        load_window(pt, rem, d);
+        be16_funnel(d, uint32_t(reinterpret_cast<uintptr_t>(pt) & 15), w);
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const int v = int(rem) - 4 * j;  // value bytes inside word j
+        uint32_t m = v >= 4 ? 0xFFFFFFFFu : (v <= 0 ? 0u : (0xFFFFFFFFu << (32 - 8 * v)));
+        uint32_t x = w[j] & m;
+        if (v >= 0 && v < 4) x |= 0x80u << (24 - 8 * v);
+        w[j] = x;
+    }
+    const uint64_t bits = len << 3;
+    const bool two = rem >= 56;
+    if (!two) {
+        w[14] = uint32_t(bits >> 32);
+        w[15] = uint32_t(bits);
+    }
+    sha1_compress(h, w);
+    if (two) {
+#pragma unroll
+        for (int j = 0; j < 14; ++j) w[j] = 0u;
+        w[14] = uint32_t(bits >> 32);
+        w[15] = uint32_t(bits);
+        sha1_compress(h, w);
+    }
+}
+
+// Full 64-byte blocks of the 64 values owned by one wavefront, streamed
+// HBM -> LDS with LDS-DMA (global_load_lds_dwordx4: no VGPR staging, fully
+// used 64-byte runs per request), one 4 KiB stage per block, wave-private.
+//
+// Stage layout: value j's block at wbuf + 64 j, its 16-byte chunk q stored
+// at chunk slot q ^ ((j >> 2) & 3), so the four ds_read_b128 of a block are
+// bank-conflict free (every 16-lane ds_read_b128 group hits 16 distinct
+// 16-byte bank slots).  DMA instruction k (k = 0..3) fills values
+// 16k .. 16k+15: lane l loads chunk (l & 3) ^ ((l >> 4) & 3) of value
+// 16k + (l >> 2), which lands at wbuf + 1024 k + 16 l -- exactly its slot.
+//
+// src[k] = chunk address of block 0 for this lane's DMA role k; nf[k] = full
+// blocks of that value (0 for a dead lane).  my_nfull: this lane's own value.
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, uint32_t(__shfl_xor(int(v), o)));
+    return __builtin_amdgcn_readfirstlane(v);
+}
+
+// issue(b) starts the four DMA instructions of block b (each lane for its DMA
+// role); nmax = the wave's largest full-block count (wave-uniform).
+template <class Issue>
+__device__ __forceinline__ void sha1_blocks_lds(const uint8_t* wbuf, uint32_t nmax, uint32_t my_nfull,
+                                                Issue issue, uint32_t h[5]) {
+    const int lane = threadIdx.x & 63;
+    const uint4* rd = reinterpret_cast<const uint4*>(wbuf + 64 * lane);
+    const uint32_t swz = (uint32_t(lane) >> 2) & 3u;
+    uint32_t w[16];
+    if (nmax == 0) return;
+    issue(0u);
+    for (uint32_t b = 0; b < nmax; ++b) {
+        uint4 c[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) c[q] = rd[q ^ swz];
+        be16_from_raw(c, w);
+        if (b + 1 < nmax) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // stage reads done before refill
+            issue(b + 1);
+        }
+        if (b < my_nfull) sha1_compress(h, w);
+    }
+}
+
+// MODE 0: value i at base + i*stride, length L.  MODE 1: base + off[i], len[i].
+// perm (MODE 1 only, nullable): lane i hashes leaf perm[i] (length bucketing).
+// FUSE: also build levels 1..min(8, top) of this block's subtree.
+template <int MODE, bool FUSE, bool ALIGNED>
+__global__ __launch_bounds__(kBlock, kLeafWavesPerSimd) void k_leaf(const uint8_t* __restrict__ base,
+                                                  const uint64_t* __restrict__ off,
+                                                  const uint64_t* __restrict__ len, uint64_t stride,
+                                                  uint64_t L, const uint32_t* __restrict__ perm,
+                                                  uint64_t n, int top, uint8_t* __restrict__ nodes) {
+    // 16 KiB: four wave-private 4 KiB LDS-DMA stages, then reused for the
+    // fused subtree reduce (5 x 256 words).
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kBlock * 64];
+    uint32_t(*lds)[kBlock] = reinterpret_cast<uint32_t(*)[kBlock]>(smem);
+    const uint64_t g = blockIdx.x;
+    const uint64_t t = g * kBlock + threadIdx.x;
+    uint32_t h[5] = {0u, 0u, 0u, 0u, 0u};
+    const bool live = t < n;
+    uint64_t leaf = t;
+    const uint8_t* p = nullptr;
+    uint64_t ln = 0;
+    if (live) {
+        if (MODE == 0) {
+            p = base + t * stride;
+            ln = L;
+        } else {
+            leaf = perm ? uint64_t(perm[t]) : t;
+            p = base + off[leaf];
+            ln = len[leaf];
+        }
+    }
+    if (ALIGNED) {
+        // wave-cooperative LDS-DMA stream of the full blocks, then the tail
+        const int lane = threadIdx.x & 63;
+        const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        uint8_t* wbuf = smem + 4096 * wave;
+        const uint32_t q = (uint32_t(lane) & 3u) ^ ((uint32_t(lane) >> 4) & 3u);
+        const uint32_t my_nfull = live ? uint32_t(ln >> 6) : 0u;
+        sha1_init(h);
+        if (MODE == 0) {
+            // value j of this wave at wave_base + j * stride (32-bit offsets:
+            // saddr-form DMA, one VGPR of addressing)
+            const uint64_t first = g * kBlock + 64 * uint64_t(wave);
+            const uint8_t* wave_base = base + first * stride;
+            const uint32_t nvalid = first < n ? uint32_t(min(uint64_t(64), n - first)) : 0u;
+            const uint32_t off0 = uint32_t(lane >> 2) * uint32_t(stride) + 16u * q;
+            const uint32_t kstep = 16u * uint32_t(stride);
+            const uint32_t nmax = nvalid ? uint32_t(L >> 6) : 0u;
+            auto issue = [&](uint32_t b) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (uint32_t(16 * k + (lane >> 2)) < nvalid)
+                        __builtin_amdgcn_global_load_lds(wave_base + (off0 + k * kstep + 64u * b),
+                                                         wbuf + 1024 * k, 16, 0, 0);
+            };
+            sha1_blocks_lds(wbuf, nmax, my_nfull, issue, h);
+        } else {
+            const uint8_t* src[4];
+            uint32_t nf[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int j = 16 * k + (lane >> 2);
+                const uint64_t pj = uint64_t(__shfl(int64_t(reinterpret_cast<uintptr_t>(p)), j));
+                src[k] = reinterpret_cast<const uint8_t*>(pj) + 16 * q;
+                nf[k] = uint32_t(__shfl(int(my_nfull), j));
+            }
+            auto issue = [&](uint32_t b) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (b < nf[k])
+                        __builtin_amdgcn_global_load_lds(src[k] + 64ull * b, wbuf + 1024 * k, 16, 0, 0);
+            };
+            sha1_blocks_lds(wbuf, wave_max_u32(my_nfull), my_nfull, issue, h);
+        }
+        if (live) {
+            sha1_tail<true>(p, ln, h);
+            store_digest(nodes, leaf, h);
+        }
+    } else if (live) {
+        sha1_value<false>(p, ln, h);
+        store_digest(nodes, leaf, h);
+    }
+    if (FUSE) {
+        __syncthreads();  // every wave is done with its DMA stage
+#pragma unroll
+        for (int k = 0; k < 5; ++k) lds[k][threadIdx.x] = h[k];
+        const int jmax = top < kFuseLevels ? top : kFuseLevels;
+        subtree_reduce(lds, n, 0, jmax, g * kBlock, nodes);
+    }
+}
+
+// K2: reduce one level j0 (already in nodes) up to min(j0 + 8, top).
+__global__ __launch_bounds__(kBlock) void k_reduce(uint8_t* __restrict__ nodes, uint64_t n, int j0,
+                                                    int jmax) {
+    __shared__ uint32_t lds[5][kBlock];
+    const uint64_t lo = uint64_t(blockIdx.x) * kBlock;
+    const uint64_t cnt = lvl_count(n, j0);
+    const uint64_t idx = lo + threadIdx.x;
+    uint32_t h[5] = {0u, 0u, 0u, 0u, 0u};
+    if (idx < cnt) load_digest(nodes, lvl_start(n, j0) + idx, h);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) lds[k][threadIdx.x] = h[k];
+    subtree_reduce(lds, n, j0, jmax, lo, nodes);
+}
+
+// K1g: generic first level for New() over arbitrary leaf Data: message i is
+// leaf[2i].Data || leaf[2i+1].Data (or the lone leaf[2i].Data), staged by the
+// host as one contiguous message per parent.  Same per-lane hash as K1.
+__global__ __launch_bounds__(kBlock) void k_hash_messages(const uint8_t* __restrict__ base,
+                                                           const uint64_t* __restrict__ off,
+                                                           const uint64_t* __restrict__ len,
+                                                           uint64_t n, uint8_t* __restrict__ out) {
+    const uint64_t t = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
+    if (t >= n) return;
+    uint32_t h[5];
+    sha1_value<false>(base + off[t], len[t], h);
+    store_digest(out, t, h);
+}
+
+// ---------------------------------------------------------------------------
+// K3: BFS image.  Levels are written top-down; level L contributes 21 bytes
+// per node (0x00 flag + digest) plus one 0x01 byte for the pad of an odd
+// level below the top.  Each thread produces 16 consecutive image bytes.
+__global__ __launch_bounds__(kBlock) void k_bfs_image(const uint8_t* __restrict__ nodes,
+                                                       BfsLayout lay, uint8_t* __restrict__ img) {
+    const uint64_t p0 = (uint64_t(blockIdx.x) * kBlock + threadIdx.x) * 16;
+    if (p0 >= lay.total) return;
+    int L = 0;  // index into the image-ordered tables (0 = top level)
+    while (L + 1 < lay.nlev && lay.img_start[L + 1] <= p0) ++L;
+    uint32_t wv[4] = {0u, 0u, 0u, 0u};
+    const int nb = (lay.total - p0) < 16 ? int(lay.total - p0) : 16;
+    for (int b = 0; b < nb; ++b) {
+        const uint64_t p = p0 + b;
+        while (L + 1 < lay.nlev && lay.img_start[L + 1] <= p) ++L;
+        const uint64_t rel = p - lay.img_start[L];
+        uint32_t byte;
+        if (rel < 21 * lay.count[L]) {
+            const uint64_t node = rel / 21;
+            const uint32_t r = uint32_t(rel - node * 21);
+            byte = r == 0 ? 0u : nodes[20 * (lay.node_start[L] + node) + r - 1];
+        } else {
+            byte = 0x01u;  // MERKLE_NODE_EMPTY pad (merklenode.go:11, merkletree.go:32-34)
+        }
+        wv[b >> 2] |= byte << (8 * (b & 3));
+    }
+    if (nb == 16) {
+        *reinterpret_cast<uint4*>(img + p0) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+    } else {
+        for (int b = 0; b < nb; ++b) img[p0 + b] = uint8_t(wv[b >> 2] >> (8 * (b & 3)));
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K0: locate values inside a serialized Data-table stream.
+// Record layout (record.go:191-199, little endian): Crc u32 @0, Timestamp i64
+// @4, Status u8 @12, TypeInfo u8 @13, KeySize u64 @14, ValueSize u64 @22,
+// Key @30, Value @30+KeySize.  rec_off[i] = start of record i.
+__device__ __forceinline__ uint64_t ld_le64(const uint8_t* p) {
+    uint64_t v = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v |= uint64_t(p[i]) << (8 * i);
+    return v;
+}
+
+__global__ __launch_bounds__(kBlock) void k_locate(const uint8_t* __restrict__ stream,
+                                                    uint64_t stream_len,
+                                                    const uint64_t* __restrict__ rec_off, uint64_t n,
+                                                    uint64_t* __restrict__ voff,
+                                                    uint64_t* __restrict__ vlen,
+                                                    unsigned int* __restrict__ err) {
+    const uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t r = rec_off[i];
+    uint64_t o = 0, l = 0;
+    if (r + 30 <= stream_len) {
+        const uint64_t ks = ld_le64(stream + r + 14);
+        const uint64_t vs = ld_le64(stream + r + 22);
+        o = r + 30 + ks;
+        l = vs;
+        if (ks > stream_len || vs > stream_len || o + l > stream_len) {
+            atomicOr(err, 1u);
+            o = 0;
+            l = 0;
+        }
+    } else {
+        atomicOr(err, 1u);
+    }
+    voff[i] = o;
+    vlen[i] = l;
+}
+
+// ---------------------------------------------------------------------------
+// synthetic input: byte j = byte (j % 8) of splitmix64(seed, j / 8), LE.
+__device__ __forceinline__ uint64_t splitmix64_at(uint64_t seed, uint64_t k) {
+    uint64_t z = seed + (k + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(kBlock) void k_fill(uint8_t* __restrict__ buf, uint64_t nbytes,
+                                                  uint64_t seed) {
+    const uint64_t stride = uint64_t(gridDim.x) * kBlock;
+    for (uint64_t t = uint64_t(blockIdx.x) * kBlock + threadIdx.x; 16 * t < nbytes; t += stride) {
+        const uint64_t a = splitmix64_at(seed, 2 * t), b = splitmix64_at(seed, 2 * t + 1);
+        if (16 * t + 16 <= nbytes) {
+            *reinterpret_cast<uint4*>(buf + 16 * t) =
+                make_uint4(uint32_t(a), uint32_t(a >> 32), uint32_t(b), uint32_t(b >> 32));
+        } else {
+            for (uint64_t j = 16 * t; j < nbytes; ++j) {
+                const uint64_t v = (j - 16 * t) < 8 ? a : b;
+                buf[j] = uint8_t(v >> (8 * (j & 7)));
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// host-side launchers
+
+static inline unsigned grid_for(uint64_t n) { return unsigned((n + kBlock - 1) / kBlock); }
+
+template <int MODE, bool FUSE, bool ALIGNED>
+static void leaf_kernel(const uint8_t* base, const uint64_t* off, const uint64_t* len,
+                        uint64_t stride, uint64_t L, const uint32_t* perm, uint64_t n, int top,
+                        uint8_t* nodes, hipStream_t s) {
+    hipLaunchKernelGGL((k_leaf<MODE, FUSE, ALIGNED>), dim3(grid_for(n)), dim3(kBlock), 0, s, base,
+                       off, len, stride, L, perm, n, top, nodes);
+}
+
+hipError_t launch_leaf_strided(const uint8_t* base, uint64_t stride, uint64_t L, uint64_t n,
+                               int top, bool fuse, uint8_t* nodes, hipStream_t s) {
+    const bool al = ((reinterpret_cast<uintptr_t>(base) | stride) & 15) == 0;
+    if (fuse && al) leaf_kernel<0, true, true>(base, nullptr, nullptr, stride, L, nullptr, n, top, nodes, s);
+    else if (fuse) leaf_kernel<0, true, false>(base, nullptr, nullptr, stride, L, nullptr, n, top, nodes, s);
+    else if (al) leaf_kernel<0, false, true>(base, nullptr, nullptr, stride, L, nullptr, n, top, nodes, s);
+    else leaf_kernel<0, false, false>(base, nullptr, nullptr, stride, L, nullptr, n, top, nodes, s);
+    return hipGetLastError();
+}
+
+hipError_t launch_leaf_offsets(const uint8_t* base, const uint64_t* off, const uint64_t* len,
+                               const uint32_t* perm, uint64_t n, int top, bool fuse, bool aligned,
+                               uint8_t* nodes, hipStream_t s) {
+    const bool f = fuse && !perm;
+    if (f && aligned) leaf_kernel<1, true, true>(base, off, len, 0, 0, nullptr, n, top, nodes, s);
+    else if (f) leaf_kernel<1, true, false>(base, off, len, 0, 0, nullptr, n, top, nodes, s);
+    else if (aligned) leaf_kernel<1, false, true>(base, off, len, 0, 0, perm, n, top, nodes, s);
+    else leaf_kernel<1, false, false>(base, off, len, 0, 0, perm, n, top, nodes, s);
+    return hipGetLastError();
+}
+
+hipError_t launch_reduce(uint8_t* nodes, uint64_t n, int from_level, int top, hipStream_t s) {
+    int j0 = from_level;
+    while (j0 < top) {
+        const int jmax = (j0 + kFuseLevels < top) ? j0 + kFuseLevels : top;
+        const uint64_t cnt = j0 == 0 ? n : ((n - 1) >> j0) + 1;
+        hipLaunchKernelGGL(k_reduce, dim3(grid_for(cnt)), dim3(kBlock), 0, s, nodes, n, j0, jmax);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        j0 = jmax;
+    }
+    return hipSuccess;
+}
+
+hipError_t launch_hash_messages(const uint8_t* base, const uint64_t* off, const uint64_t* len,
+                                uint64_t n, uint8_t* out, hipStream_t s) {
+    hipLaunchKernelGGL(k_hash_messages, dim3(grid_for(n)), dim3(kBlock), 0, s, base, off, len, n,
+                       out);
+    return hipGetLastError();
+}
+
+hipError_t launch_bfs_image(const uint8_t* nodes, const BfsLayout& lay, uint8_t* img,
+                            hipStream_t s) {
+    const uint64_t threads = (lay.total + 15) / 16;
+    hipLaunchKernelGGL(k_bfs_image, dim3(grid_for(threads)), dim3(kBlock), 0, s, nodes, lay, img);
+    return hipGetLastError();
+}
+
+hipError_t launch_locate(const uint8_t* stream, uint64_t stream_len, const uint64_t* rec_off,
+                         uint64_t n, uint64_t* voff, uint64_t* vlen, unsigned int* err,
+                         hipStream_t s) {
+    hipLaunchKernelGGL(k_locate, dim3(grid_for(n)), dim3(kBlock), 0, s, stream, stream_len,
+                       rec_off, n, voff, vlen, err);
+    return hipGetLastError();
+}
+
+hipError_t scan_exclusive_u64(const uint64_t* in, uint64_t* out, uint64_t n, void* tmp,
+                              size_t* tmp_bytes, hipStream_t s) {
+    return hipcub::DeviceScan::ExclusiveSum(tmp, *tmp_bytes, in, out, int(n), s);
+}
+
+hipError_t launch_fill(uint8_t* buf, uint64_t nbytes, uint64_t seed, hipStream_t s) {
+    uint64_t threads = (nbytes + 15) / 16;
+    uint64_t blocks = (threads + kBlock - 1) / kBlock;
+    if (blocks > 65536) blocks = 65536;
+    if (blocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_fill, dim3(unsigned(blocks)), dim3(kBlock), 0, s, buf, nbytes, seed);
+    return hipGetLastError();
+}
+
+}  // namespace nkv

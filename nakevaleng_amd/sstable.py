@@ -1,0 +1,69 @@
+"""The Merkle step of the SSTable writer (core/sstable/sstable.go), on the MI355X.
+
+  make_metadata              sstable.makeMetadata           sstable.go:58-74
+  make_table_secondaries     Merkle part of MakeTableSecondaries   sstable.go:35-47
+  make_metadata_from_records the same, hashing Values in place inside the
+                             serialized Data table
+  table_filename             util/filename.Table             filename.go:58-65, 300-309
+
+Everything else the writer produces (Data, Index, Summary, Filter files) is
+outside this path and unchanged.
+"""
+from __future__ import annotations
+
+from typing import Iterable, List
+
+import numpy as np
+
+from . import _lib
+from .merkletree import MerkleNode, MerkleTree, MerkleTreeError, New, NewLeaf
+from .record import Record
+
+TYPE_METADATA = "metadata"
+
+
+def table_filename(path: str, dbname: str, level: int, run: int, filetype: str = TYPE_METADATA) -> str:
+    if not path.endswith("/"):
+        raise ValueError("Table() :: relativePath must end with '/'")
+    if level <= 0:
+        raise ValueError("Level must be a positive integer!")
+    if run < 0:
+        raise ValueError("Run must be a non-negative integer!")
+    return f"{path}{dbname}-{level}-{run}-{filetype}.db"
+
+
+def make_metadata(path: str, dbname: str, level: int, run: int, records: Iterable[Record]) -> MerkleTree:
+    """sstable.go:58-74: NewLeaf(rec.Value) per record, New, Serialize."""
+    leaves = [NewLeaf(r.Value) for r in records]
+    tree = New(leaves)  # raises MerkleTreeError("cannot build Merkle Tree from 0 nodes") like the panic
+    tree.Serialize(table_filename(path, dbname, level, run))
+    return tree
+
+
+def make_table_secondaries(path: str, dbname: str, level: int, run: int,
+                           merkleleaves: List[MerkleNode]) -> MerkleTree:
+    """Merkle part of sstable.go:35-47 (leaves collected by lsmtree.merge, lsmtree.go:211)."""
+    tree = New(merkleleaves)
+    tree.Serialize(table_filename(path, dbname, level, run))
+    return tree
+
+
+def make_metadata_from_records(path: str, dbname: str, level: int, run: int, stream: bytes,
+                               rec_sizes: np.ndarray, device: int = 0) -> bytes:
+    """Same output file as make_metadata, straight from the Data-table bytes and
+    KeyContext.RecSize list: values are located and hashed on the device
+    (nkv_tree_from_records).  Returns the root digest."""
+    n = len(rec_sizes)
+    if n == 0:
+        raise MerkleTreeError("cannot build Merkle Tree from 0 nodes")
+    L = _lib.lib()
+    ctx = _lib.default_context(device)
+    buf = np.frombuffer(bytes(stream) + b"\0", dtype=np.uint8)
+    rs = np.ascontiguousarray(rec_sizes, dtype=np.uint64)
+    img = np.zeros(L.nkv_bfs_size(n), np.uint8)
+    root = np.zeros(20, np.uint8)
+    _lib.check(L.nkv_tree_from_records(ctx.h, _lib.p8(buf), buf.size - 1, _lib.p64(rs), n,
+                                       _lib.p8(root), None, _lib.p8(img)), "MakeTable")
+    fname = table_filename(path, dbname, level, run)
+    _lib.check(L.nkv_write_file(fname.encode(), _lib.p8(img), img.size), f"Serialize({fname})")
+    return root.tobytes()

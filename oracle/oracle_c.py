@@ -1,0 +1,136 @@
+"""ctypes binding of oracle/liboracle.so (TEST INFRASTRUCTURE ONLY).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this.
+Parity status: SHA-1 pinned by FIPS 180-4 KATs; tree layer "parity unpinned"
+(see merkle_oracle.c header and DESIGN.md).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_SO = os.path.join(_HERE, "liboracle.so")
+_lib = None
+
+u8p = ctypes.POINTER(ctypes.c_uint8)
+u64p = ctypes.POINTER(ctypes.c_uint64)
+
+
+def build() -> str:
+    src = os.path.join(_HERE, "merkle_oracle.c")
+    if not os.path.exists(_SO) or os.path.getmtime(_SO) < os.path.getmtime(src):
+        subprocess.check_call(["make", "-s", "-C", _HERE, "liboracle.so"])
+    return _SO
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = ctypes.CDLL(_SO)
+        L.nkvo_sha1.argtypes = [u8p, ctypes.c_uint64, u8p]
+        L.nkvo_splitmix64_fill.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint64]
+        L.nkvo_leaf_hashes.argtypes = [u8p, u64p, u64p, ctypes.c_uint64, u8p, ctypes.c_int]
+        L.nkvo_leaf_hashes_strided.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, u8p, ctypes.c_int]
+        L.nkvo_num_levels.argtypes = [ctypes.c_uint64]
+        L.nkvo_num_levels.restype = ctypes.c_int
+        L.nkvo_total_nodes.argtypes = [ctypes.c_uint64]
+        L.nkvo_total_nodes.restype = ctypes.c_uint64
+        L.nkvo_tree_from_digests.argtypes = [u8p, ctypes.c_uint64]
+        L.nkvo_tree_from_digests.restype = ctypes.c_int
+        L.nkvo_tree_generic.argtypes = [u8p, u64p, u64p, ctypes.c_uint64, u8p]
+        L.nkvo_tree_generic.restype = ctypes.c_int
+        L.nkvo_bfs_size.argtypes = [ctypes.c_uint64]
+        L.nkvo_bfs_size.restype = ctypes.c_uint64
+        L.nkvo_bfs_image.argtypes = [u8p, ctypes.c_uint64, u8p]
+        L.nkvo_bfs_image.restype = ctypes.c_uint64
+        _lib = L
+    return _lib
+
+
+def _p8(a: np.ndarray):
+    return a.ctypes.data_as(u8p)
+
+
+def _p64(a: np.ndarray):
+    return a.ctypes.data_as(u64p)
+
+
+def sha1(data: bytes) -> bytes:
+    a = np.frombuffer(bytes(data) + b"\0", dtype=np.uint8)
+    out = np.zeros(20, np.uint8)
+    lib().nkvo_sha1(_p8(a), len(data), _p8(out))
+    return out.tobytes()
+
+
+def splitmix64_bytes(nbytes: int, seed: int) -> np.ndarray:
+    out = np.empty(max(nbytes, 1), np.uint8)
+    lib().nkvo_splitmix64_fill(_p8(out), nbytes, seed)
+    return out[:nbytes]
+
+
+def leaf_hashes(base: np.ndarray, off: np.ndarray, ln: np.ndarray, threads: int = 1) -> np.ndarray:
+    base = np.ascontiguousarray(base, np.uint8)
+    if base.size == 0:
+        base = np.zeros(1, np.uint8)
+    off = np.ascontiguousarray(off, np.uint64)
+    ln = np.ascontiguousarray(ln, np.uint64)
+    n = off.size
+    out = np.zeros((max(n, 1), 20), np.uint8)
+    lib().nkvo_leaf_hashes(_p8(base), _p64(off), _p64(ln), n, _p8(out), threads)
+    return out[:n]
+
+
+def leaf_hashes_strided(base: np.ndarray, stride: int, L: int, n: int, threads: int = 1) -> np.ndarray:
+    base = np.ascontiguousarray(base, np.uint8)
+    out = np.zeros((max(n, 1), 20), np.uint8)
+    lib().nkvo_leaf_hashes_strided(_p8(base), stride, L, n, _p8(out), threads)
+    return out[:n]
+
+
+def num_levels(n: int) -> int:
+    return lib().nkvo_num_levels(n)
+
+
+def total_nodes(n: int) -> int:
+    return lib().nkvo_total_nodes(n)
+
+
+def tree_from_digests(leaf20: np.ndarray) -> np.ndarray:
+    """All levels, level-major bottom-up, shape (total_nodes, 20).  Root is the last row."""
+    leaf20 = np.ascontiguousarray(leaf20, np.uint8).reshape(-1, 20)
+    n = leaf20.shape[0]
+    nodes = np.zeros((total_nodes(n), 20), np.uint8)
+    nodes[:n] = leaf20
+    if lib().nkvo_tree_from_digests(_p8(nodes), n) < 0:
+        raise ValueError("cannot build Merkle Tree from 0 nodes")
+    return nodes
+
+
+def tree_generic(data: np.ndarray, off: np.ndarray, ln: np.ndarray) -> np.ndarray:
+    """Levels 1..top for leaves of arbitrary Data; shape (total_nodes(n) - n, 20)."""
+    data = np.ascontiguousarray(data, np.uint8)
+    if data.size == 0:
+        data = np.zeros(1, np.uint8)
+    off = np.ascontiguousarray(off, np.uint64)
+    ln = np.ascontiguousarray(ln, np.uint64)
+    n = off.size
+    up = np.zeros((max(total_nodes(n) - n, 1), 20), np.uint8)
+    if lib().nkvo_tree_generic(_p8(data), _p64(off), _p64(ln), n, _p8(up)) < 0:
+        raise ValueError("cannot build Merkle Tree from 0 nodes")
+    return up
+
+
+def bfs_size(n: int) -> int:
+    return lib().nkvo_bfs_size(n)
+
+
+def bfs_image(nodes: np.ndarray, n: int) -> bytes:
+    nodes = np.ascontiguousarray(nodes, np.uint8)
+    img = np.zeros(max(bfs_size(n), 1), np.uint8)
+    w = lib().nkvo_bfs_image(_p8(nodes), n, _p8(img))
+    return img[:w].tobytes()

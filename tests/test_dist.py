@@ -1,0 +1,71 @@
+"""CPU, world_size 2 over gloo: sharded per-run Merkle rebuild + root all-gather.
+
+The table builder is injected (here: the oracle); on the GPU box the default
+builder hashes on the rank's device and the group is RCCL.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from nakevaleng_amd import record
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def make_tables(k):
+    rng = np.random.default_rng(11)
+    tables = []
+    for t in range(k):
+        recs = [record.New(rng.bytes(8), rng.bytes(int(rng.integers(0, 200))), timestamp=t) for _ in range(37 + t)]
+        tables.append(record.data_table(recs))
+    return tables
+
+
+def oracle_root(table):
+    from oracle import oracle_c as oc
+    stream, sizes = table
+    off, ln = record.value_spans(stream, sizes)
+    d = oc.leaf_hashes(np.frombuffer(stream, np.uint8), off, ln)
+    return oc.tree_from_digests(d)[-1].tobytes()
+
+
+def _worker(rank, world, port, k, q):
+    import torch.distributed as dist
+    from nakevaleng_amd import lsmtree
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    built = []
+
+    def build(tb):
+        built.append(1)
+        return oracle_root(tb)
+
+    roots = lsmtree.compact_roots(make_tables(k), build=build)
+    q.put((rank, len(built), [r.hex() for r in roots]))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("k", [2, 3, 4])
+def test_compact_roots_world2(oracle, k):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, k, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    want = [oracle_root(t).hex() for t in make_tables(k)]
+    assert res[0][2] == want and res[1][2] == want  # every rank holds every root
+    assert res[0][1] + res[1][1] == k  # each table built exactly once
+    assert res[0][1] == (k + 1) // 2

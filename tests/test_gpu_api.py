@@ -1,0 +1,180 @@
+"""GPU: the ds/merkletree-shaped Python mirror, the SSTable/compaction Merkle
+steps and the records path, against the golden fixtures and the oracle."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from tests.golden.make_golden import splitmix64_bytes
+
+pytestmark = pytest.mark.gpu
+GOLDEN = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "merkle_golden.json")))
+
+
+@pytest.fixture(scope="module")
+def mt(nkv):
+    from nakevaleng_amd import merkletree
+    return merkletree
+
+
+def test_readme_example(mt):
+    g = GOLDEN["readme"]
+    t = mt.New([mt.MerkleNode(x.encode()) for x in g["leaves"]])
+    assert t.Root.String() == g["root"]
+    assert t.SerializeBytes().hex() == g["bfs_hex"]
+    assert t.Validate() is True
+
+
+def test_single_newleaf(mt):
+    t = mt.New([mt.NewLeaf(b"x")])
+    assert t.Root.String() == GOLDEN["single_x"]["root"]
+    assert t.SerializeBytes().hex() == GOLDEN["single_x"]["bfs_hex"]
+
+
+@pytest.mark.parametrize("case", GOLDEN["trees"], ids=lambda c: f"n{c['n']}x{c['value_bytes']}")
+def test_newleaf_batch_then_new(mt, case, tmp_path):
+    n, vlen = case["n"], case["value_bytes"]
+    data = splitmix64_bytes(n * vlen, case["seed"])
+    leaves = [mt.NewLeaf(data[i * vlen:(i + 1) * vlen]) for i in range(n)]
+    t = mt.New(leaves)
+    assert mt.root_of(t).hex() == case["root"]
+    f = str(tmp_path / "db-1-0-metadata.db")
+    t.Serialize(f)
+    img = open(f, "rb").read()
+    assert len(img) == case["bfs_len"] and hashlib.sha1(img).hexdigest() == case["bfs_sha1"]
+    assert hashlib.sha1(b"".join(x.Data for x in leaves)).hexdigest() == case["leaf_digests_sha1"]
+    # the materialized pointer tree serializes to the same bytes
+    assert t.Root.String() == case["root"]
+    assert hashlib.sha1(t.SerializeBytes()).hexdigest() == case["bfs_sha1"]
+    assert t.Validate()
+
+
+def test_leaf_data_before_new(mt, oracle):
+    vals = [bytes([i]) * (i * 13) for i in range(40)]
+    leaves = [mt.NewLeaf(v) for v in vals]
+    assert leaves[7].Data == hashlib.sha1(vals[7]).digest()  # resolves the pending batch on the GPU
+    t = mt.New(leaves)  # 20-byte leaves path (batch already sealed)
+    want = oracle.tree_from_digests(np.frombuffer(b"".join(hashlib.sha1(v).digest() for v in vals), np.uint8))
+    assert mt.root_of(t) == want[-1].tobytes()
+
+
+def test_validate_detects_corruption(mt):
+    t = mt.New([mt.NewLeaf(bytes([i]) * 100) for i in range(13)])
+    assert t.Validate()
+    leaf = t.Root
+    while leaf.Left is not None:
+        leaf = leaf.Left
+    leaf.Data = bytes(20)
+    assert not t.Validate()
+
+
+def test_deserialize_root_only(mt, tmp_path):
+    t = mt.New([mt.NewLeaf(bytes([i])) for i in range(100)])
+    f = str(tmp_path / "m.db")
+    t.Serialize(f)
+    t2 = mt.MerkleTree()
+    t2.Deserialize(f)
+    assert t2.Root.Data == mt.root_of(t)
+    assert t2.Root.Left is None and t2.Root.Right is None
+    assert t2.Validate()
+
+
+def test_serialize_keeps_stale_tail(mt, tmp_path):
+    f = str(tmp_path / "m.db")
+    big = mt.New([mt.NewLeaf(bytes([i])) for i in range(10)])
+    small = mt.New([mt.NewLeaf(b"a")])
+    big.Serialize(f)
+    small.Serialize(f)
+    blob = open(f, "rb").read()
+    assert len(blob) == len(big.SerializeBytes())
+    assert blob[:43] == small.SerializeBytes()
+
+
+def test_empty_new_raises(mt):
+    with pytest.raises(mt.MerkleTreeError, match="cannot build Merkle Tree from 0 nodes"):
+        mt.New([])
+
+
+@pytest.mark.parametrize("g", GOLDEN["generic"], ids=lambda g: f"n{g['n']}")
+def test_generic_leaves(mt, g):
+    raw = splitmix64_bytes(4096, g["seed"])
+    datas, p = [], g["offset0"]
+    for L in g["lens"]:
+        datas.append(raw[p:p + L])
+        p += L
+    t = mt.New([mt.MerkleNode(d) for d in datas])
+    assert mt.root_of(t).hex() == g["root"]
+    img = t.SerializeBytes()
+    assert len(img) == g["bfs_len"] and hashlib.sha1(img).hexdigest() == g["bfs_sha1"]
+
+
+def _golden_stream():
+    from nakevaleng_amd import record
+    g = GOLDEN["records"]
+    raw = splitmix64_bytes(1 << 16, g["seed"])
+    recs, p = [], 0
+    for i in range(g["n"]):
+        ks, vs = 1 + raw[i] % 20, (raw[50 + i] * 7) % 300
+        recs.append(record.New(raw[p:p + ks], raw[p + ks:p + ks + vs], timestamp=1700000000 + i))
+        p += ks + vs
+    return recs
+
+
+def test_sstable_make_metadata(nkv, tmp_path):
+    from nakevaleng_amd import sstable
+    g = GOLDEN["records"]
+    recs = _golden_stream()
+    t = sstable.make_metadata(str(tmp_path) + "/", "nakevaleng", 1, 0, recs)
+    blob = open(str(tmp_path / "nakevaleng-1-0-metadata.db"), "rb").read()
+    assert hashlib.sha1(blob).hexdigest() == g["bfs_sha1"]
+
+
+def test_metadata_from_records_in_place(nkv, tmp_path):
+    from nakevaleng_amd import record, sstable
+    g = GOLDEN["records"]
+    stream, sizes = record.data_table(_golden_stream())
+    root = sstable.make_metadata_from_records(str(tmp_path) + "/", "db", 2, 5, stream, sizes)
+    assert root.hex() == g["root"]
+    blob = open(str(tmp_path / "db-2-5-metadata.db"), "rb").read()
+    assert hashlib.sha1(blob).hexdigest() == g["bfs_sha1"]
+
+
+def test_records_path_large_and_bad_header(nkv, oracle):
+    from nakevaleng_amd import _lib, lsmtree, record
+    rng = np.random.default_rng(5)
+    recs = [record.New(rng.bytes(int(rng.integers(1, 64))), rng.bytes(int(rng.integers(0, 5000))), timestamp=i)
+            for i in range(3000)]
+    stream, sizes = record.data_table(recs)
+    off, ln = record.value_spans(stream, sizes)
+    want = oracle.tree_from_digests(oracle.leaf_hashes(np.frombuffer(stream, np.uint8), off, ln))
+    assert lsmtree.gpu_table_root((stream, sizes)) == want[-1].tobytes()
+    bad = bytearray(stream)
+    bad[22:30] = (10**12).to_bytes(8, "little")  # ValueSize of record 0 points past the stream
+    with pytest.raises(_lib.NkvError):
+        lsmtree.gpu_table_root((bytes(bad), sizes))
+
+
+def test_device_locator_matches_host(nkv):
+    import torch
+    from nakevaleng_amd import record
+    _lib, ctx = nkv
+    L = _lib.lib()
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    stream, sizes = record.data_table(_golden_stream())
+    d_stream = torch.from_numpy(np.frombuffer(stream, np.uint8).copy()).cuda()
+    d_sizes = torch.from_numpy(sizes.astype(np.uint64).view(np.int64)).cuda()
+    n = len(sizes)
+    d_roff = torch.empty(n, dtype=torch.int64, device="cuda")
+    d_voff = torch.empty(n, dtype=torch.int64, device="cuda")
+    d_vlen = torch.empty(n, dtype=torch.int64, device="cuda")
+    _lib.check(L.nkv_record_offsets_dev(ctx.h, d_sizes.data_ptr(), n, d_roff.data_ptr()))
+    _lib.check(L.nkv_locate_values_dev(ctx.h, d_stream.data_ptr(), len(stream), d_roff.data_ptr(), n,
+                                       d_voff.data_ptr(), d_vlen.data_ptr()))
+    torch.cuda.synchronize()
+    off, ln = record.value_spans(stream, sizes)
+    assert np.array_equal(d_voff.cpu().numpy().astype(np.uint64), off)
+    assert np.array_equal(d_vlen.cpu().numpy().astype(np.uint64), ln)
+    assert np.array_equal(d_roff.cpu().numpy().astype(np.uint64),
+                          np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64))

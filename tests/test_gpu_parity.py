@@ -1,0 +1,215 @@
+"""GPU parity: the HIP path (through the C-ABI) against the CPU oracle.
+
+Bit-exact comparisons only (integer/byte work).  Sizes are chosen so the oracle
+finishes in seconds; the full BASELINE config (1 Mi x 4 KiB) is compared in
+full against the multi-threaded C oracle.
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+EDGE_LENS = [0, 1, 19, 20, 55, 56, 57, 63, 64, 65, 119, 120, 127, 128, 1024, 4050, 4096, 65536]
+EDGE_N = [1, 2, 3, 4, 5, 7, 8, 9, 15, 16, 17, 255, 256, 257, 511, 512, 513, 1000, 1023, 1024,
+          1025, 65535, 65536, 65537, 70001]
+SEED = 0x6E616B65
+
+
+def _torch():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a visible device"
+    return torch
+
+
+def _dev(torch, arr: np.ndarray):
+    return torch.from_numpy(np.ascontiguousarray(arr)).cuda()
+
+
+def _bind(torch, ctx):
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+
+
+def test_leaf_hash_edge_lengths_host_api(nkv, oracle):
+    _lib, ctx = nkv
+    L = _lib.lib()
+    lens = np.array(EDGE_LENS * 3, dtype=np.uint64)
+    off = np.zeros(lens.size, np.uint64)
+    off[1:] = np.cumsum(lens[:-1] + 3)  # ragged, unaligned source offsets
+    data = oracle.splitmix64_bytes(int(off[-1] + lens[-1]) + 1, SEED)
+    out = np.zeros((lens.size, 20), np.uint8)
+    _lib.check(L.nkv_leaf_hash(ctx.h, _lib.p8(data), _lib.p64(off), _lib.p64(lens), lens.size, _lib.p8(out)))
+    want = oracle.leaf_hashes(data, off, lens)
+    assert np.array_equal(out, want)
+    for i in range(lens.size):  # independent check against OpenSSL
+        v = data[int(off[i]):int(off[i] + lens[i])].tobytes()
+        assert out[i].tobytes() == hashlib.sha1(v).digest()
+
+
+@pytest.mark.parametrize("shift", list(range(16)))
+def test_leaf_hash_every_alignment_device(nkv, oracle, shift):
+    """Unaligned in-place hashing (nkv_leaf_hash_dev): every start alignment, every tail length."""
+    torch = _torch()
+    _lib, ctx = nkv
+    _bind(torch, ctx)
+    L = _lib.lib()
+    lens = np.array(EDGE_LENS + list(range(0, 200)), dtype=np.uint64)
+    off = np.zeros(lens.size, np.uint64)
+    off[1:] = np.cumsum(((lens[:-1] + 15) // 16) * 16 + 16)
+    off += shift
+    nbytes = int(off[-1] + lens[-1])
+    data = oracle.splitmix64_bytes(nbytes, SEED + shift)
+    d_data, d_off, d_len = _dev(torch, data), _dev(torch, off), _dev(torch, lens)
+    d_nodes = torch.zeros(lens.size * 20, dtype=torch.uint8, device="cuda")
+    _lib.check(L.nkv_leaf_hash_dev(ctx.h, d_data.data_ptr(), d_off.data_ptr(), d_len.data_ptr(),
+                                   lens.size, d_nodes.data_ptr()))
+    torch.cuda.synchronize()
+    got = d_nodes.cpu().numpy().reshape(-1, 20)
+    assert np.array_equal(got, oracle.leaf_hashes(data, off, lens))
+
+
+def test_leaf_hash_mixed_wave_alignment(nkv, oracle):
+    """Lanes of one wavefront with different alignments and lengths."""
+    torch = _torch()
+    _lib, ctx = nkv
+    _bind(torch, ctx)
+    L = _lib.lib()
+    rng = np.random.default_rng(7)
+    n = 5000
+    lens = rng.integers(0, 3000, n).astype(np.uint64)
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum(lens[:-1] + rng.integers(0, 17, n - 1).astype(np.uint64))
+    data = oracle.splitmix64_bytes(int(off[-1] + lens[-1]), SEED)
+    d_data, d_off, d_len = _dev(torch, data), _dev(torch, off), _dev(torch, lens)
+    d_nodes = torch.zeros(L.nkv_total_nodes(n) * 20, dtype=torch.uint8, device="cuda")
+    _lib.check(L.nkv_tree_from_values_dev(ctx.h, d_data.data_ptr(), d_off.data_ptr(), d_len.data_ptr(),
+                                          n, d_nodes.data_ptr()))
+    torch.cuda.synchronize()
+    got = d_nodes.cpu().numpy().reshape(-1, 20)
+    want = oracle.tree_from_digests(oracle.leaf_hashes(data, off, lens))
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("n", EDGE_N)
+def test_tree_build_from_digests(nkv, oracle, n):
+    _lib, ctx = nkv
+    L = _lib.lib()
+    leaf20 = oracle.splitmix64_bytes(20 * n, SEED ^ n)
+    nodes = np.zeros((L.nkv_total_nodes(n), 20), np.uint8)
+    img = np.zeros(L.nkv_bfs_size(n), np.uint8)
+    root = np.zeros(20, np.uint8)
+    _lib.check(L.nkv_tree_build(ctx.h, _lib.p8(leaf20), n, _lib.p8(root), _lib.p8(nodes), _lib.p8(img)))
+    want = oracle.tree_from_digests(leaf20.reshape(n, 20))
+    assert np.array_equal(nodes, want)
+    assert root.tobytes() == want[-1].tobytes()
+    assert img.tobytes() == oracle.bfs_image(want, n)
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 255, 256, 257, 511, 513, 1000, 4097, 65537])
+def test_tree_from_values_fused(nkv, oracle, n):
+    """Leaf kernel fused with the first 8 levels, then the level reduce."""
+    _lib, ctx = nkv
+    L = _lib.lib()
+    vlen = 100
+    data = oracle.splitmix64_bytes(n * vlen, SEED + n)
+    off = np.arange(n, dtype=np.uint64) * vlen
+    lens = np.full(n, vlen, np.uint64)
+    nodes = np.zeros((L.nkv_total_nodes(n), 20), np.uint8)
+    img = np.zeros(L.nkv_bfs_size(n), np.uint8)
+    _lib.check(L.nkv_tree_from_values(ctx.h, _lib.p8(data), _lib.p64(off), _lib.p64(lens), n, None,
+                                      _lib.p8(nodes), _lib.p8(img)))
+    want = oracle.tree_from_digests(oracle.leaf_hashes(data, off, lens))
+    assert np.array_equal(nodes, want)
+    assert img.tobytes() == oracle.bfs_image(want, n)
+
+
+@pytest.mark.parametrize("base_off,stride,vlen", [(0, 4096, 4096), (0, 1024, 1024), (46, 4096, 4050),
+                                                  (0, 4112, 4100), (3, 64, 61)])
+def test_strided_device_path(nkv, oracle, base_off, stride, vlen):
+    """The bench path (nkv_tree_from_strided_dev), aligned and SSTable-like unaligned."""
+    torch = _torch()
+    _lib, ctx = nkv
+    _bind(torch, ctx)
+    L = _lib.lib()
+    n = 20000
+    nbytes = base_off + stride * n
+    d = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    _lib.check(L.nkv_fill_splitmix64_dev(ctx.h, d.data_ptr(), nbytes, SEED))
+    d_nodes = torch.zeros(L.nkv_total_nodes(n) * 20, dtype=torch.uint8, device="cuda")
+    _lib.check(L.nkv_tree_from_strided_dev(ctx.h, d.data_ptr() + base_off, stride, vlen, n, d_nodes.data_ptr()))
+    torch.cuda.synchronize()
+    host = oracle.splitmix64_bytes(nbytes, SEED)
+    assert np.array_equal(d.cpu().numpy(), host), "device splitmix64 fill differs from the oracle's"
+    got = d_nodes.cpu().numpy().reshape(-1, 20)
+    want = oracle.tree_from_digests(oracle.leaf_hashes_strided(host[base_off:], stride, vlen, n, threads=8))
+    assert np.array_equal(got, want)
+
+
+def test_full_size_config2_bit_exact(nkv, oracle):
+    """BASELINE config 2: 1 Mi leaves x 4 KiB, whole tree vs the C oracle."""
+    torch = _torch()
+    _lib, ctx = nkv
+    _bind(torch, ctx)
+    L = _lib.lib()
+    n, vlen = 1 << 20, 4096
+    d = torch.empty(n * vlen, dtype=torch.uint8, device="cuda")
+    _lib.check(L.nkv_fill_splitmix64_dev(ctx.h, d.data_ptr(), n * vlen, SEED))
+    d_nodes = torch.zeros(L.nkv_total_nodes(n) * 20, dtype=torch.uint8, device="cuda")
+    _lib.check(L.nkv_tree_from_strided_dev(ctx.h, d.data_ptr(), vlen, vlen, n, d_nodes.data_ptr()))
+    d_img = torch.zeros(L.nkv_bfs_size(n), dtype=torch.uint8, device="cuda")
+    _lib.check(L.nkv_bfs_image_dev(ctx.h, d_nodes.data_ptr(), n, d_img.data_ptr()))
+    torch.cuda.synchronize()
+    got = d_nodes.cpu().numpy().reshape(-1, 20)
+    img = d_img.cpu().numpy().tobytes()
+    del d
+    torch.cuda.empty_cache()
+    host = oracle.splitmix64_bytes(n * vlen, SEED)
+    want = oracle.tree_from_digests(oracle.leaf_hashes_strided(host, vlen, vlen, n, threads=16))
+    del host
+    assert np.array_equal(got, want)
+    assert len(img) == oracle.bfs_size(n) == (2 * n - 1) * 21
+    assert img == oracle.bfs_image(want, n)
+
+
+def test_bfs_image_device_odd_sizes(nkv, oracle):
+    torch = _torch()
+    _lib, ctx = nkv
+    _bind(torch, ctx)
+    L = _lib.lib()
+    for n in (1, 2, 3, 5, 1025, 300001):
+        leaf20 = oracle.splitmix64_bytes(20 * n, n)
+        want = oracle.tree_from_digests(leaf20.reshape(n, 20))
+        d_nodes = _dev(torch, want.reshape(-1))
+        d_img = torch.zeros(L.nkv_bfs_size(n), dtype=torch.uint8, device="cuda")
+        _lib.check(L.nkv_bfs_image_dev(ctx.h, d_nodes.data_ptr(), n, d_img.data_ptr()))
+        torch.cuda.synchronize()
+        assert d_img.cpu().numpy().tobytes() == oracle.bfs_image(want, n)
+
+
+def test_empty_tree_is_reference_error(nkv):
+    _lib, ctx = nkv
+    L = _lib.lib()
+    rc = L.nkv_tree_build(ctx.h, None, 0, None, None, None)
+    assert rc == _lib.NKV_ERR_EMPTY
+    assert L.nkv_strerror(rc).decode() == "cannot build Merkle Tree from 0 nodes"
+    z = np.zeros(1, np.uint64)
+    assert L.nkv_tree_from_values(ctx.h, _lib.p8(np.zeros(1, np.uint8)), _lib.p64(z), _lib.p64(z), 0,
+                                  None, None, None) == _lib.NKV_ERR_EMPTY
+
+
+def test_deterministic_repeat(nkv, oracle):
+    torch = _torch()
+    _lib, ctx = nkv
+    _bind(torch, ctx)
+    L = _lib.lib()
+    n = 100000
+    d = torch.empty(n * 1024, dtype=torch.uint8, device="cuda")
+    _lib.check(L.nkv_fill_splitmix64_dev(ctx.h, d.data_ptr(), n * 1024, 99))
+    outs = []
+    for _ in range(3):
+        d_nodes = torch.zeros(L.nkv_total_nodes(n) * 20, dtype=torch.uint8, device="cuda")
+        _lib.check(L.nkv_tree_from_strided_dev(ctx.h, d.data_ptr(), 1024, 1024, n, d_nodes.data_ptr()))
+        torch.cuda.synchronize()
+        outs.append(d_nodes.cpu().numpy())
+    assert all(np.array_equal(outs[0], o) for o in outs[1:])

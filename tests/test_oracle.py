@@ -1,0 +1,114 @@
+"""CPU: pin the oracle (C restatement + literal Python restatement) before trusting it.
+
+SHA-1 is pinned by FIPS 180-4 vectors; the tree layer by the committed golden
+fixtures (tests/golden/make_golden.py) and by agreement of the two independent
+restatements.  Parity at tree level is "unpinned" against the Go binary itself
+(no Go toolchain, no reference fixtures) -- see DESIGN.md.
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import merkle_ref as mr
+from tests.golden.make_golden import splitmix64_bytes
+
+GOLDEN = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "merkle_golden.json")))
+
+
+@pytest.mark.parametrize("kat", GOLDEN["fips"])
+def test_fips_vectors_c_oracle(oracle, kat):
+    msg = bytes.fromhex(kat["msg_hex"]) * kat["repeat"]
+    assert oracle.sha1(msg).hex() == kat["sha1"]
+    assert hashlib.sha1(msg).hexdigest() == kat["sha1"]
+
+
+def test_splitmix64_generators_agree(oracle):
+    for n, seed in ((0, 1), (1, 2), (7, 3), (8, 4), (1001, 0x6E616B65)):
+        assert oracle.splitmix64_bytes(n, seed).tobytes() == splitmix64_bytes(n, seed)
+
+
+@pytest.mark.parametrize("case", GOLDEN["leaf_lengths"], ids=lambda c: f"len{c['len']}")
+def test_leaf_lengths(oracle, case):
+    data = splitmix64_bytes(case["len"], case["seed"])
+    assert oracle.sha1(data).hex() == case["sha1"]
+    assert mr.NewLeaf(data).String() == case["sha1"]
+
+
+@pytest.mark.parametrize("case", GOLDEN["trees"], ids=lambda c: f"n{c['n']}x{c['value_bytes']}")
+def test_trees_c_oracle_vs_golden(oracle, case):
+    n, vlen = case["n"], case["value_bytes"]
+    data = np.frombuffer(splitmix64_bytes(n * vlen, case["seed"]), np.uint8)
+    leaves = oracle.leaf_hashes_strided(data, vlen, vlen, n)
+    assert hashlib.sha1(leaves.tobytes()).hexdigest() == case["leaf_digests_sha1"]
+    nodes = oracle.tree_from_digests(leaves)
+    assert nodes[-1].tobytes().hex() == case["root"]
+    img = oracle.bfs_image(nodes, n)
+    assert len(img) == case["bfs_len"] == oracle.bfs_size(n)
+    assert hashlib.sha1(img).hexdigest() == case["bfs_sha1"]
+    assert img[:64].hex() == case["bfs_head_hex"]
+    # level shape: real nodes per level plus the pad of every odd level below the top
+    sizes = case["level_sizes_with_pads"]  # top-down
+    counts = [n]
+    while len(counts) < 2 or counts[-1] > 1:
+        counts.append((counts[-1] + 1) // 2)
+    want = [c + (c & 1 if L < len(counts) - 1 else 0) for L, c in enumerate(counts)][::-1]
+    assert sizes == want
+
+
+def test_readme_example_literal_restatement():
+    g = GOLDEN["readme"]
+    t = mr.New([mr.MerkleNode(x.encode()) for x in g["leaves"]])
+    assert t.Root.String() == g["root"] == "40bd4db4f1ae6c7d962b3edd605aea88549b8dcb"
+    assert t.SerializeBytes().hex() == g["bfs_hex"]
+    assert len(bytes.fromhex(g["bfs_hex"])) == 162
+    assert t.Validate()
+
+
+def test_generic_c_oracle_vs_golden(oracle):
+    for g in GOLDEN["generic"]:
+        raw = splitmix64_bytes(4096, g["seed"])
+        off = np.cumsum([g["offset0"]] + g["lens"][:-1]).astype(np.uint64)
+        lens = np.asarray(g["lens"], np.uint64)
+        up = oracle.tree_generic(np.frombuffer(raw, np.uint8), off, lens)
+        assert up[-1].tobytes().hex() == g["root"]
+
+
+def test_deserialize_is_root_only():
+    """merkletree.go:135-143 breaks before linking any child."""
+    img = bytes.fromhex(GOLDEN["readme"]["bfs_hex"])
+    t = mr.MerkleTree()
+    t.DeserializeBytes(img)
+    assert t.Root.String() == GOLDEN["readme"]["root"]
+    assert t.Root.Left is None and t.Root.Right is None
+    assert t.Validate()
+
+
+def test_validate_detects_corrupted_leaf():
+    t = mr.New([mr.NewLeaf(bytes([i])) for i in range(9)])
+    assert t.Validate()
+    leaf = t.Root
+    while leaf.Left is not None:
+        leaf = leaf.Left
+    leaf.Data = bytes(20)
+    assert not t.Validate()
+
+
+def test_empty_tree_error_text():
+    with pytest.raises(mr.MerkleTreeError, match="^cannot build Merkle Tree from 0 nodes$"):
+        mr.New([])
+
+
+def test_literal_restatement_matches_c_oracle_random(oracle):
+    rng = np.random.default_rng(3)
+    for n in (1, 2, 3, 6, 31, 64, 129):
+        lens = rng.integers(0, 300, n).astype(np.uint64)
+        off = np.zeros(n, np.uint64)
+        off[1:] = np.cumsum(lens[:-1])
+        data = rng.integers(0, 256, int(lens.sum()) + 1, dtype=np.uint8)
+        t = mr.New([mr.NewLeaf(data[int(o):int(o + l)].tobytes()) for o, l in zip(off, lens)])
+        nodes = oracle.tree_from_digests(oracle.leaf_hashes(data, off, lens))
+        assert nodes[-1].tobytes() == t.Root.Data
+        assert oracle.bfs_image(nodes, n) == t.SerializeBytes()

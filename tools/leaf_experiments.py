@@ -1,0 +1,64 @@
+#!/usr/bin/env python3
+"""A/B experiments on the leaf kernel, interleaved rounds in one process.
+
+Each variant times nkv_tree_from_strided_dev (or the non-fused leaf kernel)
+with HIP events on the library's stream; prints median/min GB/s of payload.
+"""
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+from nakevaleng_amd import _lib  # noqa: E402
+
+
+def main():
+    L = _lib.lib()
+    ctx = _lib.Context(0)
+    s = torch.cuda.current_stream()
+    ctx.set_stream(s.cuda_stream)
+    big = torch.empty(2 * (1 << 20) * 4096, dtype=torch.uint8, device="cuda")
+    _lib.check(L.nkv_fill_splitmix64_dev(ctx.h, big.data_ptr(), big.numel(), 1))
+    nodes = torch.empty(L.nkv_total_nodes(8 << 20) * 20, dtype=torch.uint8, device="cuda")
+
+    def fused(n, stride, vlen):
+        return lambda: L.nkv_tree_from_strided_dev(ctx.h, big.data_ptr(), stride, vlen, n, nodes.data_ptr())
+
+    def leaf_only(n, stride, vlen):
+        return lambda: L.nkv_leaf_hash_strided_dev(ctx.h, big.data_ptr(), stride, vlen, n, nodes.data_ptr())
+
+    variants = {
+        "fused 1Mx4K": (fused(1 << 20, 4096, 4096), (1 << 20) * 4096),
+        "leafonly 1Mx4K": (leaf_only(1 << 20, 4096, 4096), (1 << 20) * 4096),
+        "fused 1Mx4K stride0 (L2-resident)": (fused(1 << 20, 0, 4096), (1 << 20) * 4096),
+        "fused 2Mx4K": (fused(2 << 20, 4096, 4096), (2 << 20) * 4096),
+        "fused 512Kx4K": (fused(1 << 19, 4096, 4096), (1 << 19) * 4096),
+        "fused 4Mx1K": (fused(4 << 20, 1024, 1024), (4 << 20) * 1024),
+        "fused 8Mx1K (8GiB)": (fused(8 << 20, 1024, 1024), (8 << 20) * 1024),
+    }
+    res = {k: [] for k in variants}
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    for fn, _ in variants.values():
+        _lib.check(fn())
+    torch.cuda.synchronize()
+    for _ in range(int(os.environ.get("ROUNDS", "5"))):
+        for k, (fn, nbytes) in variants.items():
+            e0.record(s)
+            for _ in range(3):
+                _lib.check(fn())
+            e1.record(s)
+            e1.synchronize()
+            ms = e0.elapsed_time(e1) / 3
+            res[k].append(nbytes / (ms * 1e-3) / 1e9)
+    for k, v in res.items():
+        print(f"{k:40s} median {statistics.median(v):8.1f} GB/s  max {max(v):8.1f}")
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

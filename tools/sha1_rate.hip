@@ -1,0 +1,70 @@
+// sha1_rate.hip -- compute-only ceiling of the per-lane SHA-1 compression
+// (nakevaleng_amd/csrc/sha1_dev.hpp) on the whole chip: no memory traffic,
+// message words in registers.  Prints SIMD-cycles per 64-byte block per wave
+// and the payload rate it would sustain (GB/s = blocks * 64 B / s).
+//   hipcc --offload-arch=gfx950 -O3 -I nakevaleng_amd/csrc tools/sha1_rate.hip -o tools/sha1_rate.bin
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include "sha1_dev.hpp"
+
+template <int WAVES>
+__global__ __launch_bounds__(256, WAVES) void k(uint32_t* out, unsigned long long* clk, int blocks) {
+    uint32_t h[5];
+    nkv::sha1_init(h);
+    uint32_t seed = blockIdx.x * 256 + threadIdx.x;
+    unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
+    for (int b = 0; b < blocks; ++b) {
+        uint32_t w[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) w[i] = nkv::bswap32(seed + i * 0x9E3779B9u + uint32_t(b));
+        nkv::sha1_compress(h, w);
+    }
+    unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
+    out[blockIdx.x * 256 + threadIdx.x] = h[0] ^ h[1] ^ h[2] ^ h[3] ^ h[4];
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        clk[0] = t1 - t0;
+        clk[1] = r1 - r0;
+    }
+}
+
+template <int WAVES>
+void run(int nblk_kernel, int blocks) {
+    uint32_t* out;
+    unsigned long long* clk;
+    (void)hipMalloc(&out, size_t(nblk_kernel) * 256 * 4);
+    (void)hipMalloc(&clk, 16);
+    hipLaunchKernelGGL(k<WAVES>, dim3(nblk_kernel), dim3(256), 0, 0, out, clk, blocks);
+    (void)hipDeviceSynchronize();
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    (void)hipEventRecord(e0);
+    hipLaunchKernelGGL(k<WAVES>, dim3(nblk_kernel), dim3(256), 0, 0, out, clk, blocks);
+    (void)hipEventRecord(e1);
+    (void)hipEventSynchronize(e1);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    unsigned long long c[2];
+    (void)hipMemcpy(c, clk, 16, hipMemcpyDeviceToHost);
+    const double ghz = double(c[0]) / (double(c[1]) / 100e6) / 1e9;
+    const double waves_per_simd = double(nblk_kernel) * 4 / 1024.0;
+    const double cyc = ms * 1e-3 * ghz * 1e9;
+    const double per_block = cyc / (waves_per_simd * blocks);
+    const double gbs = double(nblk_kernel) * 256 * blocks * 64.0 / (ms * 1e-3) / 1e9;
+    printf("waves/SIMD=%d grid=%6d  %.3f ms  clk %.2f GHz  %.0f SIMD-cycles per block per wave  %.0f GB/s\n",
+           WAVES, nblk_kernel, ms, ghz, per_block, gbs);
+    (void)hipFree(out);
+    (void)hipFree(clk);
+}
+
+int main() {
+    run<8>(2048, 4096);
+    run<8>(4096, 2048);
+    run<4>(1024, 4096);
+    run<2>(512, 4096);
+    return 0;
+}
