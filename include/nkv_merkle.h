@@ -78,6 +78,11 @@ void nkv_ctx_destroy(nkv_ctx *ctx);
 int nkv_ctx_set_stream(nkv_ctx *ctx, void *hip_stream);
 int nkv_ctx_use_own_stream(nkv_ctx *ctx);
 int nkv_ctx_sync(nkv_ctx *ctx);
+/* Tuning knobs (defaults are the measured-best settings). */
+#define NKV_OPT_LEAF_LOAD 1 /* leaf-kernel load path for 16-byte aligned values:
+                               1 = LDS-DMA stage, 2 = direct loads, 3 = direct non-temporal,
+                               4 / 5 = direct loads in 128 / 256-byte runs per lane */
+int nkv_ctx_set_option(nkv_ctx *ctx, int key, int64_t value);
 /* When enabled, the device-resident tree calls record HIP events around the
  * leaf kernel and the tree reduce on the context's stream. */
 int nkv_ctx_set_timing(nkv_ctx *ctx, int enable);

@@ -1,0 +1,393 @@
+// nkv_merkletree.hpp -- C++ mirror of the reference's ds/merkletree API over the
+// C-ABI in nkv_merkle.h (header-only; link libnkvmerkle.so).
+//
+// The reference is Go; this header is the same shim a cgo package would be
+// (INTEGRATION.md), written in C++ so it can be compiled and tested here.
+// Names and behaviour follow magley/nakevaleng (paths relative to its root):
+//
+//   MerkleNode, MERKLE_NODE_EMPTY   ds/merkletree/merklenode.go:11-19
+//   MerkleNode::String              merklenode.go:22-24
+//   NewLeaf                         merklenode.go:27-34  -- deferred: the value is copied
+//                                   into a pinned arena and hashed on the GPU by New()
+//                                   (or on first Resolve()), batched with its neighbours
+//   MerkleNode::Serialize           merklenode.go:37-63
+//   MerkleNode::Deserialize         merklenode.go:67-96  (returns true at EOF)
+//   MerkleTree, New                 merkletree.go:13-25  ("cannot build Merkle Tree from 0 nodes")
+//   MerkleTree::Serialize           merkletree.go:67-92  (O_WRONLY|O_CREAT, no O_TRUNC)
+//   MerkleTree::Deserialize         merkletree.go:97-157 (root only, as the reference)
+//   MerkleTree::Validate            merkletree.go:162-171 + merklenode.go:99-108
+//
+// Errors the reference panics on are thrown as std::runtime_error.  There is
+// no CPU hashing path: without a HIP device every hashing call throws.
+#pragma once
+
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <deque>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "nkv_merkle.h"
+
+namespace nkv {
+namespace merkletree {
+
+constexpr uint8_t MERKLE_NODE_EMPTY = NKV_MERKLE_NODE_EMPTY;
+
+inline void check(int rc, const char* what) {
+    if (rc != NKV_OK) throw std::runtime_error(std::string(what) + ": " + nkv_strerror(rc));
+}
+
+// One device context + the pinned arena that deferred NewLeaf values go to.
+class Session {
+   public:
+    explicit Session(int device = 0) {
+        check(nkv_ctx_create(device, &ctx_), "nkv_ctx_create");
+    }
+    ~Session() {
+        if (arena_) nkv_host_free(ctx_, arena_);
+        nkv_ctx_destroy(ctx_);
+    }
+    Session(const Session&) = delete;
+    Session& operator=(const Session&) = delete;
+
+    nkv_ctx* ctx() const { return ctx_; }
+
+    // The process-wide default session on device 0 (Go's package-level state).
+    static Session& Default() {
+        static Session s(0);
+        return s;
+    }
+
+    // ---- deferred leaves ----
+    struct Batch {
+        uint64_t epoch;
+        std::vector<uint64_t> off, len;
+        std::vector<uint8_t> digests;  // filled when resolved
+        bool resolved = false;
+    };
+
+    // Copies `data` into the arena; returns (batch, index).
+    std::pair<std::shared_ptr<Batch>, uint64_t> AddLeaf(const uint8_t* data, size_t n) {
+        if (!batch_ || batch_->resolved) {
+            batch_ = std::make_shared<Batch>();
+            batch_->epoch = ++epoch_;
+            used_ = 0;
+        }
+        Reserve(used_ + n);
+        if (n) std::memcpy(static_cast<uint8_t*>(arena_) + used_, data, n);
+        batch_->off.push_back(used_);
+        batch_->len.push_back(n);
+        used_ += n;
+        return {batch_, batch_->off.size() - 1};
+    }
+
+    const uint8_t* arena() const { return static_cast<const uint8_t*>(arena_); }
+
+    void ResolveBatch(Batch& b) {
+        if (b.resolved) return;
+        const uint64_t n = b.off.size();
+        b.digests.assign(20 * n, 0);
+        check(nkv_leaf_hash(ctx_, arena(), b.off.data(), b.len.data(), n, b.digests.data()), "NewLeaf");
+        b.resolved = true;
+    }
+
+   private:
+    void Reserve(uint64_t bytes) {
+        if (bytes <= cap_) return;
+        uint64_t want = cap_ ? cap_ * 2 : (uint64_t(1) << 20);
+        while (want < bytes) want *= 2;
+        void* p = nullptr;
+        check(nkv_host_alloc(ctx_, want, &p), "nkv_host_alloc");
+        if (arena_) {
+            std::memcpy(p, arena_, used_);
+            nkv_host_free(ctx_, arena_);
+        }
+        arena_ = p;
+        cap_ = want;
+    }
+
+    nkv_ctx* ctx_ = nullptr;
+    void* arena_ = nullptr;
+    uint64_t cap_ = 0, used_ = 0, epoch_ = 0;
+    std::shared_ptr<Batch> batch_;
+};
+
+struct MerkleNode {  // merklenode.go:15-19
+    std::vector<uint8_t> Data;
+    MerkleNode* Left = nullptr;
+    MerkleNode* Right = nullptr;
+
+    // deferred NewLeaf digest (resolved by New or Resolve)
+    std::shared_ptr<Session::Batch> pend;
+    uint64_t pend_idx = 0;
+
+    MerkleNode() = default;
+    explicit MerkleNode(std::vector<uint8_t> d) : Data(std::move(d)) {}
+
+    const std::vector<uint8_t>& Resolve() {
+        if (pend) {
+            Session::Default().ResolveBatch(*pend);
+            Data.assign(pend->digests.begin() + 20 * pend_idx, pend->digests.begin() + 20 * pend_idx + 20);
+            pend.reset();
+        }
+        return Data;
+    }
+
+    std::string String() {  // merklenode.go:22-24 (hex)
+        static const char* hx = "0123456789abcdef";
+        Resolve();
+        std::string s;
+        for (uint8_t b : Data) {
+            s.push_back(hx[b >> 4]);
+            s.push_back(hx[b & 15]);
+        }
+        return s;
+    }
+
+    void Serialize(std::vector<uint8_t>& w) {  // merklenode.go:37-63
+        Resolve();
+        if (Data.empty()) {
+            w.push_back(MERKLE_NODE_EMPTY);
+        } else {
+            w.push_back(0);
+            w.insert(w.end(), Data.begin(), Data.end());
+        }
+    }
+
+    // merklenode.go:67-96: true at EOF (a truncated node counts as EOF)
+    bool Deserialize(const uint8_t*& p, const uint8_t* end) {
+        if (p >= end) return true;
+        const uint8_t flags = *p++;
+        if (flags & MERKLE_NODE_EMPTY) {
+            Data.clear();
+        } else {
+            if (end - p < 20) return true;
+            Data.assign(p, p + 20);
+            p += 20;
+        }
+        pend.reset();
+        return false;
+    }
+};
+
+inline MerkleNode NewLeaf(const uint8_t* data, size_t n) {  // merklenode.go:27-34
+    MerkleNode m;
+    auto r = Session::Default().AddLeaf(data, n);
+    m.pend = r.first;
+    m.pend_idx = r.second;
+    m.Data.assign(20, 0);
+    return m;
+}
+inline MerkleNode NewLeaf(const std::vector<uint8_t>& v) { return NewLeaf(v.data(), v.size()); }
+inline MerkleNode NewLeaf(const std::string& v) {
+    return NewLeaf(reinterpret_cast<const uint8_t*>(v.data()), v.size());
+}
+
+inline std::vector<std::vector<uint8_t>> Sha1Many(const std::vector<std::vector<uint8_t>>& msgs);
+
+class MerkleTree {  // merkletree.go:13-15
+   public:
+    MerkleNode* Root = nullptr;
+
+    // merkletree.go:67-92: write the BFS image; O_WRONLY|O_CREAT without O_TRUNC
+    void Serialize(const std::string& fname) {
+        std::vector<uint8_t> img = SerializeBytes();
+        check(nkv_write_file(fname.c_str(), img.data(), img.size()), ("Serialize(" + fname + ")").c_str());
+    }
+
+    std::vector<uint8_t> SerializeBytes() {
+        std::vector<uint8_t> w;
+        std::deque<MerkleNode*> q{Root};
+        while (!q.empty()) {
+            MerkleNode* n = q.front();
+            q.pop_front();
+            if (n->Left) q.push_back(n->Left);
+            if (n->Right) q.push_back(n->Right);
+            n->Serialize(w);
+        }
+        return w;
+    }
+
+    // merkletree.go:97-157, including its quirk: the loop compares the node
+    // counter against the just-emptied queue and stops, so only the root is
+    // linked into the tree.
+    void Deserialize(const std::string& fname) {
+        FILE* f = std::fopen(fname.c_str(), "rb");
+        if (!f) throw std::runtime_error("open " + fname);
+        std::vector<uint8_t> blob;
+        uint8_t buf[1 << 16];
+        size_t k;
+        while ((k = std::fread(buf, 1, sizeof buf, f)) > 0) blob.insert(blob.end(), buf, buf + k);
+        std::fclose(f);
+        nodes_.clear();
+        const uint8_t* p = blob.data();
+        const uint8_t* end = p + blob.size();
+        while (true) {
+            MerkleNode n;
+            if (n.Deserialize(p, end)) break;
+            nodes_.push_back(std::move(n));
+        }
+        Root = nodes_.empty() ? nullptr : &nodes_.front();
+    }
+
+    // merkletree.go:162-171: recompute the root from the leaves' Data
+    bool Validate() {
+        if (!Root) throw std::runtime_error("Validate: nil root");
+        std::vector<uint8_t> h = Rehash(Root);
+        if (Root->Resolve().size() < 20 || h.size() < 20)
+            throw std::runtime_error("Validate: index out of range");
+        for (int i = 0; i < 20; ++i)
+            if (Root->Data[i] != h[i]) return false;
+        return true;
+    }
+
+    // every digest, level-major bottom-up (as the C-ABI returns it)
+    const std::vector<uint8_t>& Levels() const { return levels_; }
+
+    friend std::unique_ptr<MerkleTree> New(std::vector<MerkleNode> level, std::string* err);
+
+   private:
+    // merklenode.go:99-108 by depth on the device (pads make the tree ragged)
+    static std::vector<uint8_t> Rehash(MerkleNode* root) {
+        std::vector<std::vector<MerkleNode*>> lv{{root}};
+        while (true) {
+            std::vector<MerkleNode*> nx;
+            for (MerkleNode* n : lv.back()) {
+                if ((n->Left == nullptr) != (n->Right == nullptr))
+                    throw std::runtime_error("Validate: nil pointer dereference");
+                if (n->Left) {
+                    nx.push_back(n->Left);
+                    nx.push_back(n->Right);
+                }
+            }
+            if (nx.empty()) break;
+            lv.push_back(std::move(nx));
+        }
+        std::unordered_map<MerkleNode*, std::vector<uint8_t>> val;
+        for (size_t d = lv.size(); d-- > 0;) {
+            std::vector<std::vector<uint8_t>> msgs;
+            std::vector<MerkleNode*> owners;
+            for (MerkleNode* n : lv[d]) {
+                if (!n->Left) {
+                    val[n] = n->Resolve();
+                } else {
+                    std::vector<uint8_t> m = val[n->Left];
+                    const auto& r = val[n->Right];
+                    m.insert(m.end(), r.begin(), r.end());
+                    msgs.push_back(std::move(m));
+                    owners.push_back(n);
+                }
+            }
+            if (!msgs.empty()) {
+                auto dg = Sha1Many(msgs);
+                for (size_t i = 0; i < owners.size(); ++i) val[owners[i]] = std::move(dg[i]);
+            }
+        }
+        return val[root];
+    }
+
+    std::deque<MerkleNode> nodes_;  // owns every node of the tree (stable addresses)
+    std::vector<uint8_t> levels_;
+};
+
+inline std::vector<std::vector<uint8_t>> Sha1Many(const std::vector<std::vector<uint8_t>>& msgs) {
+    std::vector<uint8_t> flat;
+    std::vector<uint64_t> off, len;
+    for (const auto& m : msgs) {
+        off.push_back(flat.size());
+        len.push_back(m.size());
+        flat.insert(flat.end(), m.begin(), m.end());
+    }
+    flat.push_back(0);
+    std::vector<uint8_t> out(20 * msgs.size());
+    check(nkv_leaf_hash(Session::Default().ctx(), flat.data(), off.data(), len.data(), msgs.size(),
+                        out.data()),
+          "Validate");
+    std::vector<std::vector<uint8_t>> r;
+    for (size_t i = 0; i < msgs.size(); ++i) r.emplace_back(out.begin() + 20 * i, out.begin() + 20 * i + 20);
+    return r;
+}
+
+// merkletree.go:18-25 (+ build, :31-64).  Returns nullptr and sets *err to the
+// reference's error text for an empty level.
+inline std::unique_ptr<MerkleTree> New(std::vector<MerkleNode> level, std::string* err = nullptr) {
+    const uint64_t n = level.size();
+    if (n == 0) {
+        if (err) *err = "cannot build Merkle Tree from 0 nodes";
+        return nullptr;
+    }
+    nkv_ctx* ctx = Session::Default().ctx();
+    std::unique_ptr<MerkleTree> t(new MerkleTree());
+    const uint64_t total = nkv_total_nodes(n);
+    t->levels_.assign(20 * total, 0);
+    uint8_t* nodes = t->levels_.data();
+
+    // the flush / compaction pattern: n NewLeaf calls of one batch, in order
+    const auto& b0 = level[0].pend;
+    bool same_batch = b0 && !b0->resolved && b0->off.size() == n;
+    for (uint64_t i = 0; same_batch && i < n; ++i)
+        same_batch = level[i].pend == b0 && level[i].pend_idx == i && !level[i].Left && !level[i].Right;
+    if (same_batch) {
+        check(nkv_tree_from_values(ctx, Session::Default().arena(), b0->off.data(), b0->len.data(), n,
+                                   nullptr, nodes, nullptr),
+              "New");
+        b0->digests.assign(nodes, nodes + 20 * n);
+        b0->resolved = true;
+    } else {
+        bool all20 = true;
+        for (auto& x : level) all20 = all20 && x.Resolve().size() == 20;
+        if (all20) {
+            std::vector<uint8_t> leaf20;
+            for (auto& x : level) leaf20.insert(leaf20.end(), x.Data.begin(), x.Data.end());
+            check(nkv_tree_build(ctx, leaf20.data(), n, nullptr, nodes, nullptr), "New");
+        } else {
+            std::vector<uint8_t> flat;
+            std::vector<uint64_t> off, len;
+            for (auto& x : level) {
+                off.push_back(flat.size());
+                len.push_back(x.Data.size());
+                flat.insert(flat.end(), x.Data.begin(), x.Data.end());
+            }
+            flat.push_back(0);
+            check(nkv_tree_generic(ctx, flat.data(), off.data(), len.data(), n, nullptr, nodes + 20 * n,
+                                   nullptr),
+                  "New");
+        }
+    }
+    // materialize the pointer tree: copies of the given leaves (Go copies
+    // `l := level[i]`), then parents level by level with the empty pad node
+    auto& pool = t->nodes_;
+    std::vector<MerkleNode*> below;
+    for (auto& x : level) {
+        x.Resolve();
+        pool.push_back(x);
+        below.push_back(&pool.back());
+    }
+    const int lv = nkv_num_levels(n);
+    for (int L = 1; L < lv; ++L) {
+        if (below.size() % 2) {
+            pool.emplace_back();  // MerkleNode{Data: []byte{}} (merkletree.go:32-34)
+            below.push_back(&pool.back());
+        }
+        std::vector<MerkleNode*> cur;
+        const uint64_t s = nkv_level_start(n, L), c = nkv_level_count(n, L);
+        for (uint64_t i = 0; i < c; ++i) {
+            MerkleNode m(std::vector<uint8_t>(nodes + 20 * (s + i), nodes + 20 * (s + i) + 20));
+            m.Left = below[2 * i];
+            m.Right = below[2 * i + 1];
+            pool.push_back(std::move(m));
+            cur.push_back(&pool.back());
+        }
+        below.swap(cur);
+    }
+    t->Root = below[0];
+    return t;
+}
+
+}  // namespace merkletree
+}  // namespace nkv

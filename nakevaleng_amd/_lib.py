@@ -12,7 +12,7 @@ from typing import Optional
 import numpy as np
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-SO_PATH = os.path.join(_PKG, "libnkvmerkle.so")
+SO_PATH = os.environ.get("NKV_LIB", os.path.join(_PKG, "libnkvmerkle.so"))
 
 NKV_OK = 0
 NKV_ERR_EMPTY = 1
@@ -20,6 +20,7 @@ NKV_ERR_INVALID = 2
 NKV_ERR_DEVICE = 3
 NKV_ERR_NOMEM = 4
 NKV_ERR_IO = 5
+NKV_OPT_LEAF_LOAD = 1
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)
 _u64p = ctypes.POINTER(ctypes.c_uint64)
@@ -36,6 +37,7 @@ SIGNATURES = {
     "nkv_ctx_set_stream": (_int, [_vp, _vp]),
     "nkv_ctx_use_own_stream": (_int, [_vp]),
     "nkv_ctx_sync": (_int, [_vp]),
+    "nkv_ctx_set_option": (_int, [_vp, _int, ctypes.c_int64]),
     "nkv_ctx_set_timing": (_int, [_vp, _int]),
     "nkv_ctx_last_timing": (_int, [_vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
     "nkv_ctx_timing_summary": (_int, [_vp, ctypes.POINTER(_int), ctypes.POINTER(ctypes.c_float),
@@ -151,6 +153,9 @@ class Context:
 
     def set_stream(self, stream_handle: Optional[int]) -> None:
         check(lib().nkv_ctx_set_stream(self.h, stream_handle))
+
+    def set_option(self, key: int, value: int) -> None:
+        check(lib().nkv_ctx_set_option(self.h, key, value), f"nkv_ctx_set_option({key}, {value})")
 
     def sync(self) -> None:
         check(lib().nkv_ctx_sync(self.h))

@@ -22,20 +22,27 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not _stale():
+DIAG_SO = os.path.join(PKG, "libnkvmerkle_diag.so")
+
+
+def build(force: bool = False, verbose: bool = False, diag: bool = False) -> str:
+    """diag=True builds the stamp-instrumented library (tools/diag_timeline.py only)."""
+    so = DIAG_SO if diag else SO
+    if not force and not diag and not _stale():
         return SO
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    tmp = SO + ".tmp"
+    tmp = so + ".tmp"
     cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-Wall", "-Wno-unused-result", "-I", os.path.join(ROOT, "include"), "-I", CSRC]
+    if diag:
+        cmd.append("-DNKV_DIAG")
     cmd += [os.path.join(CSRC, f) for f in SOURCES] + ["-o", tmp]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.check_call(cmd)
-    os.replace(tmp, SO)
-    return SO
+    os.replace(tmp, so)
+    return so
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    print(build(force="--force" in sys.argv, verbose=True, diag="--diag" in sys.argv))

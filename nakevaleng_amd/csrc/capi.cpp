@@ -95,6 +95,7 @@ struct nkv_ctx {
     int device = 0;
     hipStream_t own = nullptr;
     hipStream_t stream = nullptr;
+    int leaf_load = 1;  // NKV_OPT_LEAF_LOAD
     bool timing = false;
     bool timed = false;
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
@@ -237,9 +238,9 @@ int tree_from_device_values(nkv_ctx* c, const uint8_t* base, const uint64_t* off
                             const uint64_t* len, uint64_t n, bool aligned, uint8_t* nodes) {
     const int top = levels_of(n) - 1;
     TRY(mark(c, 0));
-    HIPTRY(launch_leaf_offsets(base, off, len, nullptr, n, top, true, aligned, nodes, c->stream));
+    HIPTRY(launch_leaf_offsets(base, off, len, nullptr, n, top, true, aligned, c->leaf_load, nodes, c->stream));
     TRY(mark(c, 1));
-    HIPTRY(launch_reduce(nodes, n, std::min(top, kFuseLevels), top, c->stream));
+    HIPTRY(launch_reduce(nodes, n, std::min(top, kWaveLevels), top, c->stream));
     return mark(c, 2);
 }
 
@@ -316,6 +317,18 @@ int nkv_ctx_use_own_stream(nkv_ctx* c) {
     TRY(bind(c));
     c->stream = c->own;
     return NKV_OK;
+}
+
+int nkv_ctx_set_option(nkv_ctx* c, int key, int64_t value) {
+    TRY(bind(c));
+    switch (key) {
+        case NKV_OPT_LEAF_LOAD:
+            if (value < 1 || value > 5) return NKV_ERR_INVALID;
+            c->leaf_load = int(value);
+            return NKV_OK;
+        default:
+            return NKV_ERR_INVALID;
+    }
 }
 
 int nkv_ctx_sync(nkv_ctx* c) {
@@ -401,7 +414,7 @@ int nkv_leaf_hash(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const ui
     uint8_t* nodes = static_cast<uint8_t*>(c->d_nodes.p);
     HIPTRY(launch_leaf_offsets(static_cast<const uint8_t*>(c->d_data.p),
                                static_cast<const uint64_t*>(c->d_off.p),
-                               static_cast<const uint64_t*>(c->d_len.p), nullptr, n, 0, false, true,
+                               static_cast<const uint64_t*>(c->d_len.p), nullptr, n, 0, false, true, c->leaf_load,
                                nodes, c->stream));
     HIPTRY(hipMemcpyAsync(out20, nodes, 20 * n, hipMemcpyDeviceToHost, c->stream));
     return st(hipStreamSynchronize(c->stream));
@@ -478,7 +491,7 @@ int nkv_tree_generic(nkv_ctx* c, const uint8_t* data, const uint64_t* off, const
     HIPTRY(launch_leaf_offsets(static_cast<const uint8_t*>(c->d_data.p),
                                static_cast<const uint64_t*>(c->d_off.p),
                                static_cast<const uint64_t*>(c->d_len.p), nullptr, n1, 0, false,
-                               true, up, c->stream));
+                               true, c->leaf_load, up, c->stream));
     if (n1 > 1) HIPTRY(launch_reduce(up, n1, 0, levels_of(n1) - 1, c->stream));
     if (upper_out)
         HIPTRY(hipMemcpyAsync(upper_out, up, 20 * up_total, hipMemcpyDeviceToHost, c->stream));
@@ -570,7 +583,8 @@ int nkv_leaf_hash_dev(nkv_ctx* c, const void* d_base, const uint64_t* d_off,
     if (n == 0) return NKV_OK;
     if (!d_base || !d_off || !d_len || !d_nodes) return NKV_ERR_INVALID;
     return st(launch_leaf_offsets(static_cast<const uint8_t*>(d_base), d_off, d_len, nullptr, n, 0,
-                                  false, false, static_cast<uint8_t*>(d_nodes), c->stream));
+                                  false, false, c->leaf_load, static_cast<uint8_t*>(d_nodes),
+                                  c->stream));
 }
 
 int nkv_leaf_hash_strided_dev(nkv_ctx* c, const void* d_base, uint64_t stride, uint64_t len,
@@ -579,7 +593,7 @@ int nkv_leaf_hash_strided_dev(nkv_ctx* c, const void* d_base, uint64_t stride, u
     if (n == 0) return NKV_OK;
     if (!d_base || !d_nodes) return NKV_ERR_INVALID;
     return st(launch_leaf_strided(static_cast<const uint8_t*>(d_base), stride, len, n, 0, false,
-                                  static_cast<uint8_t*>(d_nodes), c->stream));
+                                  c->leaf_load, static_cast<uint8_t*>(d_nodes), c->stream));
 }
 
 int nkv_tree_reduce_dev(nkv_ctx* c, void* d_nodes, uint64_t n) {
@@ -607,9 +621,9 @@ int nkv_tree_from_strided_dev(nkv_ctx* c, const void* d_base, uint64_t stride, u
     const int top = levels_of(n) - 1;
     TRY(mark(c, 0));
     HIPTRY(launch_leaf_strided(static_cast<const uint8_t*>(d_base), stride, len, n, top, true,
-                               nodes, c->stream));
+                               c->leaf_load, nodes, c->stream));
     TRY(mark(c, 1));
-    HIPTRY(launch_reduce(nodes, n, std::min(top, kFuseLevels), top, c->stream));
+    HIPTRY(launch_reduce(nodes, n, std::min(top, kWaveLevels), top, c->stream));
     return mark(c, 2);
 }
 

@@ -7,6 +7,7 @@ namespace nkv {
 
 constexpr int kBlock = 256;       // threads per workgroup = leaves per K1 block
 constexpr int kFuseLevels = 8;    // log2(kBlock): levels one workgroup reduces in LDS
+constexpr int kWaveLevels = 6;    // log2(64): levels the leaf kernel's waves reduce by shuffles
 constexpr int kMaxLevels = 64;
 #ifndef NKV_LEAF_WAVES
 #define NKV_LEAF_WAVES 8
@@ -22,11 +23,13 @@ struct BfsLayout {
     uint64_t count[kMaxLevels];       // real nodes in the level
 };
 
+// load: leaf-kernel load path for aligned values (1 LDS-DMA, 2 direct, 3 direct
+// non-temporal); unaligned values always take the register funnel (0).
 hipError_t launch_leaf_strided(const uint8_t* base, uint64_t stride, uint64_t L, uint64_t n,
-                               int top, bool fuse, uint8_t* nodes, hipStream_t s);
+                               int top, bool fuse, int load, uint8_t* nodes, hipStream_t s);
 hipError_t launch_leaf_offsets(const uint8_t* base, const uint64_t* off, const uint64_t* len,
                                const uint32_t* perm, uint64_t n, int top, bool fuse, bool aligned,
-                               uint8_t* nodes, hipStream_t s);
+                               int load, uint8_t* nodes, hipStream_t s);
 hipError_t launch_reduce(uint8_t* nodes, uint64_t n, int from_level, int top, hipStream_t s);
 hipError_t launch_hash_messages(const uint8_t* base, const uint64_t* off, const uint64_t* len,
                                 uint64_t n, uint8_t* out, hipStream_t s);

@@ -23,6 +23,24 @@
 
 namespace nkv {
 
+#ifdef NKV_DIAG
+// Diagnostic build only (tools/diag_timeline.py): per-wave s_memtime /
+// s_memrealtime stamps, never part of an output.
+__device__ unsigned long long* g_diag = nullptr;
+#define NKV_STAMP(slot)                                                                 \
+    do {                                                                                \
+        if (g_diag && (threadIdx.x & 63) == 0) {                                        \
+            const size_t w_ = size_t(blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6);   \
+            g_diag[w_ * 8 + 2 * (slot)] = __builtin_amdgcn_s_memrealtime();             \
+            g_diag[w_ * 8 + 2 * (slot) + 1] = __builtin_amdgcn_s_memtime();             \
+        }                                                                               \
+    } while (0)
+#else
+#define NKV_STAMP(slot) \
+    do {                \
+    } while (0)
+#endif
+
 // ---------------------------------------------------------------------------
 // tree shape helpers (device side; host side mirrors them in capi.cpp)
 
@@ -84,6 +102,40 @@ __device__ __forceinline__ void subtree_reduce(uint32_t (*lds)[kBlock], uint64_t
 #pragma unroll
             for (int k = 0; k < 5; ++k) lds[k][tid] = out[k];
             store_digest(nodes, start_cur + lo_cur + tid, out);
+        }
+        nprev = ncur;
+        start_cur += ncur;
+        lo_prev = lo_cur;
+    }
+}
+
+// Subtree reduce inside one wavefront, no workgroup barrier: lane t holds
+// (state words of) node lo + t of level 0, t < 64; levels 1..jmax (<= 6) are
+// built with cross-lane shuffles and written to the global nodes buffer.
+// Used as the leaf kernel's epilogue so a finished wave never waits for the
+// other waves of its workgroup.
+__device__ __forceinline__ void wave_reduce(uint32_t h[5], uint64_t n, int jmax, uint64_t lo,
+                                            uint8_t* nodes) {
+    const int lane = threadIdx.x & 63;
+    uint64_t nprev = n;
+    uint64_t start_cur = n;
+    uint64_t lo_prev = lo;
+    int span = 64;
+    for (int j = 1; j <= jmax; ++j) {
+        const uint64_t ncur = ((nprev - 1) >> 1) + 1;
+        const uint64_t lo_cur = lo_prev >> 1;
+        span >>= 1;
+        const int src = (2 * lane) & 63;
+        uint32_t l[5], r[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            l[k] = uint32_t(__shfl(int(h[k]), src));
+            r[k] = uint32_t(__shfl(int(h[k]), src + 1));
+        }
+        if (lane < span && lo_cur + lane < ncur) {
+            const bool lone = (2 * (lo_cur + lane) + 1) >= nprev;
+            sha1_parent(l, r, lone, h);
+            store_digest(nodes, start_cur + lo_cur + lane, h);
         }
         nprev = ncur;
         start_cur += ncur;
@@ -274,11 +326,60 @@ __device__ __forceinline__ void sha1_blocks_lds(const uint8_t* wbuf, uint32_t nm
     }
 }
 
+// Full blocks straight from HBM into registers, 4 x global_load_dwordx4 per
+// block and lane (no LDS stage, no prefetch: the other resident waves cover
+// the load latency).  NT: non-temporal loads (read-once data).
+template <bool NT>
+__device__ __forceinline__ void sha1_blocks_direct(const uint8_t* p, uint32_t nfull, uint32_t h[5]) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4* q = reinterpret_cast<const u32x4*>(p);
+    uint32_t w[16];
+    for (uint32_t b = 0; b < nfull; ++b) {
+        uint4 c[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const u32x4 v = NT ? __builtin_nontemporal_load(q + 4 * b + i) : q[4 * b + i];
+            c[i] = make_uint4(v.x, v.y, v.z, v.w);
+        }
+        be16_from_raw(c, w);
+        sha1_compress(h, w);
+    }
+}
+
+// Full blocks in runs of S blocks: each lane loads S*64 contiguous bytes of its
+// value (4S x global_load_dwordx4) before compressing them, so every request
+// stream touches a DRAM page for a longer run.
+template <int S>
+__device__ __forceinline__ void sha1_blocks_runs(const uint8_t* p, uint32_t nfull, uint32_t h[5]) {
+    const uint4* q = reinterpret_cast<const uint4*>(p);
+    uint32_t w[16];
+    uint32_t b = 0;
+    for (; b + S <= nfull; b += S) {
+        uint4 c[4 * S];
+#pragma unroll
+        for (int i = 0; i < 4 * S; ++i) c[i] = q[4 * b + i];
+#pragma unroll
+        for (int j = 0; j < S; ++j) {
+            be16_from_raw(c + 4 * j, w);
+            sha1_compress(h, w);
+        }
+    }
+    for (; b < nfull; ++b) {
+        uint4 c[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) c[i] = q[4 * b + i];
+        be16_from_raw(c, w);
+        sha1_compress(h, w);
+    }
+}
+
 // MODE 0: value i at base + i*stride, length L.  MODE 1: base + off[i], len[i].
 // perm (MODE 1 only, nullable): lane i hashes leaf perm[i] (length bucketing).
 // FUSE: also build levels 1..min(8, top) of this block's subtree.
-template <int MODE, bool FUSE, bool ALIGNED>
-__global__ __launch_bounds__(kBlock, kLeafWavesPerSimd) void k_leaf(const uint8_t* __restrict__ base,
+// LOAD: 0 = any alignment (register funnel); 1 = 16-byte aligned, LDS-DMA
+// stage; 2 = aligned, direct loads; 3 = aligned, direct non-temporal loads.
+template <int MODE, bool FUSE, int LOAD>
+__global__ __launch_bounds__(kBlock, LOAD >= 4 ? 4 : kLeafWavesPerSimd) void k_leaf(const uint8_t* __restrict__ base,
                                                   const uint64_t* __restrict__ off,
                                                   const uint64_t* __restrict__ len, uint64_t stride,
                                                   uint64_t L, const uint32_t* __restrict__ perm,
@@ -287,6 +388,7 @@ __global__ __launch_bounds__(kBlock, kLeafWavesPerSimd) void k_leaf(const uint8_
     // fused subtree reduce (5 x 256 words).
     __shared__ __attribute__((aligned(16))) uint8_t smem[kBlock * 64];
     uint32_t(*lds)[kBlock] = reinterpret_cast<uint32_t(*)[kBlock]>(smem);
+    NKV_STAMP(0);
     const uint64_t g = blockIdx.x;
     const uint64_t t = g * kBlock + threadIdx.x;
     uint32_t h[5] = {0u, 0u, 0u, 0u, 0u};
@@ -304,7 +406,17 @@ __global__ __launch_bounds__(kBlock, kLeafWavesPerSimd) void k_leaf(const uint8_
             ln = len[leaf];
         }
     }
-    if (ALIGNED) {
+    if (LOAD >= 2) {
+        sha1_init(h);
+        if (live) {
+            if (LOAD == 2) sha1_blocks_direct<false>(p, uint32_t(ln >> 6), h);
+            else if (LOAD == 3) sha1_blocks_direct<true>(p, uint32_t(ln >> 6), h);
+            else if (LOAD == 4) sha1_blocks_runs<2>(p, uint32_t(ln >> 6), h);
+            else sha1_blocks_runs<4>(p, uint32_t(ln >> 6), h);
+            sha1_tail<true>(p, ln, h);
+            store_digest(nodes, leaf, h);
+        }
+    } else if (LOAD == 1) {
         // wave-cooperative LDS-DMA stream of the full blocks, then the tail
         const int lane = threadIdx.x & 63;
         const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -355,13 +467,22 @@ __global__ __launch_bounds__(kBlock, kLeafWavesPerSimd) void k_leaf(const uint8_
         sha1_value<false>(p, ln, h);
         store_digest(nodes, leaf, h);
     }
+    NKV_STAMP(1);
     if (FUSE) {
-        __syncthreads();  // every wave is done with its DMA stage
-#pragma unroll
-        for (int k = 0; k < 5; ++k) lds[k][threadIdx.x] = h[k];
-        const int jmax = top < kFuseLevels ? top : kFuseLevels;
-        subtree_reduce(lds, n, 0, jmax, g * kBlock, nodes);
+        const int jmax = top < kWaveLevels ? top : kWaveLevels;
+        wave_reduce(h, n, jmax, g * kBlock + 64 * (threadIdx.x >> 6), nodes);
     }
+    NKV_STAMP(2);
+#ifdef NKV_DIAG
+    if (g_diag && (threadIdx.x & 63) == 0) {
+        unsigned xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        unsigned hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        const size_t w_ = size_t(blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6);
+        g_diag[w_ * 8 + 6] = (uint64_t(xcc) << 32) | hw;
+    }
+#endif
 }
 
 // K2: reduce one level j0 (already in nodes) up to min(j0 + 8, top).
@@ -495,32 +616,43 @@ __global__ __launch_bounds__(kBlock) void k_fill(uint8_t* __restrict__ buf, uint
 
 static inline unsigned grid_for(uint64_t n) { return unsigned((n + kBlock - 1) / kBlock); }
 
-template <int MODE, bool FUSE, bool ALIGNED>
+template <int MODE, bool FUSE, int LOAD>
 static void leaf_kernel(const uint8_t* base, const uint64_t* off, const uint64_t* len,
                         uint64_t stride, uint64_t L, const uint32_t* perm, uint64_t n, int top,
                         uint8_t* nodes, hipStream_t s) {
-    hipLaunchKernelGGL((k_leaf<MODE, FUSE, ALIGNED>), dim3(grid_for(n)), dim3(kBlock), 0, s, base,
+    hipLaunchKernelGGL((k_leaf<MODE, FUSE, LOAD>), dim3(grid_for(n)), dim3(kBlock), 0, s, base,
                        off, len, stride, L, perm, n, top, nodes);
 }
 
+template <int MODE, bool FUSE>
+static void leaf_dispatch(int load, const uint8_t* base, const uint64_t* off, const uint64_t* len,
+                          uint64_t stride, uint64_t L, const uint32_t* perm, uint64_t n, int top,
+                          uint8_t* nodes, hipStream_t s) {
+    switch (load) {
+        case 1: leaf_kernel<MODE, FUSE, 1>(base, off, len, stride, L, perm, n, top, nodes, s); break;
+        case 2: leaf_kernel<MODE, FUSE, 2>(base, off, len, stride, L, perm, n, top, nodes, s); break;
+        case 3: leaf_kernel<MODE, FUSE, 3>(base, off, len, stride, L, perm, n, top, nodes, s); break;
+        case 4: leaf_kernel<MODE, FUSE, 4>(base, off, len, stride, L, perm, n, top, nodes, s); break;
+        case 5: leaf_kernel<MODE, FUSE, 5>(base, off, len, stride, L, perm, n, top, nodes, s); break;
+        default: leaf_kernel<MODE, FUSE, 0>(base, off, len, stride, L, perm, n, top, nodes, s); break;
+    }
+}
+
 hipError_t launch_leaf_strided(const uint8_t* base, uint64_t stride, uint64_t L, uint64_t n,
-                               int top, bool fuse, uint8_t* nodes, hipStream_t s) {
+                               int top, bool fuse, int load, uint8_t* nodes, hipStream_t s) {
     const bool al = ((reinterpret_cast<uintptr_t>(base) | stride) & 15) == 0;
-    if (fuse && al) leaf_kernel<0, true, true>(base, nullptr, nullptr, stride, L, nullptr, n, top, nodes, s);
-    else if (fuse) leaf_kernel<0, true, false>(base, nullptr, nullptr, stride, L, nullptr, n, top, nodes, s);
-    else if (al) leaf_kernel<0, false, true>(base, nullptr, nullptr, stride, L, nullptr, n, top, nodes, s);
-    else leaf_kernel<0, false, false>(base, nullptr, nullptr, stride, L, nullptr, n, top, nodes, s);
+    if (!al) load = 0;
+    if (fuse) leaf_dispatch<0, true>(load, base, nullptr, nullptr, stride, L, nullptr, n, top, nodes, s);
+    else leaf_dispatch<0, false>(load, base, nullptr, nullptr, stride, L, nullptr, n, top, nodes, s);
     return hipGetLastError();
 }
 
 hipError_t launch_leaf_offsets(const uint8_t* base, const uint64_t* off, const uint64_t* len,
                                const uint32_t* perm, uint64_t n, int top, bool fuse, bool aligned,
-                               uint8_t* nodes, hipStream_t s) {
-    const bool f = fuse && !perm;
-    if (f && aligned) leaf_kernel<1, true, true>(base, off, len, 0, 0, nullptr, n, top, nodes, s);
-    else if (f) leaf_kernel<1, true, false>(base, off, len, 0, 0, nullptr, n, top, nodes, s);
-    else if (aligned) leaf_kernel<1, false, true>(base, off, len, 0, 0, perm, n, top, nodes, s);
-    else leaf_kernel<1, false, false>(base, off, len, 0, 0, perm, n, top, nodes, s);
+                               int load, uint8_t* nodes, hipStream_t s) {
+    if (!aligned) load = 0;
+    if (fuse && !perm) leaf_dispatch<1, true>(load, base, off, len, 0, 0, nullptr, n, top, nodes, s);
+    else leaf_dispatch<1, false>(load, base, off, len, 0, 0, perm, n, top, nodes, s);
     return hipGetLastError();
 }
 
@@ -563,6 +695,13 @@ hipError_t scan_exclusive_u64(const uint64_t* in, uint64_t* out, uint64_t n, voi
                               size_t* tmp_bytes, hipStream_t s) {
     return hipcub::DeviceScan::ExclusiveSum(tmp, *tmp_bytes, in, out, int(n), s);
 }
+
+#ifdef NKV_DIAG
+extern "C" int nkv_diag_set_buffer(void* d) {
+    unsigned long long* p = static_cast<unsigned long long*>(d);
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_diag), &p, sizeof(p)) == hipSuccess ? 0 : 3;
+}
+#endif
 
 hipError_t launch_fill(uint8_t* buf, uint64_t nbytes, uint64_t seed, hipStream_t s) {
     uint64_t threads = (nbytes + 15) / 16;

@@ -43,6 +43,19 @@ __device__ __forceinline__ uint32_t be_word(uint32_t hi, uint32_t lo, uint32_t s
     return __builtin_amdgcn_perm(hi, lo, sel);
 }
 
+// v_add3_u32 as an opaque (but non-volatile, freely schedulable) instruction,
+// so the association below survives instruction selection.
+__device__ __forceinline__ uint32_t add3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_add3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ uint32_t add3k(uint32_t a, uint32_t b, uint32_t k) {
+    uint32_t r;
+    asm("v_add3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(k));
+    return r;
+}
+
 __device__ __forceinline__ void sha1_init(uint32_t h[5]) {
     h[0] = 0x67452301u;
     h[1] = 0xEFCDAB89u;
@@ -78,7 +91,14 @@ __device__ __forceinline__ void sha1_compress(uint32_t h[5], uint32_t w[16]) {
             f = xor3(b, c, d);
             k = 0xCA62C1D6u;
         }
+#ifdef NKV_SHA1_ADD_CHAIN3
         uint32_t tmp = rotl(a, 5) + f + e + k + wt;
+#else
+        // e + W + K does not depend on this round's a/b, so the critical path
+        // through a round is two ops (rotl5 or f, then one add3)
+        const uint32_t ewk = add3k(e, wt, k);
+        const uint32_t tmp = add3(rotl(a, 5), f, ewk);
+#endif
         e = d;
         d = c;
         c = rotl(b, 30);

@@ -1,0 +1,91 @@
+// Drives the C++ ds/merkletree mirror (include/nkv_merkletree.hpp) through the
+// C-ABI on the GPU and prints "key value" lines that tests/test_cpp_api.py checks
+// against the golden fixtures and the oracle.
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "nkv_merkletree.hpp"
+
+using nkv::merkletree::MerkleNode;
+using nkv::merkletree::MerkleTree;
+using nkv::merkletree::New;
+using nkv::merkletree::NewLeaf;
+
+static std::string hex(const std::vector<uint8_t>& v) {
+    static const char* h = "0123456789abcdef";
+    std::string s;
+    for (uint8_t b : v) {
+        s.push_back(h[b >> 4]);
+        s.push_back(h[b & 15]);
+    }
+    return s;
+}
+
+static std::vector<uint8_t> splitmix64_bytes(size_t n, uint64_t seed) {
+    std::vector<uint8_t> out(n);
+    for (size_t j = 0; j < n; j += 8) {
+        uint64_t z = seed + (j / 8 + 1) * 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        z ^= z >> 31;
+        for (size_t b = 0; b < 8 && j + b < n; ++b) out[j + b] = uint8_t(z >> (8 * b));
+    }
+    return out;
+}
+
+int main(int argc, char** argv) {
+    const std::string dir = argc > 1 ? argv[1] : "/tmp";
+    // README example (ds/merkletree/README.md:44-57)
+    {
+        std::vector<MerkleNode> lv;
+        for (int i = 1; i <= 7; ++i) lv.emplace_back(std::vector<uint8_t>{uint8_t('0' + i)});
+        auto t = New(lv);
+        std::printf("readme_root %s\n", t->Root->String().c_str());
+        std::printf("readme_bfs %s\n", hex(t->SerializeBytes()).c_str());
+        std::printf("readme_validate %d\n", int(t->Validate()));
+        t->Serialize(dir + "/readme-1-0-metadata.db");
+        MerkleTree t2;
+        t2.Deserialize(dir + "/readme-1-0-metadata.db");
+        std::printf("readme_deser_root %s\n", t2.Root->String().c_str());
+        std::printf("readme_deser_children %d\n", int(t2.Root->Left != nullptr || t2.Root->Right != nullptr));
+        std::printf("readme_deser_validate %d\n", int(t2.Validate()));
+    }
+    // empty level: the reference's error
+    {
+        std::string err;
+        auto t = New({}, &err);
+        std::printf("empty_null %d\n", int(t == nullptr));
+        std::printf("empty_err %s\n", err.c_str());
+    }
+    // the flush pattern: NewLeaf per value, then New, then Serialize
+    for (uint64_t n : {1ull, 2ull, 3ull, 255ull, 256ull, 257ull, 1000ull, 1025ull}) {
+        const size_t vlen = n > 300 ? 64 : 100;
+        auto data = splitmix64_bytes(n * vlen, 0x6E616B65ull + n);
+        std::vector<MerkleNode> leaves;
+        for (uint64_t i = 0; i < n; ++i) leaves.push_back(NewLeaf(data.data() + i * vlen, vlen));
+        auto t = New(leaves);
+        auto img = t->SerializeBytes();
+        std::printf("tree%llu_root %s\n", (unsigned long long)n, t->Root->String().c_str());
+        std::printf("tree%llu_bfs_len %zu\n", (unsigned long long)n, img.size());
+        std::printf("tree%llu_bfs_head %s\n", (unsigned long long)n,
+                    hex(std::vector<uint8_t>(img.begin(), img.begin() + std::min<size_t>(64, img.size()))).c_str());
+        std::printf("tree%llu_validate %d\n", (unsigned long long)n, int(t->Validate()));
+        if (n == 1000) {
+            // corrupt one leaf of the materialized tree: Validate must fail
+            MerkleNode* leaf = t->Root;
+            while (leaf->Left) leaf = leaf->Left;
+            leaf->Data.assign(20, 0);
+            std::printf("tree1000_corrupt_validate %d\n", int(t->Validate()));
+        }
+    }
+    // leaf Data read before New resolves the pending batch on the GPU
+    {
+        std::vector<MerkleNode> lv;
+        for (int i = 0; i < 10; ++i) lv.push_back(NewLeaf(std::string(size_t(i) * 7, char('a' + i))));
+        std::printf("early_leaf3 %s\n", lv[3].String().c_str());
+        auto t = New(lv);
+        std::printf("early_root %s\n", t->Root->String().c_str());
+    }
+    return 0;
+}

@@ -1,0 +1,54 @@
+"""The C++ ds/merkletree mirror (include/nkv_merkletree.hpp): compiles on CPU;
+on the GPU its outputs match the golden fixtures and the oracle."""
+import hashlib
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "tests", "cpp", "test_merkletree_api.cpp")
+GOLDEN = json.load(open(os.path.join(ROOT, "tests", "golden", "merkle_golden.json")))
+
+
+def build_binary(tmpdir):
+    from nakevaleng_amd import build as b
+    so = b.build()
+    out = os.path.join(tmpdir, "test_merkletree_api")
+    libdir = os.path.dirname(so)
+    subprocess.check_call(["g++", "-std=c++17", "-O2", "-Wall", "-I", os.path.join(ROOT, "include"), SRC,
+                           "-L", libdir, "-lnkvmerkle", f"-Wl,-rpath,{libdir}", "-o", out])
+    return out
+
+
+def test_cpp_mirror_compiles(tmp_path):
+    assert os.path.exists(build_binary(str(tmp_path)))
+
+
+@pytest.mark.gpu
+def test_cpp_mirror_on_gpu(tmp_path, oracle):
+    exe = build_binary(str(tmp_path))
+    out = subprocess.run([exe, str(tmp_path)], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    kv = dict(line.split(" ", 1) for line in out.stdout.strip().splitlines())
+    g = GOLDEN["readme"]
+    assert kv["readme_root"] == g["root"]
+    assert kv["readme_bfs"] == g["bfs_hex"]
+    assert kv["readme_validate"] == "1"
+    assert kv["readme_deser_root"] == g["root"] and kv["readme_deser_children"] == "0"
+    assert kv["readme_deser_validate"] == "1"
+    assert kv["empty_null"] == "1" and kv["empty_err"] == "cannot build Merkle Tree from 0 nodes"
+    trees = {c["n"]: c for c in GOLDEN["trees"] if c["value_bytes"] in (64, 100)}
+    for n in (1, 2, 3, 255, 256, 257, 1000, 1025):
+        c = trees[n]
+        assert kv[f"tree{n}_root"] == c["root"]
+        assert int(kv[f"tree{n}_bfs_len"]) == c["bfs_len"]
+        assert kv[f"tree{n}_bfs_head"] == c["bfs_head_hex"]
+        assert kv[f"tree{n}_validate"] == "1"
+    assert kv["tree1000_corrupt_validate"] == "0"
+    vals = [bytes([ord("a") + i]) * (7 * i) for i in range(10)]
+    assert kv["early_leaf3"] == hashlib.sha1(vals[3]).hexdigest()
+    want = oracle.tree_from_digests(np.frombuffer(b"".join(hashlib.sha1(v).digest() for v in vals), np.uint8))
+    assert kv["early_root"] == want[-1].tobytes().hex()

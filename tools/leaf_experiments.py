@@ -31,15 +31,19 @@ def main():
     def leaf_only(n, stride, vlen):
         return lambda: L.nkv_leaf_hash_strided_dev(ctx.h, big.data_ptr(), stride, vlen, n, nodes.data_ptr())
 
-    variants = {
-        "fused 1Mx4K": (fused(1 << 20, 4096, 4096), (1 << 20) * 4096),
-        "leafonly 1Mx4K": (leaf_only(1 << 20, 4096, 4096), (1 << 20) * 4096),
-        "fused 1Mx4K stride0 (L2-resident)": (fused(1 << 20, 0, 4096), (1 << 20) * 4096),
-        "fused 2Mx4K": (fused(2 << 20, 4096, 4096), (2 << 20) * 4096),
-        "fused 512Kx4K": (fused(1 << 19, 4096, 4096), (1 << 19) * 4096),
-        "fused 4Mx1K": (fused(4 << 20, 1024, 1024), (4 << 20) * 1024),
-        "fused 8Mx1K (8GiB)": (fused(8 << 20, 1024, 1024), (8 << 20) * 1024),
-    }
+    def with_load(mode, fn):
+        def run():
+            ctx.set_option(_lib.NKV_OPT_LEAF_LOAD, mode)
+            return fn()
+        return run
+
+    M = 1 << 20
+    variants = {}
+    for mode, name in ((1, "lds-dma"), (2, "direct"), (4, "runs128"), (5, "runs256")):
+        variants[f"{name:10s} fused 1Mx4K"] = (with_load(mode, fused(M, 4096, 4096)), M * 4096)
+        variants[f"{name:10s} leafonly 1Mx4K"] = (with_load(mode, leaf_only(M, 4096, 4096)), M * 4096)
+        variants[f"{name:10s} fused 1Mx4K stride0"] = (with_load(mode, fused(M, 0, 4096)), M * 4096)
+        variants[f"{name:10s} fused 4Mx1K"] = (with_load(mode, fused(4 * M, 1024, 1024)), 4 * M * 1024)
     res = {k: [] for k in variants}
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)

@@ -9,8 +9,11 @@
 
 #include "sha1_dev.hpp"
 
-template <int WAVES>
-__global__ __launch_bounds__(256, WAVES) void k(uint32_t* out, unsigned long long* clk, int blocks) {
+// LOADS: message words read from a 64 KiB L2-resident buffer (per-lane 64-byte
+// rows) instead of being generated in registers.
+template <int WAVES, bool LOADS = false>
+__global__ __launch_bounds__(256, WAVES) void k(uint32_t* out, unsigned long long* clk, int blocks,
+                                                const uint4* src = nullptr) {
     uint32_t h[5];
     nkv::sha1_init(h);
     uint32_t seed = blockIdx.x * 256 + threadIdx.x;
@@ -18,8 +21,20 @@ __global__ __launch_bounds__(256, WAVES) void k(uint32_t* out, unsigned long lon
     unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
     for (int b = 0; b < blocks; ++b) {
         uint32_t w[16];
+        if (LOADS) {
+            const uint4* q = src + ((threadIdx.x + 64 * (b & 15)) & 1023) * 4;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) w[i] = nkv::bswap32(seed + i * 0x9E3779B9u + uint32_t(b));
+            for (int i = 0; i < 4; ++i) {
+                const uint4 v = q[i];
+                w[4 * i] = nkv::bswap32(v.x);
+                w[4 * i + 1] = nkv::bswap32(v.y);
+                w[4 * i + 2] = nkv::bswap32(v.z);
+                w[4 * i + 3] = nkv::bswap32(v.w);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) w[i] = nkv::bswap32(seed + i * 0x9E3779B9u + uint32_t(b));
+        }
         nkv::sha1_compress(h, w);
     }
     unsigned long long t1 = __builtin_amdgcn_s_memtime();
@@ -31,19 +46,22 @@ __global__ __launch_bounds__(256, WAVES) void k(uint32_t* out, unsigned long lon
     }
 }
 
-template <int WAVES>
+template <int WAVES, bool LOADS = false>
 void run(int nblk_kernel, int blocks) {
     uint32_t* out;
     unsigned long long* clk;
+    uint4* src;
     (void)hipMalloc(&out, size_t(nblk_kernel) * 256 * 4);
     (void)hipMalloc(&clk, 16);
-    hipLaunchKernelGGL(k<WAVES>, dim3(nblk_kernel), dim3(256), 0, 0, out, clk, blocks);
+    (void)hipMalloc(&src, 65536);
+    (void)hipMemset(src, 0x5a, 65536);
+    hipLaunchKernelGGL((k<WAVES, LOADS>), dim3(nblk_kernel), dim3(256), 0, 0, out, clk, blocks, src);
     (void)hipDeviceSynchronize();
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
     (void)hipEventRecord(e0);
-    hipLaunchKernelGGL(k<WAVES>, dim3(nblk_kernel), dim3(256), 0, 0, out, clk, blocks);
+    hipLaunchKernelGGL((k<WAVES, LOADS>), dim3(nblk_kernel), dim3(256), 0, 0, out, clk, blocks, src);
     (void)hipEventRecord(e1);
     (void)hipEventSynchronize(e1);
     float ms = 0;
@@ -55,10 +73,11 @@ void run(int nblk_kernel, int blocks) {
     const double cyc = ms * 1e-3 * ghz * 1e9;
     const double per_block = cyc / (waves_per_simd * blocks);
     const double gbs = double(nblk_kernel) * 256 * blocks * 64.0 / (ms * 1e-3) / 1e9;
-    printf("waves/SIMD=%d grid=%6d  %.3f ms  clk %.2f GHz  %.0f SIMD-cycles per block per wave  %.0f GB/s\n",
-           WAVES, nblk_kernel, ms, ghz, per_block, gbs);
+    printf("%s waves/SIMD=%d grid=%6d  %.3f ms  clk %.2f GHz  %.0f SIMD-cycles per block per wave  %.0f GB/s\n",
+           LOADS ? "L2-loads" : "regs    ", WAVES, nblk_kernel, ms, ghz, per_block, gbs);
     (void)hipFree(out);
     (void)hipFree(clk);
+    (void)hipFree(src);
 }
 
 int main() {
@@ -66,5 +85,8 @@ int main() {
     run<8>(4096, 2048);
     run<4>(1024, 4096);
     run<2>(512, 4096);
+    run<1>(256, 2048);
+    run<8, true>(2048, 4096);
+    run<8, true>(4096, 2048);
     return 0;
 }

@@ -32,6 +32,21 @@
 #define OP_SHL(r) "v_lshlrev_b32 " #r ", 5, " #r
 #define OP_ADDLIT(r) "v_add_u32 " #r ", 0x5a827999, " #r
 #define OP_ADD3S(r) "v_add3_u32 " #r ", " #r ", %8, s0"
+#define OP_MIX1(r) "v_alignbit_b32 " #r ", " #r ", " #r ", 27\n\tv_xor_b32 " #r ", " #r ", %8"
+#define OP_MIX2(r) "v_add3_u32 " #r ", " #r ", %8, %9\n\tv_bitop3_b32 " #r ", " #r ", %8, %9 bitop3:0x96"
+#define OP_MIX3(r) "v_alignbit_b32 " #r ", " #r ", " #r ", 27\n\tv_xor_b32 " #r ", " #r ", %8\n\tv_xor_b32 " #r ", " #r ", %9\n\tv_bitop3_b32 " #r ", " #r ", %8, %9 bitop3:0x96"
+#define CL_ALIGN(r) "v_alignbit_b32 " #r ", " #r ", " #r ", 27"
+#define CL_XOR(r) "v_xor_b32 " #r ", " #r ", %8"
+#define CL_BITOP(r) "v_bitop3_b32 " #r ", " #r ", %8, %9 bitop3:0x96"
+#define BODYCL(OPA, OPB)                                                           \
+    asm volatile(".rept " "64" "\n\t"                                              \
+                 OPA(%0) "\n\t" OPA(%1) "\n\t" OPA(%2) "\n\t" OPA(%3) "\n\t"        \
+                 OPA(%4) "\n\t" OPA(%5) "\n\t" OPA(%6) "\n\t" OPA(%7) "\n\t"        \
+                 OPB(%0) "\n\t" OPB(%1) "\n\t" OPB(%2) "\n\t" OPB(%3) "\n\t"        \
+                 OPB(%4) "\n\t" OPB(%5) "\n\t" OPB(%6) "\n\t" OPB(%7) "\n\t"        \
+                 ".endr"                                                          \
+                 : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) \
+                 : "v"(x), "v"(y))
 #define OP_MADU24(r) "v_mad_u32_u24 " #r ", " #r ", %8, %9"
 
 template <int K>
@@ -56,6 +71,12 @@ __global__ __launch_bounds__(256) void k(uint32_t* out, unsigned long long* clk,
         if (K == 11) BODY8(OP_SHL);
         if (K == 12) BODY8(OP_ADDLIT);
         if (K == 13) BODY8(OP_MADU24);
+        if (K == 14) BODY8(OP_MIX1);
+        if (K == 15) BODY8(OP_MIX2);
+        if (K == 16) BODY8(OP_MIX3);
+        if (K == 17) BODYCL(CL_ALIGN, CL_XOR);
+        if (K == 18) BODYCL(CL_BITOP, CL_XOR);
+        if (K == 19) BODYCL(CL_XOR, CL_XOR);
     }
     unsigned long long t1 = __builtin_amdgcn_s_memtime();
     unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
@@ -112,6 +133,12 @@ int main() {
         run<11>("v_lshlrev", blocks);
         run<12>("v_add_lit", blocks);
         run<13>("v_mad_u24", blocks);
+        run<14>("mix alignbit+xor (2 instr)", blocks);
+        run<15>("mix add3+bitop3 (2 instr)", blocks);
+        run<16>("mix alignbit+3 full (4 instr)", blocks);
+        run<17>("clustered 8 alignbit + 8 xor (per 2)", blocks);
+        run<18>("clustered 8 bitop3 + 8 xor (per 2)", blocks);
+        run<19>("16 xor (per 2)", blocks);
     }
     return 0;
 }
