@@ -26,6 +26,22 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md (chip table)
 SEED = 0x6E616B65
+SEED_MIXED = 0x6E616B66
+
+
+def mixed_lengths(target_bytes: int, seed: int):
+    """BASELINE configs[2]: L = floor(2^U(6,16)) (64 B - 64 KiB, log-uniform), values
+    packed back to back (so mostly unaligned), until the payload reaches target_bytes."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    est = int(target_bytes / 9000) + 1024
+    lens = np.floor(2.0 ** rng.uniform(6, 16, est)).astype(np.uint64)
+    cs = np.cumsum(lens)
+    k = int(np.searchsorted(cs, target_bytes, side="right"))
+    lens = lens[:max(k, 1)]
+    off = np.zeros(len(lens), np.uint64)
+    off[1:] = np.cumsum(lens[:-1])
+    return lens, off
 
 
 def parse():
@@ -33,6 +49,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", choices=["sstable4k", "mixed"], default="sstable4k",
+                    help="sstable4k = BASELINE configs[1] (the metric); mixed = configs[2]")
+    ap.add_argument("--mixed-bytes", type=int, default=4 << 30, help="payload of the mixed config")
+    ap.add_argument("--no-bucket", action="store_true", help="mixed: hash in input order")
+    ap.add_argument("--leaf-load", type=int, default=0, help="NKV_OPT_LEAF_LOAD override (0 = library default)")
     ap.add_argument("--leaves", type=int, default=1 << 20)
     ap.add_argument("--value-bytes", type=int, default=4096)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -99,16 +120,38 @@ def main():
     stream = torch.cuda.current_stream()
     ctx.set_stream(stream.cuda_stream)
 
-    n, vlen = args.leaves, args.value_bytes
-    nbytes = n * vlen
-    data = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
-    _lib.check(L.nkv_fill_splitmix64_dev(ctx.h, data.data_ptr(), nbytes, SEED + rank))
-    total_nodes = L.nkv_total_nodes(n)
-    nodes = torch.empty(total_nodes * 20, dtype=torch.uint8, device="cuda")
+    if args.leaf_load:
+        ctx.set_option(_lib.NKV_OPT_LEAF_LOAD, args.leaf_load)
+    if args.no_bucket:
+        ctx.set_option(_lib.NKV_OPT_BUCKET, 0)
     roots = torch.empty(world * 20, dtype=torch.uint8, device="cuda")
+    mixed = args.config == "mixed"
+    if not mixed:
+        n, vlen = args.leaves, args.value_bytes
+        nbytes = n * vlen
+        data = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+        _lib.check(L.nkv_fill_splitmix64_dev(ctx.h, data.data_ptr(), nbytes, SEED + rank))
+        nodes = torch.empty(L.nkv_total_nodes(n) * 20, dtype=torch.uint8, device="cuda")
+
+        def tree():
+            _lib.check(L.nkv_tree_from_strided_dev(ctx.h, data.data_ptr(), vlen, vlen, n, nodes.data_ptr()))
+    else:
+        import numpy as np
+        lens_h, off_h = mixed_lengths(args.mixed_bytes, SEED_MIXED + rank)
+        n, vlen = len(lens_h), None
+        nbytes = int(lens_h.sum())
+        data = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+        _lib.check(L.nkv_fill_splitmix64_dev(ctx.h, data.data_ptr(), nbytes, SEED_MIXED + rank))
+        d_off = torch.from_numpy(off_h.view(np.int64)).cuda()
+        d_len = torch.from_numpy(lens_h.view(np.int64)).cuda()
+        nodes = torch.empty(L.nkv_total_nodes(n) * 20, dtype=torch.uint8, device="cuda")
+
+        def tree():
+            _lib.check(L.nkv_tree_from_values_dev(ctx.h, data.data_ptr(), d_off.data_ptr(), d_len.data_ptr(),
+                                                  n, nodes.data_ptr()))
 
     def step():
-        _lib.check(L.nkv_tree_from_strided_dev(ctx.h, data.data_ptr(), vlen, vlen, n, nodes.data_ptr()))
+        tree()
         if world > 1:  # C1: gather the per-table roots
             dist.all_gather_into_tensor(roots, nodes[-20:])
 
@@ -158,13 +201,17 @@ def main():
     verified = None
     if args.verify and rank == 0:
         from oracle import oracle_c as oc
-        host = oc.splitmix64_bytes(nbytes, SEED)
-        want = oc.tree_from_digests(oc.leaf_hashes_strided(host, vlen, vlen, n, threads=16))
+        if mixed:
+            host = oc.splitmix64_bytes(nbytes, SEED_MIXED)
+            want = oc.tree_from_digests(oc.leaf_hashes(host, off_h, lens_h, threads=16))
+        else:
+            host = oc.splitmix64_bytes(nbytes, SEED)
+            want = oc.tree_from_digests(oc.leaf_hashes_strided(host, vlen, vlen, n, threads=16))
         verified = want[-1].tobytes().hex() == root
         del host
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not mixed:
         cpu = cpu_baseline(min(args.cpu_sample_leaves, n), vlen)
 
     if rank == 0:
@@ -192,10 +239,12 @@ def main():
             "dtype": "u32",
             "data": f"synthetic: splitmix64 bytes (seed {SEED:#x} + rank) generated in HBM",
             "config": {
-                "workload": "BASELINE configs[1]: single SSTable flush, 1 Mi x 4 KiB values, "
+                "workload": ("BASELINE configs[2]: mixed 64 B - 64 KiB log-uniform values packed back to back, "
+                             + ("input order" if args.no_bucket else "length-bucketed")) if mixed else
+                            "BASELINE configs[1]: single SSTable flush, 1 Mi x 4 KiB values, "
                             "leaf SHA-1 + full tree reduce (one table per GPU; roots all-gathered over RCCL when N>1)",
                 "leaves_per_gpu": n,
-                "value_bytes": vlen,
+                "value_bytes": vlen if not mixed else "64..65536 (mean %.0f)" % (nbytes / n),
                 "parallelism": f"{world} independent tables" + (" + RCCL all_gather of roots" if world > 1 else ""),
             },
             "roofline": {

@@ -82,6 +82,9 @@ int nkv_ctx_sync(nkv_ctx *ctx);
 #define NKV_OPT_LEAF_LOAD 1 /* leaf-kernel load path for 16-byte aligned values:
                                1 = LDS-DMA stage, 2 = direct loads, 3 = direct non-temporal,
                                4 / 5 = direct loads in 128 / 256-byte runs per lane */
+#define NKV_OPT_BUCKET 2    /* 1 (default) = hash ragged values (nkv_tree_from_values*,
+                               nkv_tree_from_records) in length-sorted order; 0 = in
+                               input order, fused with the first tree levels */
 int nkv_ctx_set_option(nkv_ctx *ctx, int key, int64_t value);
 /* When enabled, the device-resident tree calls record HIP events around the
  * leaf kernel and the tree reduce on the context's stream. */

@@ -96,13 +96,14 @@ struct nkv_ctx {
     hipStream_t own = nullptr;
     hipStream_t stream = nullptr;
     int leaf_load = 1;  // NKV_OPT_LEAF_LOAD
+    int bucket = 1;     // NKV_OPT_BUCKET
     bool timing = false;
     bool timed = false;
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
     // per-call event triples (leaf start, leaf end / reduce start, reduce end)
     std::vector<hipEvent_t> ring;
     size_t ring_used = 0;
-    DevBuf d_data, d_off, d_len, d_nodes, d_img, d_tmp, d_err, d_aux;
+    DevBuf d_data, d_off, d_len, d_nodes, d_img, d_tmp, d_err, d_aux, d_keys, d_perm, d_stmp;
     void* h_stage = nullptr;
     size_t h_cap = 0;
 };
@@ -234,13 +235,42 @@ int mark(nkv_ctx* c, int which) {
     return NKV_OK;
 }
 
+// Level 0 only: the leaf kernel over the length-sorted order when bucketing
+// (ragged values), else in input order.  Not fused with tree levels.
+int leaf_level(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint64_t* len,
+               uint64_t n, bool aligned, uint8_t* nodes) {
+    const uint32_t* perm = nullptr;
+    if (c->bucket && n > 64) {
+        if (n > 0x7fffffffull) return NKV_ERR_INVALID;
+        TRY(grow(c->d_keys, 8 * n));
+        TRY(grow(c->d_perm, 8 * n));
+        uint32_t* keys = static_cast<uint32_t*>(c->d_keys.p);
+        uint32_t* pp = static_cast<uint32_t*>(c->d_perm.p);
+        size_t tb = 0;
+        HIPTRY(sort_by_length_desc(len, n, keys, pp, nullptr, &tb, c->stream));
+        TRY(grow(c->d_stmp, tb));
+        HIPTRY(sort_by_length_desc(len, n, keys, pp, c->d_stmp.p, &tb, c->stream));
+        perm = pp + n;
+    }
+    return st(launch_leaf_offsets(base, off, len, perm, n, 0, false, aligned, c->leaf_load, nodes,
+                                  c->stream));
+}
+
 int tree_from_device_values(nkv_ctx* c, const uint8_t* base, const uint64_t* off,
                             const uint64_t* len, uint64_t n, bool aligned, uint8_t* nodes) {
     const int top = levels_of(n) - 1;
     TRY(mark(c, 0));
-    HIPTRY(launch_leaf_offsets(base, off, len, nullptr, n, top, true, aligned, c->leaf_load, nodes, c->stream));
-    TRY(mark(c, 1));
-    HIPTRY(launch_reduce(nodes, n, std::min(top, kWaveLevels), top, c->stream));
+    if (c->bucket && n > 64) {
+        // a permuted wave does not own a subtree: reduce everything from level 0
+        TRY(leaf_level(c, base, off, len, n, aligned, nodes));
+        TRY(mark(c, 1));
+        HIPTRY(launch_reduce(nodes, n, 0, top, c->stream));
+    } else {
+        HIPTRY(launch_leaf_offsets(base, off, len, nullptr, n, top, true, aligned, c->leaf_load, nodes,
+                                   c->stream));
+        TRY(mark(c, 1));
+        HIPTRY(launch_reduce(nodes, n, std::min(top, kWaveLevels), top, c->stream));
+    }
     return mark(c, 2);
 }
 
@@ -297,7 +327,7 @@ void nkv_ctx_destroy(nkv_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (DevBuf* b : {&c->d_data, &c->d_off, &c->d_len, &c->d_nodes, &c->d_img, &c->d_tmp,
-                      &c->d_err, &c->d_aux})
+                      &c->d_err, &c->d_aux, &c->d_keys, &c->d_perm, &c->d_stmp})
         if (b->p) (void)hipFree(b->p);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
     for (hipEvent_t e : c->ev)
@@ -325,6 +355,10 @@ int nkv_ctx_set_option(nkv_ctx* c, int key, int64_t value) {
         case NKV_OPT_LEAF_LOAD:
             if (value < 1 || value > 5) return NKV_ERR_INVALID;
             c->leaf_load = int(value);
+            return NKV_OK;
+        case NKV_OPT_BUCKET:
+            if (value < 0 || value > 1) return NKV_ERR_INVALID;
+            c->bucket = int(value);
             return NKV_OK;
         default:
             return NKV_ERR_INVALID;
@@ -412,10 +446,8 @@ int nkv_leaf_hash(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const ui
     TRY(stage_values(c, base, off, len, n));
     TRY(grow(c->d_nodes, 20 * n));
     uint8_t* nodes = static_cast<uint8_t*>(c->d_nodes.p);
-    HIPTRY(launch_leaf_offsets(static_cast<const uint8_t*>(c->d_data.p),
-                               static_cast<const uint64_t*>(c->d_off.p),
-                               static_cast<const uint64_t*>(c->d_len.p), nullptr, n, 0, false, true, c->leaf_load,
-                               nodes, c->stream));
+    TRY(leaf_level(c, static_cast<const uint8_t*>(c->d_data.p), static_cast<const uint64_t*>(c->d_off.p),
+                   static_cast<const uint64_t*>(c->d_len.p), n, true, nodes));
     HIPTRY(hipMemcpyAsync(out20, nodes, 20 * n, hipMemcpyDeviceToHost, c->stream));
     return st(hipStreamSynchronize(c->stream));
 }
@@ -488,10 +520,8 @@ int nkv_tree_generic(nkv_ctx* c, const uint8_t* data, const uint64_t* off, const
     const uint64_t up_total = n1 == 1 ? 1 : total_of(n1);
     TRY(grow(c->d_nodes, 20 * up_total));
     uint8_t* up = static_cast<uint8_t*>(c->d_nodes.p);
-    HIPTRY(launch_leaf_offsets(static_cast<const uint8_t*>(c->d_data.p),
-                               static_cast<const uint64_t*>(c->d_off.p),
-                               static_cast<const uint64_t*>(c->d_len.p), nullptr, n1, 0, false,
-                               true, c->leaf_load, up, c->stream));
+    TRY(leaf_level(c, static_cast<const uint8_t*>(c->d_data.p), static_cast<const uint64_t*>(c->d_off.p),
+                   static_cast<const uint64_t*>(c->d_len.p), n1, true, up));
     if (n1 > 1) HIPTRY(launch_reduce(up, n1, 0, levels_of(n1) - 1, c->stream));
     if (upper_out)
         HIPTRY(hipMemcpyAsync(upper_out, up, 20 * up_total, hipMemcpyDeviceToHost, c->stream));
@@ -582,9 +612,8 @@ int nkv_leaf_hash_dev(nkv_ctx* c, const void* d_base, const uint64_t* d_off,
     TRY(bind(c));
     if (n == 0) return NKV_OK;
     if (!d_base || !d_off || !d_len || !d_nodes) return NKV_ERR_INVALID;
-    return st(launch_leaf_offsets(static_cast<const uint8_t*>(d_base), d_off, d_len, nullptr, n, 0,
-                                  false, false, c->leaf_load, static_cast<uint8_t*>(d_nodes),
-                                  c->stream));
+    return leaf_level(c, static_cast<const uint8_t*>(d_base), d_off, d_len, n, false,
+                      static_cast<uint8_t*>(d_nodes));
 }
 
 int nkv_leaf_hash_strided_dev(nkv_ctx* c, const void* d_base, uint64_t stride, uint64_t len,

@@ -31,8 +31,6 @@ hipError_t launch_leaf_offsets(const uint8_t* base, const uint64_t* off, const u
                                const uint32_t* perm, uint64_t n, int top, bool fuse, bool aligned,
                                int load, uint8_t* nodes, hipStream_t s);
 hipError_t launch_reduce(uint8_t* nodes, uint64_t n, int from_level, int top, hipStream_t s);
-hipError_t launch_hash_messages(const uint8_t* base, const uint64_t* off, const uint64_t* len,
-                                uint64_t n, uint8_t* out, hipStream_t s);
 hipError_t launch_bfs_image(const uint8_t* nodes, const BfsLayout& lay, uint8_t* img,
                             hipStream_t s);
 hipError_t launch_locate(const uint8_t* stream, uint64_t stream_len, const uint64_t* rec_off,
@@ -40,6 +38,9 @@ hipError_t launch_locate(const uint8_t* stream, uint64_t stream_len, const uint6
                          hipStream_t s);
 hipError_t scan_exclusive_u64(const uint64_t* in, uint64_t* out, uint64_t n, void* tmp,
                               size_t* tmp_bytes, hipStream_t s);
+// Two-phase (tmp == nullptr: size query).  The permutation lands in perm + n.
+hipError_t sort_by_length_desc(const uint64_t* len, uint64_t n, uint32_t* keys, uint32_t* perm,
+                               void* tmp, size_t* tmp_bytes, hipStream_t s);
 hipError_t launch_fill(uint8_t* buf, uint64_t nbytes, uint64_t seed, hipStream_t s);
 
 }  // namespace nkv

@@ -185,9 +185,10 @@ __device__ __forceinline__ void be16_funnel(const uint32_t d[20], uint32_t s, ui
 
 __device__ __forceinline__ void load_window(const uint8_t* p, uint32_t avail, uint32_t d[20]) {
     // p: stream start; avail: value bytes available from p (>= 1 unless empty).
-    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-    const uint4* q = reinterpret_cast<const uint4*>(a & ~uintptr_t(15));
-    const uint32_t s = uint32_t(a & 15);
+    // p - s (not an integer-to-pointer cast) keeps the global address space,
+    // so these stay global_load_dwordx4 rather than flat loads
+    const uint32_t s = uint32_t(reinterpret_cast<uintptr_t>(p) & 15);
+    const uint4* q = reinterpret_cast<const uint4*>(p - s);
 #pragma unroll
     for (int c = 0; c < 5; ++c) {
         uint4 v = make_uint4(0u, 0u, 0u, 0u);
@@ -228,11 +229,13 @@ __device__ __forceinline__ void sha1_value(const uint8_t* p, uint64_t len, uint3
             sha1_compress(h, w);
         }
     } else {
+        // one-window register prefetch (the loads of block b+1 overlap block b)
         const uint32_t s = uint32_t(reinterpret_cast<uintptr_t>(p) & 15);
+        uint32_t d[20];
+        if (nfull > 0) load_window(p, 64u, d);
         for (uint64_t b = 0; b < nfull; ++b) {
-            uint32_t d[20];
-            load_window(p + 64 * b, 64u, d);
             be16_funnel(d, s, w);
+            if (b + 1 < nfull) load_window(p + 64 * (b + 1), 64u, d);
             sha1_compress(h, w);
         }
     }
@@ -384,10 +387,8 @@ __global__ __launch_bounds__(kBlock, LOAD >= 4 ? 4 : kLeafWavesPerSimd) void k_l
                                                   const uint64_t* __restrict__ len, uint64_t stride,
                                                   uint64_t L, const uint32_t* __restrict__ perm,
                                                   uint64_t n, int top, uint8_t* __restrict__ nodes) {
-    // 16 KiB: four wave-private 4 KiB LDS-DMA stages, then reused for the
-    // fused subtree reduce (5 x 256 words).
+    // 16 KiB: four wave-private 4 KiB LDS-DMA stages (LOAD == 1)
     __shared__ __attribute__((aligned(16))) uint8_t smem[kBlock * 64];
-    uint32_t(*lds)[kBlock] = reinterpret_cast<uint32_t(*)[kBlock]>(smem);
     NKV_STAMP(0);
     const uint64_t g = blockIdx.x;
     const uint64_t t = g * kBlock + threadIdx.x;
@@ -499,18 +500,19 @@ __global__ __launch_bounds__(kBlock) void k_reduce(uint8_t* __restrict__ nodes, 
     subtree_reduce(lds, n, j0, jmax, lo, nodes);
 }
 
-// K1g: generic first level for New() over arbitrary leaf Data: message i is
-// leaf[2i].Data || leaf[2i+1].Data (or the lone leaf[2i].Data), staged by the
-// host as one contiguous message per parent.  Same per-lane hash as K1.
-__global__ __launch_bounds__(kBlock) void k_hash_messages(const uint8_t* __restrict__ base,
-                                                           const uint64_t* __restrict__ off,
-                                                           const uint64_t* __restrict__ len,
-                                                           uint64_t n, uint8_t* __restrict__ out) {
+// ---------------------------------------------------------------------------
+// Length bucketing for ragged values: one lane per value means a wavefront
+// runs for its longest value, so values are ordered by compression count,
+// longest first (longest-processing-time order for the dispatcher), and the
+// leaf kernel reads them through the permutation.
+__global__ __launch_bounds__(kBlock) void k_bucket_keys(const uint64_t* __restrict__ len, uint64_t n,
+                                                         uint32_t* __restrict__ keys,
+                                                         uint32_t* __restrict__ idx) {
     const uint64_t t = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
     if (t >= n) return;
-    uint32_t h[5];
-    sha1_value<false>(base + off[t], len[t], h);
-    store_digest(out, t, h);
+    const uint64_t blocks = (len[t] + 8) / 64 + 1;  // SHA-1 compressions of the value
+    keys[t] = blocks > 0xFFFFFFFFull ? 0xFFFFFFFFu : uint32_t(blocks);
+    idx[t] = uint32_t(t);
 }
 
 // ---------------------------------------------------------------------------
@@ -669,13 +671,6 @@ hipError_t launch_reduce(uint8_t* nodes, uint64_t n, int from_level, int top, hi
     return hipSuccess;
 }
 
-hipError_t launch_hash_messages(const uint8_t* base, const uint64_t* off, const uint64_t* len,
-                                uint64_t n, uint8_t* out, hipStream_t s) {
-    hipLaunchKernelGGL(k_hash_messages, dim3(grid_for(n)), dim3(kBlock), 0, s, base, off, len, n,
-                       out);
-    return hipGetLastError();
-}
-
 hipError_t launch_bfs_image(const uint8_t* nodes, const BfsLayout& lay, uint8_t* img,
                             hipStream_t s) {
     const uint64_t threads = (lay.total + 15) / 16;
@@ -702,6 +697,19 @@ extern "C" int nkv_diag_set_buffer(void* d) {
     return hipMemcpyToSymbol(HIP_SYMBOL(g_diag), &p, sizeof(p)) == hipSuccess ? 0 : 3;
 }
 #endif
+
+hipError_t sort_by_length_desc(const uint64_t* len, uint64_t n, uint32_t* keys, uint32_t* perm,
+                               void* tmp, size_t* tmp_bytes, hipStream_t s) {
+    // keys: 2n u32 (in | out), perm: 2n u32 (iota in | permutation out)
+    if (tmp == nullptr)
+        return hipcub::DeviceRadixSort::SortPairsDescending(nullptr, *tmp_bytes, keys, keys + n, perm,
+                                                            perm + n, int(n), 0, 32, s);
+    hipLaunchKernelGGL(k_bucket_keys, dim3(grid_for(n)), dim3(kBlock), 0, s, len, n, keys, perm);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return hipcub::DeviceRadixSort::SortPairsDescending(tmp, *tmp_bytes, keys, keys + n, perm, perm + n,
+                                                        int(n), 0, 32, s);
+}
 
 hipError_t launch_fill(uint8_t* buf, uint64_t nbytes, uint64_t seed, hipStream_t s) {
     uint64_t threads = (nbytes + 15) / 16;

@@ -69,11 +69,14 @@ def test_leaf_hash_every_alignment_device(nkv, oracle, shift):
     assert np.array_equal(got, oracle.leaf_hashes(data, off, lens))
 
 
-def test_leaf_hash_mixed_wave_alignment(nkv, oracle):
-    """Lanes of one wavefront with different alignments and lengths."""
+@pytest.mark.parametrize("bucket", [1, 0])
+def test_leaf_hash_mixed_wave_alignment(nkv, oracle, bucket):
+    """Lanes of one wavefront with different alignments and lengths (with and
+    without length bucketing)."""
     torch = _torch()
     _lib, ctx = nkv
     _bind(torch, ctx)
+    ctx.set_option(_lib.NKV_OPT_BUCKET, bucket)
     L = _lib.lib()
     rng = np.random.default_rng(7)
     n = 5000
@@ -88,7 +91,40 @@ def test_leaf_hash_mixed_wave_alignment(nkv, oracle):
     torch.cuda.synchronize()
     got = d_nodes.cpu().numpy().reshape(-1, 20)
     want = oracle.tree_from_digests(oracle.leaf_hashes(data, off, lens))
+    ctx.set_option(_lib.NKV_OPT_BUCKET, 1)
     assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("load", [1, 2, 4, 5])
+def test_mixed_sizes_log_uniform(nkv, oracle, load):
+    """BASELINE configs[2] shape at reduced count: log-uniform 64 B - 64 KiB values,
+    packed back to back (unaligned), every load path."""
+    torch = _torch()
+    _lib, ctx = nkv
+    _bind(torch, ctx)
+    L = _lib.lib()
+    rng = np.random.default_rng(0x6E616B66)
+    n = 6000
+    lens = np.floor(2.0 ** rng.uniform(6, 16, n)).astype(np.uint64)
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum(lens[:-1])
+    data = oracle.splitmix64_bytes(int(lens.sum()), 0x6E616B66)
+    d_data, d_off, d_len = _dev(torch, data), _dev(torch, off), _dev(torch, lens)
+    d_nodes = torch.zeros(L.nkv_total_nodes(n) * 20, dtype=torch.uint8, device="cuda")
+    ctx.set_option(_lib.NKV_OPT_LEAF_LOAD, load)
+    try:
+        _lib.check(L.nkv_tree_from_values_dev(ctx.h, d_data.data_ptr(), d_off.data_ptr(), d_len.data_ptr(),
+                                              n, d_nodes.data_ptr()))
+        torch.cuda.synchronize()
+    finally:
+        ctx.set_option(_lib.NKV_OPT_LEAF_LOAD, 1)
+    want = oracle.tree_from_digests(oracle.leaf_hashes(data, off, lens, threads=8))
+    assert np.array_equal(d_nodes.cpu().numpy().reshape(-1, 20), want)
+    # aligned copy of the same values (host API path packs at 16 B)
+    nodes = np.zeros((L.nkv_total_nodes(n), 20), np.uint8)
+    _lib.check(L.nkv_tree_from_values(ctx.h, _lib.p8(data), _lib.p64(off), _lib.p64(lens), n, None,
+                                      _lib.p8(nodes), None))
+    assert np.array_equal(nodes, want)
 
 
 @pytest.mark.parametrize("n", EDGE_N)
@@ -144,6 +180,27 @@ def test_strided_device_path(nkv, oracle, base_off, stride, vlen):
     got = d_nodes.cpu().numpy().reshape(-1, 20)
     want = oracle.tree_from_digests(oracle.leaf_hashes_strided(host[base_off:], stride, vlen, n, threads=8))
     assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("load", [1, 2, 3, 4, 5])
+def test_strided_every_load_path(nkv, oracle, load):
+    torch = _torch()
+    _lib, ctx = nkv
+    _bind(torch, ctx)
+    L = _lib.lib()
+    n, vlen = 9000, 4096 + 48
+    d = torch.empty(n * vlen, dtype=torch.uint8, device="cuda")
+    _lib.check(L.nkv_fill_splitmix64_dev(ctx.h, d.data_ptr(), n * vlen, SEED))
+    d_nodes = torch.zeros(L.nkv_total_nodes(n) * 20, dtype=torch.uint8, device="cuda")
+    ctx.set_option(_lib.NKV_OPT_LEAF_LOAD, load)
+    try:
+        _lib.check(L.nkv_tree_from_strided_dev(ctx.h, d.data_ptr(), vlen, vlen, n, d_nodes.data_ptr()))
+        torch.cuda.synchronize()
+    finally:
+        ctx.set_option(_lib.NKV_OPT_LEAF_LOAD, 1)
+    host = oracle.splitmix64_bytes(n * vlen, SEED)
+    want = oracle.tree_from_digests(oracle.leaf_hashes_strided(host, vlen, vlen, n, threads=8))
+    assert np.array_equal(d_nodes.cpu().numpy().reshape(-1, 20), want)
 
 
 def test_full_size_config2_bit_exact(nkv, oracle):

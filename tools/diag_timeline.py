@@ -30,16 +30,33 @@ def main():
     s = torch.cuda.current_stream()
     ctx.set_stream(s.cuda_stream)
     ctx.set_option(_lib.NKV_OPT_LEAF_LOAD, int(os.environ.get("NKV_LEAF_LOAD", "1")))
-    data = torch.empty(n * vlen, dtype=torch.uint8, device="cuda")
-    _lib.check(L.nkv_fill_splitmix64_dev(ctx.h, data.data_ptr(), n * vlen, 1))
+    mixed = os.environ.get("MIXED") == "1"
+    if mixed:
+        import bench
+        lens_h, off_h = bench.mixed_lengths(4 << 30, bench.SEED_MIXED)
+        n = len(lens_h)
+        nbytes = int(lens_h.sum())
+        d_off = torch.from_numpy(off_h.view(np.int64)).cuda()
+        d_len = torch.from_numpy(lens_h.view(np.int64)).cuda()
+    else:
+        nbytes = n * vlen
+    data = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    _lib.check(L.nkv_fill_splitmix64_dev(ctx.h, data.data_ptr(), nbytes, 1))
     nodes = torch.empty(L.nkv_total_nodes(n) * 20, dtype=torch.uint8, device="cuda")
     waves = (n + 255) // 256 * 4
     diag = torch.zeros(waves * 8, dtype=torch.int64, device="cuda")
-    for _ in range(20):
-        _lib.check(L.nkv_tree_from_strided_dev(ctx.h, data.data_ptr(), stride, vlen, n, nodes.data_ptr()))
+
+    def run():
+        if mixed:
+            _lib.check(L.nkv_tree_from_values_dev(ctx.h, data.data_ptr(), d_off.data_ptr(), d_len.data_ptr(),
+                                                  n, nodes.data_ptr()))
+        else:
+            _lib.check(L.nkv_tree_from_strided_dev(ctx.h, data.data_ptr(), stride, vlen, n, nodes.data_ptr()))
+    for _ in range(10):
+        run()
     torch.cuda.synchronize()
     assert L.nkv_diag_set_buffer(diag.data_ptr()) == 0
-    _lib.check(L.nkv_tree_from_strided_dev(ctx.h, data.data_ptr(), stride, vlen, n, nodes.data_ptr()))
+    run()
     torch.cuda.synchronize()
     assert L.nkv_diag_set_buffer(None) == 0
     d = diag.cpu().numpy().view(np.uint64).reshape(waves, 8).astype(np.float64)
@@ -65,6 +82,9 @@ def main():
     print(f"first wave ends at {first_end:.1f} us; {late.sum()} waves start after that; "
           f"last start {starts.max():.1f} us; last end {ends.max():.1f} us")
     xcc = (d[:, 6].astype(np.uint64) >> np.uint64(32)).astype(int)
+    dur = ends - starts
+    order = np.argsort(-dur)
+    print("longest waves (us): " + ", ".join(f"w{int(i)} start {starts[i]:.0f} dur {dur[i]:.0f}" for i in order[:6]))
     for x in range(8):
         m = xcc == x
         if m.any():

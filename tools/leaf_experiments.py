@@ -39,11 +39,35 @@ def main():
 
     M = 1 << 20
     variants = {}
-    for mode, name in ((1, "lds-dma"), (2, "direct"), (4, "runs128"), (5, "runs256")):
-        variants[f"{name:10s} fused 1Mx4K"] = (with_load(mode, fused(M, 4096, 4096)), M * 4096)
-        variants[f"{name:10s} leafonly 1Mx4K"] = (with_load(mode, leaf_only(M, 4096, 4096)), M * 4096)
-        variants[f"{name:10s} fused 1Mx4K stride0"] = (with_load(mode, fused(M, 0, 4096)), M * 4096)
-        variants[f"{name:10s} fused 4Mx1K"] = (with_load(mode, fused(4 * M, 1024, 1024)), 4 * M * 1024)
+    import numpy as np
+    sel = os.environ.get("EXP", "loads")
+    if sel == "loads":
+        for mode, name in ((1, "lds-dma"), (2, "direct"), (4, "runs128"), (5, "runs256")):
+            variants[f"{name:10s} fused 1Mx4K"] = (with_load(mode, fused(M, 4096, 4096)), M * 4096)
+            variants[f"{name:10s} leafonly 1Mx4K"] = (with_load(mode, leaf_only(M, 4096, 4096)), M * 4096)
+            variants[f"{name:10s} fused 1Mx4K stride0"] = (with_load(mode, fused(M, 0, 4096)), M * 4096)
+            variants[f"{name:10s} fused 4Mx1K"] = (with_load(mode, fused(4 * M, 1024, 1024)), 4 * M * 1024)
+    else:
+        # funnel (unaligned) vs aligned, strided and offset-array paths
+        variants["strided aligned 1Mx4096"] = (fused(M, 4096, 4096), M * 4096)
+        base46 = big.data_ptr() + 46
+        variants["strided unaligned(+46) 1Mx4050"] = (
+            lambda: L.nkv_tree_from_strided_dev(ctx.h, base46, 4096, 4050, M, nodes.data_ptr()), M * 4050)
+        off_a = torch.from_numpy((np.arange(M, dtype=np.int64) * 4096)).cuda()
+        off_u = torch.from_numpy((np.arange(M, dtype=np.int64) * 4096 + 46)).cuda()
+        len_a = torch.full((M,), 4096, dtype=torch.int64, device="cuda")
+        len_u = torch.full((M,), 4050, dtype=torch.int64, device="cuda")
+
+        def offs(o, l, bucket):
+            def run():
+                ctx.set_option(_lib.NKV_OPT_BUCKET, bucket)
+                return L.nkv_tree_from_values_dev(ctx.h, big.data_ptr(), o.data_ptr(), l.data_ptr(), M,
+                                                  nodes.data_ptr())
+            return run
+        variants["offsets aligned bucket0"] = (offs(off_a, len_a, 0), M * 4096)
+        variants["offsets aligned bucket1"] = (offs(off_a, len_a, 1), M * 4096)
+        variants["offsets unaligned bucket0"] = (offs(off_u, len_u, 0), M * 4050)
+        variants["offsets unaligned bucket1"] = (offs(off_u, len_u, 1), M * 4050)
     res = {k: [] for k in variants}
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
