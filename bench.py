@@ -25,6 +25,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md (chip table)
+# Measured compute ceiling of the per-lane SHA-1 (no memory traffic, 8 waves/SIMD,
+# 2.37-2.39 GHz): tools/sha1_rate.hip -> profiles/r01_sha1_compute_rate.txt.
+SHA1_VALU_CEILING_GBS = 4100.0
 SEED = 0x6E616B65
 SEED_MIXED = 0x6E616B66
 
@@ -218,13 +221,14 @@ def main():
         total_bytes = nbytes * world * args.steps
         value = total_bytes / elapsed / 2**30
         achieved = nbytes / (leaf_ms * 1e-3) / 1e9  # algorithmic payload bytes per K1 launch
-        traffic = None
+        traffic, traffic_bounds = None, None
         pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc_path):
+        if os.path.exists(pmc_path) and not mixed:
             with open(pmc_path) as f:
                 pmc = json.load(f)
             if pmc.get("leaves") == n and pmc.get("value_bytes") == vlen:
                 traffic = pmc.get("hbm_bytes_per_launch")
+                traffic_bounds = pmc.get("hbm_read_bytes_bounds_per_launch")
         out = {
             "metric": "GiB/s Merkle leaf-hash + tree-reduce over device-resident record blocks",
             "value": round(value, 2),
@@ -255,6 +259,9 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
+                "traffic_bounds": traffic_bounds,  # RDREQ x 64 .. x 128 B (profiles/pmc_traffic.json)
+                "valu_ceiling": SHA1_VALU_CEILING_GBS,
+                "valu_frac": round(achieved / SHA1_VALU_CEILING_GBS, 4),
             },
             "kernel_ms": {"leaf_fused": round(leaf_ms, 4), "tree_reduce_rest": round(reduce_ms, 4),
                           "bfs_image": round(bfs_ms, 4)},
