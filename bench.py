@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--mixed-bytes", type=int, default=4 << 30, help="payload of the mixed config")
     ap.add_argument("--no-bucket", action="store_true", help="mixed: hash in input order")
     ap.add_argument("--leaf-load", type=int, default=0, help="NKV_OPT_LEAF_LOAD override (0 = library default)")
+    ap.add_argument("--deep", type=int, default=-1,
+                    help="NKV_OPT_DEEP_PREFETCH override for ragged batches (-1 = library default)")
     ap.add_argument("--leaves", type=int, default=1 << 20)
     ap.add_argument("--value-bytes", type=int, default=4096)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -125,6 +127,8 @@ def main():
 
     if args.leaf_load:
         ctx.set_option(_lib.NKV_OPT_LEAF_LOAD, args.leaf_load)
+    if args.deep >= 0:
+        ctx.set_option(_lib.NKV_OPT_DEEP_PREFETCH, args.deep)
     if args.no_bucket:
         ctx.set_option(_lib.NKV_OPT_BUCKET, 0)
     roots = torch.empty(world * 20, dtype=torch.uint8, device="cuda")

@@ -85,6 +85,11 @@ int nkv_ctx_sync(nkv_ctx *ctx);
 #define NKV_OPT_BUCKET 2    /* 1 (default) = hash ragged values (nkv_tree_from_values*,
                                nkv_tree_from_records) in length-sorted order; 0 = in
                                input order, fused with the first tree levels */
+#define NKV_OPT_DEEP_PREFETCH 3 /* length-sorted ragged batches: 0 = one block of
+                                   lookahead; 1 = several blocks; 2 = several blocks in a
+                                   work-queue kernel that spreads the longest chains one
+                                   per SIMD; 3 = the work-queue kernel with values
+                                   staged as aligned 64-B chunks through an LDS ring */
 int nkv_ctx_set_option(nkv_ctx *ctx, int key, int64_t value);
 /* When enabled, the device-resident tree calls record HIP events around the
  * leaf kernel and the tree reduce on the context's stream. */

@@ -22,6 +22,7 @@ NKV_ERR_NOMEM = 4
 NKV_ERR_IO = 5
 NKV_OPT_LEAF_LOAD = 1
 NKV_OPT_BUCKET = 2
+NKV_OPT_DEEP_PREFETCH = 3
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)
 _u64p = ctypes.POINTER(ctypes.c_uint64)

@@ -97,13 +97,15 @@ struct nkv_ctx {
     hipStream_t stream = nullptr;
     int leaf_load = 1;  // NKV_OPT_LEAF_LOAD
     int bucket = 1;     // NKV_OPT_BUCKET
+    int deep = 1;       // NKV_OPT_DEEP_PREFETCH (2 = work-queue kernel)
+    uint32_t simds = 1024;  // SIMDs on the device (CUs x 4)
     bool timing = false;
     bool timed = false;
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
     // per-call event triples (leaf start, leaf end / reduce start, reduce end)
     std::vector<hipEvent_t> ring;
     size_t ring_used = 0;
-    DevBuf d_data, d_off, d_len, d_nodes, d_img, d_tmp, d_err, d_aux, d_keys, d_perm, d_stmp;
+    DevBuf d_data, d_off, d_len, d_nodes, d_img, d_tmp, d_err, d_aux, d_keys, d_perm, d_stmp, d_queue;
     void* h_stage = nullptr;
     size_t h_cap = 0;
 };
@@ -251,9 +253,16 @@ int leaf_level(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint6
         TRY(grow(c->d_stmp, tb));
         HIPTRY(sort_by_length_desc(len, n, keys, pp, c->d_stmp.p, &tb, c->stream));
         perm = pp + n;
+        if (c->deep >= 2) {
+            TRY(grow(c->d_queue, 4 * queue_words(n)));
+            const bool ring = c->deep == 3;
+            return st(launch_leaf_queue(base, off, len, perm, n, aligned, ring,
+                                        static_cast<uint32_t*>(c->d_queue.p), (ring ? 4 : 2) * c->simds, nodes,
+                                        c->stream));
+        }
     }
     return st(launch_leaf_offsets(base, off, len, perm, n, 0, false, aligned, c->leaf_load, nodes,
-                                  c->stream));
+                                  c->stream, c->deep != 0));
 }
 
 int tree_from_device_values(nkv_ctx* c, const uint8_t* base, const uint64_t* off,
@@ -318,6 +327,9 @@ int nkv_ctx_create(int device, nkv_ctx** out) {
         return rc;
     }
     c->stream = c->own;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+        c->simds = uint32_t(prop.multiProcessorCount) * 4;
     *out = c;
     return NKV_OK;
 }
@@ -327,7 +339,7 @@ void nkv_ctx_destroy(nkv_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (DevBuf* b : {&c->d_data, &c->d_off, &c->d_len, &c->d_nodes, &c->d_img, &c->d_tmp,
-                      &c->d_err, &c->d_aux, &c->d_keys, &c->d_perm, &c->d_stmp})
+                      &c->d_err, &c->d_aux, &c->d_keys, &c->d_perm, &c->d_stmp, &c->d_queue})
         if (b->p) (void)hipFree(b->p);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
     for (hipEvent_t e : c->ev)
@@ -359,6 +371,10 @@ int nkv_ctx_set_option(nkv_ctx* c, int key, int64_t value) {
         case NKV_OPT_BUCKET:
             if (value < 0 || value > 1) return NKV_ERR_INVALID;
             c->bucket = int(value);
+            return NKV_OK;
+        case NKV_OPT_DEEP_PREFETCH:
+            if (value < 0 || value > 3) return NKV_ERR_INVALID;
+            c->deep = int(value);
             return NKV_OK;
         default:
             return NKV_ERR_INVALID;

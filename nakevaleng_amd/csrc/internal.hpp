@@ -29,7 +29,13 @@ hipError_t launch_leaf_strided(const uint8_t* base, uint64_t stride, uint64_t L,
                                int top, bool fuse, int load, uint8_t* nodes, hipStream_t s);
 hipError_t launch_leaf_offsets(const uint8_t* base, const uint64_t* off, const uint64_t* len,
                                const uint32_t* perm, uint64_t n, int top, bool fuse, bool aligned,
-                               int load, uint8_t* nodes, hipStream_t s);
+                               int load, uint8_t* nodes, hipStream_t s, bool deep = true);
+// Ragged batch through the work-queue leaf kernel (perm = length-sorted order,
+// longest first); q must hold queue_words(n) u32; waves = 2 x SIMDs.
+uint64_t queue_words(uint64_t n);
+hipError_t launch_leaf_queue(const uint8_t* base, const uint64_t* off, const uint64_t* len,
+                             const uint32_t* perm, uint64_t n, bool aligned, bool ring, uint32_t* q,
+                             uint32_t waves, uint8_t* nodes, hipStream_t s);
 hipError_t launch_reduce(uint8_t* nodes, uint64_t n, int from_level, int top, hipStream_t s);
 hipError_t launch_bfs_image(const uint8_t* nodes, const BfsLayout& lay, uint8_t* img,
                             hipStream_t s);

@@ -376,13 +376,134 @@ __device__ __forceinline__ void sha1_blocks_runs(const uint8_t* p, uint32_t nful
     }
 }
 
+// Deep register prefetch for ragged batches: a long value is one chain of
+// dependent compressions, and while its wave runs nearly alone (the short waves
+// have finished) one block of lookahead cannot cover HBM latency under load.
+// D windows are in flight; the loop is unrolled by D so every buffer index is
+// static.  Aligned: 4 chunks per window; unaligned: 5 chunks + v_perm funnel.
+template <bool ALIGNED, int D>
+__device__ __forceinline__ void sha1_blocks_deep(const uint8_t* p, uint32_t nfull, uint32_t h[5]) {
+    constexpr int C = ALIGNED ? 4 : 5;
+    const uint32_t s = ALIGNED ? 0u : uint32_t(reinterpret_cast<uintptr_t>(p) & 15);
+    const uint4* q0 = reinterpret_cast<const uint4*>(p - s);
+    uint4 buf[D][C];
+    auto load = [&](int slot, uint32_t b) {
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+            buf[slot][c] = (c < 4 || s > 0) ? q0[4 * b + c] : make_uint4(0u, 0u, 0u, 0u);
+    };
+    auto use = [&](int slot, uint32_t w[16]) {
+        if (ALIGNED) {
+            be16_from_raw(buf[slot], w);
+        } else {
+            uint32_t d[20];
+#pragma unroll
+            for (int c = 0; c < 5; ++c) {
+                d[4 * c] = buf[slot][c].x;
+                d[4 * c + 1] = buf[slot][c].y;
+                d[4 * c + 2] = buf[slot][c].z;
+                d[4 * c + 3] = buf[slot][c].w;
+            }
+            be16_funnel(d, s, w);
+        }
+    };
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+        if (uint32_t(i) < nfull) load(i, uint32_t(i));
+    uint32_t b = 0;
+    for (; b + D <= nfull; b += D) {
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+            uint32_t w[16];
+            use(i, w);
+            if (b + i + D < nfull) load(i, b + i + D);
+            sha1_compress(h, w);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < D - 1; ++i) {
+        if (b + i < nfull) {
+            uint32_t w[16];
+            use(i, w);
+            sha1_compress(h, w);
+        }
+    }
+}
+
+// Ragged values of any alignment through a wave-private LDS ring of aligned
+// 64-B chunks (two 4 KiB slots; chunk c of every value in slot c & 1).  DMA
+// role as in the LOAD 1 path: wave-instruction k moves one chunk of values
+// 16k .. 16k+15, 64 contiguous bytes each, so one instruction touches 16
+// segments instead of 64 scattered 16-B pieces.  Block b of a value at byte
+// offset o = p & 63 spans chunks b and b+1: the lane reads the five quads
+// holding bytes [o, o + 64) and funnels them by o & 15.  Chunk b+2 goes into
+// block b's slot once its reads are done, so one block of compute (and the
+// other resident waves) covers the DMA.  Only chunks holding full-block bytes
+// are fetched: an aligned 64-B chunk with one valid byte lies in that byte's
+// page, so nothing outside the value's pages is read.
+__device__ __forceinline__ void sha1_blocks_ring(uint8_t* wbuf, const uint8_t* p, uint32_t my_nfull,
+                                                 uint32_t h[5]) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t o = uint32_t(reinterpret_cast<uintptr_t>(p)) & 63u;
+    const uint32_t nch = my_nfull ? my_nfull + (o != 0u) : 0u;
+    const uint32_t dq = (uint32_t(lane) & 3u) ^ ((uint32_t(lane) >> 4) & 3u);
+    const uint8_t* src[4];
+    uint32_t nc[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int j = 16 * k + (lane >> 2);
+        const uint64_t aj = uint64_t(__shfl(int64_t(reinterpret_cast<uintptr_t>(p - o)), j));
+        src[k] = reinterpret_cast<const uint8_t*>(aj) + 16 * dq;
+        nc[k] = uint32_t(__shfl(int(nch), j));
+    }
+    const uint32_t nmax = wave_max_u32(my_nfull);
+    if (nmax == 0) return;
+    auto issue = [&](uint32_t c) {
+        uint8_t* dst = wbuf + 4096 * (c & 1u);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (c < nc[k]) __builtin_amdgcn_global_load_lds(src[k] + 64ull * c, dst + 1024 * k, 16, 0, 0);
+    };
+    // byte offset in wbuf of quad i of the window for an even block; an odd
+    // block swaps the slots (bit 12)
+    const uint32_t swz = (uint32_t(lane) >> 2) & 3u;
+    uint32_t ro[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        const uint32_t qi = (o >> 4) + uint32_t(i);
+        ro[i] = (qi >> 2) * 4096u + 64u * uint32_t(lane) + 16u * ((qi & 3u) ^ swz);
+    }
+    const uint32_t s = o & 15u;
+    issue(0u);
+    issue(1u);
+    for (uint32_t b = 0; b < nmax; ++b) {
+        const uint32_t flip = (b & 1u) << 12;
+        uint32_t d[20];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            const uint4 c = *reinterpret_cast<const uint4*>(wbuf + (ro[i] ^ flip));
+            d[4 * i] = c.x;
+            d[4 * i + 1] = c.y;
+            d[4 * i + 2] = c.z;
+            d[4 * i + 3] = c.w;
+        }
+        uint32_t w[16];
+        be16_funnel(d, s, w);
+        if (b + 2 <= nmax) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot reads done before refill
+            issue(b + 2);
+        }
+        if (b < my_nfull) sha1_compress(h, w);
+    }
+}
+
 // MODE 0: value i at base + i*stride, length L.  MODE 1: base + off[i], len[i].
 // perm (MODE 1 only, nullable): lane i hashes leaf perm[i] (length bucketing).
 // FUSE: also build levels 1..min(8, top) of this block's subtree.
 // LOAD: 0 = any alignment (register funnel); 1 = 16-byte aligned, LDS-DMA
 // stage; 2 = aligned, direct loads; 3 = aligned, direct non-temporal loads.
 template <int MODE, bool FUSE, int LOAD>
-__global__ __launch_bounds__(kBlock, LOAD >= 4 ? 4 : kLeafWavesPerSimd) void k_leaf(const uint8_t* __restrict__ base,
+__global__ __launch_bounds__(kBlock, LOAD >= 6 ? 2 : (LOAD >= 4 ? 4 : kLeafWavesPerSimd)) void k_leaf(const uint8_t* __restrict__ base,
                                                   const uint64_t* __restrict__ off,
                                                   const uint64_t* __restrict__ len, uint64_t stride,
                                                   uint64_t L, const uint32_t* __restrict__ perm,
@@ -413,8 +534,11 @@ __global__ __launch_bounds__(kBlock, LOAD >= 4 ? 4 : kLeafWavesPerSimd) void k_l
             if (LOAD == 2) sha1_blocks_direct<false>(p, uint32_t(ln >> 6), h);
             else if (LOAD == 3) sha1_blocks_direct<true>(p, uint32_t(ln >> 6), h);
             else if (LOAD == 4) sha1_blocks_runs<2>(p, uint32_t(ln >> 6), h);
-            else sha1_blocks_runs<4>(p, uint32_t(ln >> 6), h);
-            sha1_tail<true>(p, ln, h);
+            else if (LOAD == 5) sha1_blocks_runs<4>(p, uint32_t(ln >> 6), h);
+            else if (LOAD == 6) sha1_blocks_deep<true, 4>(p, uint32_t(ln >> 6), h);
+            else sha1_blocks_deep<false, 4>(p, uint32_t(ln >> 6), h);
+            if (LOAD == 7) sha1_tail<false>(p, ln, h);
+            else sha1_tail<true>(p, ln, h);
             store_digest(nodes, leaf, h);
         }
     } else if (LOAD == 1) {
@@ -482,6 +606,100 @@ __global__ __launch_bounds__(kBlock, LOAD >= 4 ? 4 : kLeafWavesPerSimd) void k_l
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
         const size_t w_ = size_t(blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6);
         g_diag[w_ * 8 + 6] = (uint64_t(xcc) << 32) | hw;
+    }
+#endif
+}
+
+// K1q: ragged batches, work-queue form.  Values are length-sorted, longest
+// first, and cut into 64-value groups.  A group is one wavefront's work, and a
+// group's 64 chains run as long as its longest value, so the batch can finish
+// no sooner than its longest group.  Static dispatch places consecutive
+// (= equally long) workgroups on one CU, which stacks the longest chains on a
+// few SIMDs.  Here each wave (64-thread workgroup, two per SIMD) reads its
+// SIMD id: the first wave on a SIMD pulls groups from the long end at priority
+// 3, the others pull from the short end and fill the issue slots the long
+// chain leaves.  The two ends meet; a per-group claim flag settles the last
+// group.  Every wave exits once its end meets the other one.
+//
+// q: [0] front ticket, [1] back ticket, [2, 2 + kSimdKeys) per-SIMD arrivals,
+//    then ngroups claim flags; zeroed before the launch.
+constexpr uint32_t kSimdKeys = 8 * 8 * 2 * 16 * 4;  // xcc, se, sh, cu, simd
+
+template <int LOAD>
+__global__ __launch_bounds__(64, LOAD == 8 ? 4 : 2) void k_leaf_queue(const uint8_t* __restrict__ base,
+                                                       const uint64_t* __restrict__ off,
+                                                       const uint64_t* __restrict__ len,
+                                                       const uint32_t* __restrict__ perm, uint64_t n,
+                                                       uint32_t ngroups, uint32_t* __restrict__ q,
+                                                       uint8_t* __restrict__ nodes) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[LOAD == 8 ? 8192 : 16];
+    const int lane = threadIdx.x;
+    uint32_t hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    const uint32_t key = ((((xcc & 7) * 8 + ((hw >> 13) & 7)) * 2 + ((hw >> 12) & 1)) * 16 + ((hw >> 8) & 15)) * 4 +
+                         ((hw >> 4) & 3);
+    uint32_t slot = 0;
+    if (lane == 0) slot = atomicAdd(q + 2 + key, 1u);
+    slot = __builtin_amdgcn_readfirstlane(slot);
+    const bool front = slot == 0;
+    if (front) __builtin_amdgcn_s_setprio(3);
+    uint32_t* claimed = q + 2 + kSimdKeys;
+#ifdef NKV_DIAG
+    uint64_t d_t0 = __builtin_amdgcn_s_memrealtime(), d_c0 = __builtin_amdgcn_s_memtime(), d_first = 0;
+    uint64_t d_groups = 0, d_blocks = 0;
+#endif
+    while (true) {
+        uint32_t g = 0xFFFFFFFFu;
+        if (lane == 0) {
+            const uint32_t t = atomicAdd(q + (front ? 0 : 1), 1u);
+            if (t < ngroups) {
+                const uint32_t c = front ? t : ngroups - 1 - t;
+                if (atomicExch(claimed + c, 1u) == 0u) g = c;
+            }
+        }
+        g = __builtin_amdgcn_readfirstlane(g);
+        if (g == 0xFFFFFFFFu) break;
+        const uint64_t i = uint64_t(g) * 64 + lane;
+        if (LOAD == 8) {
+            const bool live = i < n;
+            const uint64_t leaf = live ? perm[i] : 0;
+            const uint8_t* p = live ? base + off[leaf] : base;
+            const uint64_t ln = live ? len[leaf] : 0;
+            uint32_t h[5];
+            sha1_init(h);
+            sha1_blocks_ring(smem, p, uint32_t(ln >> 6), h);
+            if (live) {
+                sha1_tail<false>(p, ln, h);
+                store_digest(nodes, leaf, h);
+            }
+        } else if (i < n) {
+            const uint64_t leaf = perm[i];
+            const uint8_t* p = base + off[leaf];
+            const uint64_t ln = len[leaf];
+            uint32_t h[5];
+            sha1_init(h);
+            sha1_blocks_deep<LOAD == 6, 4>(p, uint32_t(ln >> 6), h);
+            if (LOAD == 6) sha1_tail<true>(p, ln, h);
+            else sha1_tail<false>(p, ln, h);
+            store_digest(nodes, leaf, h);
+        }
+#ifdef NKV_DIAG
+        d_blocks += wave_max_u32(i < n ? uint32_t(len[perm[i]] >> 6) : 0u);
+        if (d_groups++ == 0) d_first = __builtin_amdgcn_s_memrealtime();
+#endif
+    }
+#ifdef NKV_DIAG
+    if (g_diag && lane == 0) {
+        unsigned long long* d = g_diag + size_t(blockIdx.x) * 8;
+        d[0] = d_t0;
+        d[1] = __builtin_amdgcn_s_memrealtime();
+        d[2] = d_c0;
+        d[3] = __builtin_amdgcn_s_memtime();
+        d[4] = (uint64_t(slot) << 32) | key;
+        d[5] = d_groups;
+        d[6] = d_blocks;
+        d[7] = d_first;
     }
 #endif
 }
@@ -636,6 +854,8 @@ static void leaf_dispatch(int load, const uint8_t* base, const uint64_t* off, co
         case 3: leaf_kernel<MODE, FUSE, 3>(base, off, len, stride, L, perm, n, top, nodes, s); break;
         case 4: leaf_kernel<MODE, FUSE, 4>(base, off, len, stride, L, perm, n, top, nodes, s); break;
         case 5: leaf_kernel<MODE, FUSE, 5>(base, off, len, stride, L, perm, n, top, nodes, s); break;
+        case 6: leaf_kernel<MODE, FUSE, 6>(base, off, len, stride, L, perm, n, top, nodes, s); break;
+        case 7: leaf_kernel<MODE, FUSE, 7>(base, off, len, stride, L, perm, n, top, nodes, s); break;
         default: leaf_kernel<MODE, FUSE, 0>(base, off, len, stride, L, perm, n, top, nodes, s); break;
     }
 }
@@ -651,12 +871,30 @@ hipError_t launch_leaf_strided(const uint8_t* base, uint64_t stride, uint64_t L,
 
 hipError_t launch_leaf_offsets(const uint8_t* base, const uint64_t* off, const uint64_t* len,
                                const uint32_t* perm, uint64_t n, int top, bool fuse, bool aligned,
-                               int load, uint8_t* nodes, hipStream_t s) {
-    if (!aligned) load = 0;
+                               int load, uint8_t* nodes, hipStream_t s, bool deep) {
+    if (perm && deep) load = aligned ? 6 : 7;  // ragged, length-sorted: deep prefetch
+    else if (!aligned) load = 0;
     if (fuse && !perm) leaf_dispatch<1, true>(load, base, off, len, 0, 0, nullptr, n, top, nodes, s);
     else leaf_dispatch<1, false>(load, base, off, len, 0, 0, perm, n, top, nodes, s);
     return hipGetLastError();
 }
+
+hipError_t launch_leaf_queue(const uint8_t* base, const uint64_t* off, const uint64_t* len,
+                             const uint32_t* perm, uint64_t n, bool aligned, bool ring, uint32_t* q,
+                             uint32_t waves, uint8_t* nodes, hipStream_t s) {
+    const uint32_t ngroups = uint32_t((n + 63) / 64);
+    hipError_t e = hipMemsetAsync(q, 0, queue_words(n) * sizeof(uint32_t), s);
+    if (e != hipSuccess) return e;
+    if (ring)
+        hipLaunchKernelGGL(k_leaf_queue<8>, dim3(waves), dim3(64), 0, s, base, off, len, perm, n, ngroups, q, nodes);
+    else if (aligned)
+        hipLaunchKernelGGL(k_leaf_queue<6>, dim3(waves), dim3(64), 0, s, base, off, len, perm, n, ngroups, q, nodes);
+    else
+        hipLaunchKernelGGL(k_leaf_queue<7>, dim3(waves), dim3(64), 0, s, base, off, len, perm, n, ngroups, q, nodes);
+    return hipGetLastError();
+}
+
+uint64_t queue_words(uint64_t n) { return 2 + kSimdKeys + (n + 63) / 64; }
 
 hipError_t launch_reduce(uint8_t* nodes, uint64_t n, int from_level, int top, hipStream_t s) {
     int j0 = from_level;

@@ -127,6 +127,41 @@ def test_mixed_sizes_log_uniform(nkv, oracle, load):
     assert np.array_equal(nodes, want)
 
 
+@pytest.mark.parametrize("deep", [0, 1, 2, 3])
+@pytest.mark.parametrize("n,packed", [(1, True), (63, True), (65, False), (3001, True), (3001, False),
+                                      (20000, True)])
+def test_ragged_deep_and_queue_paths(nkv, oracle, deep, n, packed):
+    """Length-sorted ragged batches through each NKV_OPT_DEEP_PREFETCH mode:
+    0 = one-block lookahead, 1 = several blocks, 2 = the work-queue kernel (groups
+    pulled from both ends, claim flags at the meeting point), 3 = the work-queue
+    kernel with the LDS chunk ring.  Packed = back to
+    back (unaligned path); otherwise 16-B aligned starts (aligned path)."""
+    torch = _torch()
+    _lib, ctx = nkv
+    _bind(torch, ctx)
+    L = _lib.lib()
+    rng = np.random.default_rng(1000 * n + deep)
+    lens = np.floor(2.0 ** rng.uniform(0, 15, n)).astype(np.uint64)
+    lens[rng.integers(0, n, max(1, n // 50))] = 0
+    step = lens if packed else (lens + 15) // 16 * 16
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum(step[:-1])
+    data = oracle.splitmix64_bytes(int(off[-1] + lens[-1]) + 1, SEED + n)
+    d_data, d_off, d_len = _dev(torch, data), _dev(torch, off), _dev(torch, lens)
+    d_nodes = torch.zeros(L.nkv_total_nodes(n) * 20, dtype=torch.uint8, device="cuda")
+    ctx.set_option(_lib.NKV_OPT_DEEP_PREFETCH, deep)
+    try:
+        for _ in range(2):  # the queue state is reset per launch
+            d_nodes.zero_()
+            _lib.check(L.nkv_tree_from_values_dev(ctx.h, d_data.data_ptr(), d_off.data_ptr(), d_len.data_ptr(),
+                                                  n, d_nodes.data_ptr()))
+            torch.cuda.synchronize()
+            want = oracle.tree_from_digests(oracle.leaf_hashes(data, off, lens, threads=8))
+            assert np.array_equal(d_nodes.cpu().numpy().reshape(-1, 20), want)
+    finally:
+        ctx.set_option(_lib.NKV_OPT_DEEP_PREFETCH, 1)
+
+
 @pytest.mark.parametrize("n", EDGE_N)
 def test_tree_build_from_digests(nkv, oracle, n):
     _lib, ctx = nkv

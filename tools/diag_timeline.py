@@ -85,6 +85,22 @@ def main():
     dur = ends - starts
     order = np.argsort(-dur)
     print("longest waves (us): " + ", ".join(f"w{int(i)} start {starts[i]:.0f} dur {dur[i]:.0f}" for i in order[:6]))
+    hw = (d[:, 6].astype(np.uint64) & np.uint64(0xFFFFFFFF)).astype(np.int64)
+    xcc_all = (d[:, 6].astype(np.uint64) >> np.uint64(32)).astype(np.int64)
+    simd = (hw >> 4) & 3
+    cu = (hw >> 8) & 15
+    sh = (hw >> 12) & 1
+    se = (hw >> 13) & 7
+    simd_key = (((xcc_all * 8 + se) * 2 + sh) * 16 + cu) * 4 + simd
+    cu_key = simd_key // 4
+    top = order[:1024]
+    from collections import Counter
+    cs = Counter(simd_key[top].tolist())
+    cc = Counter(cu_key[top].tolist())
+    print(f"1024 longest waves: on {len(cs)} distinct SIMDs (max {max(cs.values())} per SIMD), "
+          f"{len(cc)} distinct CUs (max {max(cc.values())} per CU); all waves on {len(set(simd_key.tolist()))} SIMDs")
+    wpsimd = Counter(simd_key.tolist())
+    print(f"waves per SIMD over the kernel: min {min(wpsimd.values())} max {max(wpsimd.values())}")
     for x in range(8):
         m = xcc == x
         if m.any():

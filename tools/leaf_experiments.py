@@ -47,6 +47,19 @@ def main():
             variants[f"{name:10s} leafonly 1Mx4K"] = (with_load(mode, leaf_only(M, 4096, 4096)), M * 4096)
             variants[f"{name:10s} fused 1Mx4K stride0"] = (with_load(mode, fused(M, 0, 4096)), M * 4096)
             variants[f"{name:10s} fused 4Mx1K"] = (with_load(mode, fused(4 * M, 1024, 1024)), 4 * M * 1024)
+    elif sel == "long":
+        # few, long chains: 1 and 2 waves per SIMD
+        for mode, name in ((1, "lds-dma"), (2, "direct"), (5, "runs256")):
+            variants[f"{name:8s} 64K x 64KiB (1 wave/SIMD)"] = (with_load(mode, fused(65536, 65536, 65536)), 65536 * 65536)
+            variants[f"{name:8s} 128K x 32KiB (2 waves/SIMD)"] = (with_load(mode, fused(131072, 32768, 32768)), 131072 * 32768)
+        offl = torch.from_numpy(np.arange(65536, dtype=np.int64) * 65536).cuda()
+        lenl = torch.full((65536,), 65536, dtype=torch.int64, device="cuda")
+        for deep in (0, 1):
+            def runl(deep=deep):
+                ctx.set_option(_lib.NKV_OPT_DEEP_PREFETCH, deep)
+                return L.nkv_tree_from_values_dev(ctx.h, big.data_ptr(), offl.data_ptr(), lenl.data_ptr(), 65536,
+                                                  nodes.data_ptr())
+            variants[f"offsets bucketed deep={deep} 64K x 64KiB"] = (runl, 65536 * 65536)
     else:
         # funnel (unaligned) vs aligned, strided and offset-array paths
         variants["strided aligned 1Mx4096"] = (fused(M, 4096, 4096), M * 4096)
