@@ -32,6 +32,10 @@ SEED = 0x6E616B65
 SEED_MIXED = 0x6E616B66
 
 
+LEAF_KERNEL = {-1: "library default", 0: "k_leaf, one-block lookahead", 1: "k_leaf, deep register prefetch",
+               2: "k_leaf_queue, deep register prefetch", 3: "k_leaf_queue, LDS chunk ring"}
+
+
 def mixed_lengths(target_bytes: int, seed: int):
     """BASELINE configs[2]: L = floor(2^U(6,16)) (64 B - 64 KiB, log-uniform), values
     packed back to back (so mostly unaligned), until the payload reaches target_bytes."""
@@ -245,7 +249,7 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u32",
-            "data": f"synthetic: splitmix64 bytes (seed {SEED:#x} + rank) generated in HBM",
+            "data": f"synthetic: splitmix64 bytes (seed {SEED_MIXED if mixed else SEED:#x} + rank) generated in HBM",
             "config": {
                 "workload": ("BASELINE configs[2]: mixed 64 B - 64 KiB log-uniform values packed back to back, "
                              + ("input order" if args.no_bucket else "length-bucketed")) if mixed else
@@ -257,7 +261,8 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_leaf<strided,fused,aligned> (leaf SHA-1 + first 8 levels)",
+                "kernel": ("leaf phase: length sort + ragged leaf SHA-1 (%s)" % LEAF_KERNEL.get(args.deep, "default"))
+                          if mixed else "k_leaf<strided,fused,aligned> (leaf SHA-1 + first 8 levels)",
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

@@ -22,6 +22,9 @@
  *   (*MerkleTree).Validate  ds/merkletree/merkletree.go:162-171 nkv_tree_build / nkv_tree_generic
  *                           ds/merkletree/merklenode.go:99-108    + 20-byte root compare
  *   record value location   core/record/record.go:191-199       nkv_locate_values_dev
+ *   record checksum         core/record/record.go:51 (New),     nkv_record_crc /
+ *     crc32.ChecksumIEEE    :163-169 (Deserialize check)        nkv_record_crc_dev /
+ *     over Key ++ Value                                         nkv_crc32_dev
  *
  * Conventions
  *   - Every function returns an nkv_status (0 = NKV_OK) unless noted; nothing
@@ -145,6 +148,17 @@ int nkv_tree_from_records(nkv_ctx *ctx, const uint8_t *stream, uint64_t stream_l
                           const uint64_t *rec_size, uint64_t n, uint8_t *root20,
                           uint8_t *nodes_out, uint8_t *img_out);
 
+/* Record checksums: CRC-32/IEEE of Key ++ Value of each
+ * serialized record (stream and rec_size as for nkv_tree_from_records).
+ * crc_out (nullable): n checksums, what record.New stores (record.go:51).
+ * *n_bad: records whose stored Crc differs from the recomputed one, the check
+ * record.Deserialize panics on (record.go:163-169); *first_bad: the lowest such
+ * index, UINT64_MAX if none.  NKV_ERR_INVALID if a header points outside the
+ * stream. */
+int nkv_record_crc(nkv_ctx *ctx, const uint8_t *stream, uint64_t stream_len,
+                   const uint64_t *rec_size, uint64_t n, uint32_t *crc_out, uint64_t *n_bad,
+                   uint64_t *first_bad);
+
 /* Serialize()'s file semantics: open O_WRONLY|O_CREAT (mode 0666) WITHOUT
  * O_TRUNC (merkletree.go:68), write len bytes at offset 0, close. */
 int nkv_write_file(const char *fname, const uint8_t *data, uint64_t len);
@@ -174,6 +188,16 @@ int nkv_record_offsets_dev(nkv_ctx *ctx, const uint64_t *d_rec_size, uint64_t n,
 int nkv_locate_values_dev(nkv_ctx *ctx, const void *d_stream, uint64_t stream_len,
                           const uint64_t *d_rec_off, uint64_t n, uint64_t *d_voff,
                           uint64_t *d_vlen);
+/* CRC-32/IEEE (Go crc32.ChecksumIEEE) of n byte spans d_base + d_off[i],
+ * d_len[i] (any alignment) into d_crc[i] */
+int nkv_crc32_dev(nkv_ctx *ctx, const void *d_base, const uint64_t *d_off, const uint64_t *d_len,
+                  uint64_t n, uint32_t *d_crc);
+/* Record checksums over Key ++ Value of the records at d_stream + d_rec_off[i].
+ * d_crc (nullable): n checksums.  d_stats (nullable, 3 x u64 on the device,
+ * overwritten): [0] records whose stored Crc differs, [1] the lowest such index
+ * (UINT64_MAX if none), [2] 1 if a header points outside the stream. */
+int nkv_record_crc_dev(nkv_ctx *ctx, const void *d_stream, uint64_t stream_len,
+                       const uint64_t *d_rec_off, uint64_t n, uint32_t *d_crc, uint64_t *d_stats);
 /* synthetic input: byte j = byte (j % 8) of splitmix64(seed, j / 8) */
 int nkv_fill_splitmix64_dev(nkv_ctx *ctx, void *d_buf, uint64_t nbytes, uint64_t seed);
 

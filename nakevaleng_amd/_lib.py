@@ -57,6 +57,7 @@ SIGNATURES = {
     "nkv_generic_bfs_size": (_u64, [_u64p, _u64]),
     "nkv_tree_generic": (_int, [_vp, _u8p, _u64p, _u64p, _u64, _u8p, _u8p, _u8p]),
     "nkv_tree_from_records": (_int, [_vp, _u8p, _u64, _u64p, _u64, _u8p, _u8p, _u8p]),
+    "nkv_record_crc": (_int, [_vp, _u8p, _u64, _u64p, _u64, ctypes.POINTER(ctypes.c_uint32), _u64p, _u64p]),
     "nkv_write_file": (_int, [ctypes.c_char_p, _u8p, _u64]),
     "nkv_leaf_hash_dev": (_int, [_vp, _vp, _vp, _vp, _u64, _vp]),
     "nkv_leaf_hash_strided_dev": (_int, [_vp, _vp, _u64, _u64, _u64, _vp]),
@@ -66,6 +67,8 @@ SIGNATURES = {
     "nkv_bfs_image_dev": (_int, [_vp, _vp, _u64, _vp]),
     "nkv_record_offsets_dev": (_int, [_vp, _vp, _u64, _vp]),
     "nkv_locate_values_dev": (_int, [_vp, _vp, _u64, _vp, _u64, _vp, _vp]),
+    "nkv_crc32_dev": (_int, [_vp, _vp, _vp, _vp, _u64, _vp]),
+    "nkv_record_crc_dev": (_int, [_vp, _vp, _u64, _vp, _u64, _vp, _vp]),
     "nkv_fill_splitmix64_dev": (_int, [_vp, _vp, _u64, _u64]),
 }
 

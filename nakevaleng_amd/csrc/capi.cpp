@@ -105,7 +105,7 @@ struct nkv_ctx {
     // per-call event triples (leaf start, leaf end / reduce start, reduce end)
     std::vector<hipEvent_t> ring;
     size_t ring_used = 0;
-    DevBuf d_data, d_off, d_len, d_nodes, d_img, d_tmp, d_err, d_aux, d_keys, d_perm, d_stmp, d_queue;
+    DevBuf d_data, d_off, d_len, d_nodes, d_img, d_tmp, d_err, d_aux, d_keys, d_perm, d_stmp, d_queue, d_stats;
     void* h_stage = nullptr;
     size_t h_cap = 0;
 };
@@ -339,7 +339,7 @@ void nkv_ctx_destroy(nkv_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (DevBuf* b : {&c->d_data, &c->d_off, &c->d_len, &c->d_nodes, &c->d_img, &c->d_tmp,
-                      &c->d_err, &c->d_aux, &c->d_keys, &c->d_perm, &c->d_stmp, &c->d_queue})
+                      &c->d_err, &c->d_aux, &c->d_keys, &c->d_perm, &c->d_stmp, &c->d_queue, &c->d_stats})
         if (b->p) (void)hipFree(b->p);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
     for (hipEvent_t e : c->ev)
@@ -606,6 +606,44 @@ int nkv_tree_from_records(nkv_ctx* c, const uint8_t* stream, uint64_t stream_len
     return finish_tree(c, nodes, n, root20, nodes_out, img_out);
 }
 
+int nkv_record_crc(nkv_ctx* c, const uint8_t* stream, uint64_t stream_len, const uint64_t* rec_size,
+                   uint64_t n, uint32_t* crc_out, uint64_t* n_bad, uint64_t* first_bad) {
+    TRY(bind(c));
+    if (n_bad) *n_bad = 0;
+    if (first_bad) *first_bad = ~0ull;
+    if (n == 0) return NKV_OK;
+    if (!stream || !rec_size) return NKV_ERR_INVALID;
+    uint64_t sum = 0;
+    for (uint64_t i = 0; i < n; ++i) sum += rec_size[i];
+    if (sum > stream_len) return NKV_ERR_INVALID;
+    TRY(grow_host(c, std::max<uint64_t>(stream_len + 8 * n, 4 * n + 24)));
+    TRY(grow(c->d_data, stream_len));
+    TRY(grow(c->d_aux, 8 * n));
+    TRY(grow(c->d_len, 8 * n));
+    TRY(grow(c->d_off, 4 * n));
+    uint8_t* h = static_cast<uint8_t*>(c->h_stage);
+    memcpy(h, stream, stream_len);
+    memcpy(h + stream_len, rec_size, 8 * n);
+    HIPTRY(hipMemcpyAsync(c->d_data.p, h, stream_len, hipMemcpyHostToDevice, c->stream));
+    HIPTRY(hipMemcpyAsync(c->d_aux.p, h + stream_len, 8 * n, hipMemcpyHostToDevice, c->stream));
+    uint64_t* rec_off = static_cast<uint64_t*>(c->d_len.p);
+    TRY(nkv_record_offsets_dev(c, static_cast<const uint64_t*>(c->d_aux.p), n, rec_off));
+    TRY(grow(c->d_stats, 24));
+    uint32_t* d_crc = static_cast<uint32_t*>(c->d_off.p);
+    uint64_t* d_stats = static_cast<uint64_t*>(c->d_stats.p);
+    TRY(nkv_record_crc_dev(c, c->d_data.p, stream_len, rec_off, n, d_crc, d_stats));
+    // the staging copies above have been consumed once the stream reaches here
+    uint64_t* hs = reinterpret_cast<uint64_t*>(h);
+    HIPTRY(hipMemcpyAsync(hs, d_stats, 24, hipMemcpyDeviceToHost, c->stream));
+    if (crc_out) HIPTRY(hipMemcpyAsync(h + 24, d_crc, 4 * n, hipMemcpyDeviceToHost, c->stream));
+    HIPTRY(hipStreamSynchronize(c->stream));
+    if (hs[2]) return NKV_ERR_INVALID;
+    if (n_bad) *n_bad = hs[0];
+    if (first_bad) *first_bad = hs[1];
+    if (crc_out) memcpy(crc_out, h + 24, 4 * n);
+    return NKV_OK;
+}
+
 int nkv_write_file(const char* fname, const uint8_t* data, uint64_t len) {
     if (!fname || (!data && len)) return NKV_ERR_INVALID;
     int fd = open(fname, O_WRONLY | O_CREAT, 0666);  // no O_TRUNC: merkletree.go:68
@@ -707,6 +745,35 @@ int nkv_locate_values_dev(nkv_ctx* c, const void* d_stream, uint64_t stream_len,
     HIPTRY(hipMemcpyAsync(&h, err, 4, hipMemcpyDeviceToHost, c->stream));
     HIPTRY(hipStreamSynchronize(c->stream));
     return h ? NKV_ERR_INVALID : NKV_OK;
+}
+
+int nkv_crc32_dev(nkv_ctx* c, const void* d_base, const uint64_t* d_off, const uint64_t* d_len, uint64_t n,
+                  uint32_t* d_crc) {
+    TRY(bind(c));
+    if (n == 0) return NKV_OK;
+    if (!d_base || !d_off || !d_len || !d_crc) return NKV_ERR_INVALID;
+    return st(launch_crc_spans(static_cast<const uint8_t*>(d_base), d_off, d_len, n, d_crc, c->stream));
+}
+
+int nkv_record_crc_dev(nkv_ctx* c, const void* d_stream, uint64_t stream_len, const uint64_t* d_rec_off,
+                       uint64_t n, uint32_t* d_crc, uint64_t* d_stats) {
+    TRY(bind(c));
+    if (!d_stream && n) return NKV_ERR_INVALID;
+    if (n && !d_rec_off) return NKV_ERR_INVALID;
+    if (n == 0) {
+        if (d_stats) {
+            HIPTRY(hipMemsetAsync(d_stats, 0, 24, c->stream));
+            HIPTRY(hipMemsetAsync(d_stats + 1, 0xFF, 8, c->stream));
+        }
+        return NKV_OK;
+    }
+    unsigned long long* stats = reinterpret_cast<unsigned long long*>(d_stats);
+    if (!stats) {
+        TRY(grow(c->d_stats, 24));
+        stats = static_cast<unsigned long long*>(c->d_stats.p);
+    }
+    return st(launch_record_crc(static_cast<const uint8_t*>(d_stream), stream_len, d_rec_off, n, d_crc, stats,
+                                c->stream));
 }
 
 int nkv_fill_splitmix64_dev(nkv_ctx* c, void* d_buf, uint64_t nbytes, uint64_t seed) {

@@ -1,0 +1,193 @@
+// crc.hip -- record checksums on gfx950.
+//
+// Reference: core/record/record.go:51 (New: Crc = crc32.ChecksumIEEE(key ++
+// value)) and :163-169 (Deserialize: recompute, panic on mismatch); the
+// arithmetic is Go's hash/crc32 IEEE (reflected, poly 0xEDB88320, init and
+// final XOR 0xFFFFFFFF).  Key and value are contiguous in a serialized record
+// (record.go:191-204), so the checksum covers one byte span per record:
+// [rec + 30, rec + 30 + KeySize + ValueSize).
+//
+// One lane per span.  Slicing-by-4: one 32-bit word per step, four table
+// lookups from LDS.  The four 256-entry tables are replicated kCrcCopies times
+// and interleaved so lane l reads copy l % kCrcCopies: a ds_read_b32 is served
+// in two 32-lane groups over 32 banks, entry e of table k of copy c sits in
+// bank (8 e + c) % 32, so the 4 lanes sharing a copy inside a group collide only
+// when their entries agree mod 4 (about 2-way on random data instead of ~4-way
+// with one copy).
+//
+// Per span: 0-3 head bytes (byte steps) up to the first 4-aligned address,
+// then whole aligned words in aligned 64-byte chunks (4 x global_load_dwordx4
+// per lane per chunk; every loaded chunk holds a span byte, so no load leaves
+// the span's pages), then 0-3 tail bytes.  Chunks a lane does not own are
+// masked; only a span's first and last chunk mask single words.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "internal.hpp"
+
+namespace nkv {
+
+struct CrcTables {
+    uint32_t t[4][256];
+};
+
+constexpr CrcTables make_crc_tables() {
+    CrcTables r{};
+    for (uint32_t i = 0; i < 256; ++i) {
+        uint32_t c = i;
+        for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (0xEDB88320u & (0u - (c & 1u)));
+        r.t[0][i] = c;
+    }
+    for (int k = 1; k < 4; ++k)
+        for (uint32_t i = 0; i < 256; ++i) r.t[k][i] = (r.t[k - 1][i] >> 8) ^ r.t[0][r.t[k - 1][i] & 0xFFu];
+    return r;
+}
+
+__constant__ CrcTables c_crc = make_crc_tables();
+
+constexpr int kCrcCopies = 8;
+constexpr int kCrcBlock = 256;
+
+// tab: this lane's copy (LDS base + lane % kCrcCopies)
+__device__ __forceinline__ uint32_t crc_lut(const uint32_t* tab, int k, uint32_t e) {
+    return tab[(uint32_t(k) * 256u + e) * kCrcCopies];
+}
+
+__device__ __forceinline__ uint32_t crc_word(uint32_t crc, uint32_t w, const uint32_t* tab) {
+    const uint32_t x = crc ^ w;
+    return crc_lut(tab, 3, x & 0xFFu) ^ crc_lut(tab, 2, (x >> 8) & 0xFFu) ^ crc_lut(tab, 1, (x >> 16) & 0xFFu) ^
+           crc_lut(tab, 0, x >> 24);
+}
+
+__device__ __forceinline__ uint32_t crc_byte(uint32_t crc, uint32_t b, const uint32_t* tab) {
+    return crc_lut(tab, 0, (crc ^ b) & 0xFFu) ^ (crc >> 8);
+}
+
+__device__ __forceinline__ uint64_t crc_ld_le64(const uint8_t* p) {
+    uint64_t v = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v |= uint64_t(p[i]) << (8 * i);
+    return v;
+}
+
+__device__ __forceinline__ uint32_t crc_wave_max(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, uint32_t(__shfl_xor(int(v), o)));
+    return __builtin_amdgcn_readfirstlane(v);
+}
+
+// CRC-32/IEEE of [s, s + len) (finalised).  Every lane of the wave calls it
+// (dead lanes with len 0).
+__device__ __forceinline__ uint32_t crc_span(const uint8_t* s, uint64_t len, const uint32_t* tab) {
+    uint32_t crc = 0xFFFFFFFFu;
+    const uint64_t sa = uint64_t(reinterpret_cast<uintptr_t>(s));
+    const uint64_t ea = sa + len;
+    const uint64_t s4 = (sa + 3) & ~uint64_t(3);
+    const uint64_t e4 = ea & ~uint64_t(3);
+    const uint64_t hb = s4 < ea ? s4 : ea;
+    for (uint64_t a = sa; a < hb; ++a) crc = crc_byte(crc, s[a - sa], tab);
+    const uint64_t A = s4 & ~uint64_t(63);
+    const uint32_t nch = e4 > s4 ? uint32_t((e4 - A + 63) >> 6) : 0u;
+    const uint32_t nmax = crc_wave_max(nch);
+    // s + (A - sa): stays a global pointer (no integer-to-pointer cast)
+    const uint4* q = reinterpret_cast<const uint4*>(s + (A - sa));
+    for (uint32_t c = 0; c < nmax; ++c) {
+        if (c < nch) {
+            uint4 v[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = q[4 * c + i];
+            const uint32_t w[16] = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w,
+                                    v[2].x, v[2].y, v[2].z, v[2].w, v[3].x, v[3].y, v[3].z, v[3].w};
+            const uint64_t b0 = A + 64ull * c;
+            if (b0 >= s4 && b0 + 64 <= e4) {
+#pragma unroll
+                for (int j = 0; j < 16; ++j) crc = crc_word(crc, w[j], tab);
+            } else {
+                const uint64_t lo = s4 > b0 ? (s4 - b0) >> 2 : 0;
+                const uint64_t hi = e4 - b0 >= 64 ? 16 : (e4 - b0) >> 2;
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    const uint32_t u = crc_word(crc, w[j], tab);
+                    crc = (uint64_t(j) >= lo && uint64_t(j) < hi) ? u : crc;
+                }
+            }
+        }
+    }
+    const uint64_t tb = e4 > hb ? e4 : hb;
+    for (uint64_t a = tb; a < ea; ++a) crc = crc_byte(crc, s[a - sa], tab);
+    return ~crc;
+}
+
+// RECORDS: span of record i from its header at base + off[i] (len unused),
+// checked against stream_len; stats[0] += records whose stored Crc differs,
+// stats[1] = min such index, stats[2] |= 1 on a header outside the stream.
+// Otherwise span i = [base + off[i], + len[i]).
+template <bool RECORDS>
+__global__ __launch_bounds__(kCrcBlock) void k_crc(const uint8_t* __restrict__ base,
+                                                   const uint64_t* __restrict__ off,
+                                                   const uint64_t* __restrict__ len, uint64_t stream_len,
+                                                   uint64_t n, uint32_t* __restrict__ out,
+                                                   unsigned long long* __restrict__ stats) {
+    __shared__ uint32_t tab[4 * 256 * kCrcCopies];
+    for (int i = threadIdx.x; i < 4 * 256 * kCrcCopies; i += kCrcBlock) tab[i] = (&c_crc.t[0][0])[i / kCrcCopies];
+    __syncthreads();
+    const uint32_t* mytab = tab + (threadIdx.x % kCrcCopies);
+    const uint64_t i = uint64_t(blockIdx.x) * kCrcBlock + threadIdx.x;
+    const uint8_t* s = base;
+    uint64_t L = 0;
+    uint32_t stored = 0;
+    bool live = i < n, hdr_bad = false;
+    if (live) {
+        if (RECORDS) {
+            const uint64_t r = off[i];
+            if (r + 30 <= stream_len) {
+                const uint64_t ks = crc_ld_le64(base + r + 14);
+                const uint64_t vs = crc_ld_le64(base + r + 22);
+                if (ks <= stream_len && vs <= stream_len && r + 30 + ks + vs <= stream_len) {
+                    s = base + r + 30;
+                    L = ks + vs;
+                    stored = uint32_t(base[r]) | uint32_t(base[r + 1]) << 8 | uint32_t(base[r + 2]) << 16 |
+                             uint32_t(base[r + 3]) << 24;
+                } else {
+                    hdr_bad = true;
+                }
+            } else {
+                hdr_bad = true;
+            }
+        } else {
+            s = base + off[i];
+            L = len[i];
+        }
+    }
+    const uint32_t crc = crc_span(s, L, mytab);
+    if (!live) return;
+    if (out) out[i] = crc;
+    if (RECORDS && stats) {
+        if (hdr_bad) atomicOr(stats + 2, 1ull);
+        else if (crc != stored) {
+            atomicAdd(stats, 1ull);
+            atomicMin(stats + 1, (unsigned long long)i);
+        }
+    }
+}
+
+hipError_t launch_crc_spans(const uint8_t* base, const uint64_t* off, const uint64_t* len, uint64_t n,
+                            uint32_t* out, hipStream_t s) {
+    const uint64_t grid = (n + kCrcBlock - 1) / kCrcBlock;
+    hipLaunchKernelGGL(k_crc<false>, dim3(uint32_t(grid)), dim3(kCrcBlock), 0, s, base, off, len, uint64_t(0), n,
+                       out, nullptr);
+    return hipGetLastError();
+}
+
+hipError_t launch_record_crc(const uint8_t* stream, uint64_t stream_len, const uint64_t* rec_off, uint64_t n,
+                             uint32_t* out, unsigned long long* stats, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(stats, 0, 3 * sizeof(unsigned long long), s);
+    if (e == hipSuccess) e = hipMemsetAsync(stats + 1, 0xFF, sizeof(unsigned long long), s);
+    if (e != hipSuccess) return e;
+    const uint64_t grid = (n + kCrcBlock - 1) / kCrcBlock;
+    hipLaunchKernelGGL(k_crc<true>, dim3(uint32_t(grid)), dim3(kCrcBlock), 0, s, stream, rec_off,
+                       static_cast<const uint64_t*>(nullptr), stream_len, n, out, stats);
+    return hipGetLastError();
+}
+
+}  // namespace nkv

@@ -47,6 +47,12 @@ hipError_t scan_exclusive_u64(const uint64_t* in, uint64_t* out, uint64_t n, voi
 // Two-phase (tmp == nullptr: size query).  The permutation lands in perm + n.
 hipError_t sort_by_length_desc(const uint64_t* len, uint64_t n, uint32_t* keys, uint32_t* perm,
                                void* tmp, size_t* tmp_bytes, hipStream_t s);
+// crc.hip: CRC-32/IEEE of byte spans / of records' Key ++ Value (stats: 3 x u64,
+// initialised by the launcher).
+hipError_t launch_crc_spans(const uint8_t* base, const uint64_t* off, const uint64_t* len, uint64_t n,
+                            uint32_t* out, hipStream_t s);
+hipError_t launch_record_crc(const uint8_t* stream, uint64_t stream_len, const uint64_t* rec_off, uint64_t n,
+                             uint32_t* out, unsigned long long* stats, hipStream_t s);
 hipError_t launch_fill(uint8_t* buf, uint64_t nbytes, uint64_t seed, hipStream_t s);
 
 }  // namespace nkv

@@ -88,3 +88,35 @@ def value_spans(stream: bytes, rec_sizes: np.ndarray) -> Tuple[np.ndarray, np.nd
         lens[i] = vs
         p += int(rs)
     return offs, lens
+
+
+def checksums(stream, rec_sizes, ctx=None) -> Tuple[np.ndarray, int, int]:
+    """Device CRC-32/IEEE of every record's Key || Value in a Data-table stream
+    (nkv_record_crc; record.go:51 and :163-169).  Returns (checksums, number of
+    records whose stored Crc differs, lowest such index or -1)."""
+    import ctypes
+    from nakevaleng_amd import _lib
+    ctx = ctx or _lib.default_context()
+    buf = np.frombuffer(bytes(stream), np.uint8) if not isinstance(stream, np.ndarray) else stream
+    buf = np.ascontiguousarray(buf, dtype=np.uint8)
+    sizes = np.ascontiguousarray(rec_sizes, dtype=np.uint64)
+    n = sizes.size
+    crc = np.zeros(max(n, 1), np.uint32)
+    bad, first = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    _lib.check(_lib.lib().nkv_record_crc(ctx.h, _lib.p8(buf if buf.size else np.zeros(1, np.uint8)), buf.size,
+                                         _lib.p64(sizes if n else np.zeros(1, np.uint64)), n,
+                                         crc.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+                                         ctypes.byref(bad), ctypes.byref(first)))
+    return crc[:n], int(bad.value), (-1 if first.value == 2**64 - 1 else int(first.value))
+
+
+def verify(stream, rec_sizes, ctx=None) -> np.ndarray:
+    """record.Deserialize's checksum check over a whole Data-table stream on the
+    device: raises ValueError with the reference's message (record.go:166-167)
+    for the first bad record, else returns the checksums."""
+    crc, bad, first = checksums(stream, rec_sizes, ctx)
+    if bad:
+        off = int(np.sum(np.asarray(rec_sizes, dtype=np.uint64)[:first]))
+        stored = _HDR.unpack_from(bytes(stream), off)[0]
+        raise ValueError(f"Bad Record checksum (got {int(crc[first])}, expected {stored})")
+    return crc

@@ -21,8 +21,8 @@ u64p = ctypes.POINTER(ctypes.c_uint64)
 
 
 def build() -> str:
-    src = os.path.join(_HERE, "merkle_oracle.c")
-    if not os.path.exists(_SO) or os.path.getmtime(_SO) < os.path.getmtime(src):
+    srcs = [os.path.join(_HERE, f) for f in ("merkle_oracle.c", "record_crc_oracle.c")]
+    if not os.path.exists(_SO) or os.path.getmtime(_SO) < max(os.path.getmtime(s) for s in srcs):
         subprocess.check_call(["make", "-s", "-C", _HERE, "liboracle.so"])
     return _SO
 
@@ -48,6 +48,10 @@ def lib():
         L.nkvo_bfs_size.restype = ctypes.c_uint64
         L.nkvo_bfs_image.argtypes = [u8p, ctypes.c_uint64, u8p]
         L.nkvo_bfs_image.restype = ctypes.c_uint64
+        L.nkvo_crc32.argtypes = [u8p, ctypes.c_uint64]
+        L.nkvo_crc32.restype = ctypes.c_uint32
+        L.nkvo_record_crcs.argtypes = [u8p, u64p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint32), u8p]
+        L.nkvo_record_crcs.restype = ctypes.c_uint64
         _lib = L
     return _lib
 
@@ -134,3 +138,22 @@ def bfs_image(nodes: np.ndarray, n: int) -> bytes:
     img = np.zeros(max(bfs_size(n), 1), np.uint8)
     w = lib().nkvo_bfs_image(_p8(nodes), n, _p8(img))
     return img[:w].tobytes()
+
+
+def crc32(data) -> int:
+    """CRC-32 (IEEE) as Go's crc32.ChecksumIEEE (record.go:51)."""
+    a = np.frombuffer(bytes(data), np.uint8) if not isinstance(data, np.ndarray) else data
+    a = np.ascontiguousarray(a, dtype=np.uint8)
+    buf = a if a.size else np.zeros(1, np.uint8)
+    return int(lib().nkvo_crc32(_p8(buf), a.size))
+
+
+def record_crcs(stream: np.ndarray, rec_off: np.ndarray):
+    """(crc per record over key ++ value, ok flags, number of mismatches)."""
+    off = np.ascontiguousarray(rec_off, dtype=np.uint64)
+    n = off.size
+    crc = np.zeros(max(n, 1), np.uint32)
+    ok = np.zeros(max(n, 1), np.uint8)
+    bad = lib().nkvo_record_crcs(_p8(stream), _p64(off if n else np.zeros(1, np.uint64)), n,
+                                 crc.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), _p8(ok))
+    return crc[:n], ok[:n].astype(bool), int(bad)

@@ -112,3 +112,38 @@ def test_literal_restatement_matches_c_oracle_random(oracle):
         nodes = oracle.tree_from_digests(oracle.leaf_hashes(data, off, lens))
         assert nodes[-1].tobytes() == t.Root.Data
         assert oracle.bfs_image(nodes, n) == t.SerializeBytes()
+
+
+# --- record checksum: CRC-32/IEEE over key ++ value ---
+
+def test_crc32_published_check_value(oracle):
+    # ISO-HDLC / Go crc32.ChecksumIEEE check value
+    assert oracle.crc32(b"123456789") == 0xCBF43926
+    assert oracle.crc32(b"") == 0
+
+
+def test_crc32_matches_zlib(oracle):
+    import zlib
+    rng = np.random.default_rng(11)
+    for n in (1, 2, 3, 4, 5, 15, 16, 17, 63, 64, 65, 255, 4066, 10000):
+        d = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        assert oracle.crc32(d) == zlib.crc32(d)
+
+
+def test_record_crcs_on_serialized_stream(oracle):
+    from nakevaleng_amd import record
+    rng = np.random.default_rng(12)
+    recs = [record.New(rng.integers(0, 256, int(k), dtype=np.uint8).tobytes(),
+                       rng.integers(0, 256, int(v), dtype=np.uint8).tobytes(), timestamp=7)
+            for k, v in zip(rng.integers(0, 40, 50), rng.integers(0, 3000, 50))]
+    recs.append(record.New(b"", b"", timestamp=7))
+    stream, sizes = record.data_table(recs)
+    off = np.zeros(len(recs), np.uint64)
+    off[1:] = np.cumsum(sizes[:-1])
+    buf = np.frombuffer(stream, np.uint8).copy()
+    crc, ok, bad = oracle.record_crcs(buf, off)
+    assert bad == 0 and ok.all()
+    assert [int(c) for c in crc] == [r.Crc for r in recs]
+    buf[int(off[3]) + 30] ^= 1  # corrupt record 3's first key byte
+    crc2, ok2, bad2 = oracle.record_crcs(buf, off)
+    assert bad2 == 1 and not ok2[3] and ok2[[i for i in range(len(recs)) if i != 3]].all()
