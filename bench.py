@@ -63,6 +63,8 @@ def parse():
     ap.add_argument("--leaf-load", type=int, default=0, help="NKV_OPT_LEAF_LOAD override (0 = library default)")
     ap.add_argument("--deep", type=int, default=-1,
                     help="NKV_OPT_DEEP_PREFETCH override for ragged batches (-1 = library default)")
+    ap.add_argument("--queue-split", type=int, default=-1, help="NKV_OPT_QUEUE_SPLIT override")
+    ap.add_argument("--queue-waves", type=int, default=0, help="NKV_OPT_QUEUE_WAVES override")
     ap.add_argument("--leaves", type=int, default=1 << 20)
     ap.add_argument("--value-bytes", type=int, default=4096)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -133,6 +135,10 @@ def main():
         ctx.set_option(_lib.NKV_OPT_LEAF_LOAD, args.leaf_load)
     if args.deep >= 0:
         ctx.set_option(_lib.NKV_OPT_DEEP_PREFETCH, args.deep)
+    if args.queue_split >= 0:
+        ctx.set_option(_lib.NKV_OPT_QUEUE_SPLIT, args.queue_split)
+    if args.queue_waves:
+        ctx.set_option(_lib.NKV_OPT_QUEUE_WAVES, args.queue_waves)
     if args.no_bucket:
         ctx.set_option(_lib.NKV_OPT_BUCKET, 0)
     roots = torch.empty(world * 20, dtype=torch.uint8, device="cuda")

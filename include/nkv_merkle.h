@@ -91,8 +91,13 @@ int nkv_ctx_sync(nkv_ctx *ctx);
 #define NKV_OPT_DEEP_PREFETCH 3 /* length-sorted ragged batches: 0 = one block of
                                    lookahead; 1 = several blocks; 2 = several blocks in a
                                    work-queue kernel that spreads the longest chains one
-                                   per SIMD; 3 = the work-queue kernel with values
-                                   staged as aligned 64-B chunks through an LDS ring */
+                                   per SIMD; 3 (default) = the work-queue kernel with
+                                   values staged as aligned 64-B chunks through an LDS
+                                   ring */
+#define NKV_OPT_QUEUE_SPLIT 4 /* work-queue kernel: groups whose longest value has at most
+                                 this many 64-B blocks may go to the non-priority waves
+                                 when the longest value bounds the batch (default 32) */
+#define NKV_OPT_QUEUE_WAVES 5 /* work-queue kernel (LDS ring): waves per SIMD, 1..5 (default 4) */
 int nkv_ctx_set_option(nkv_ctx *ctx, int key, int64_t value);
 /* When enabled, the device-resident tree calls record HIP events around the
  * leaf kernel and the tree reduce on the context's stream. */

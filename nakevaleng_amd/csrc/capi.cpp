@@ -97,8 +97,10 @@ struct nkv_ctx {
     hipStream_t stream = nullptr;
     int leaf_load = 1;  // NKV_OPT_LEAF_LOAD
     int bucket = 1;     // NKV_OPT_BUCKET
-    int deep = 1;       // NKV_OPT_DEEP_PREFETCH (2 = work-queue kernel)
+    int deep = 3;       // NKV_OPT_DEEP_PREFETCH (2, 3 = work-queue kernel)
     uint32_t simds = 1024;  // SIMDs on the device (CUs x 4)
+    int queue_split = 32;   // NKV_OPT_QUEUE_SPLIT
+    int queue_waves = 4;    // NKV_OPT_QUEUE_WAVES
     bool timing = false;
     bool timed = false;
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
@@ -257,8 +259,9 @@ int leaf_level(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint6
             TRY(grow(c->d_queue, 4 * queue_words(n)));
             const bool ring = c->deep == 3;
             return st(launch_leaf_queue(base, off, len, perm, n, aligned, ring,
-                                        static_cast<uint32_t*>(c->d_queue.p), (ring ? 4 : 2) * c->simds, nodes,
-                                        c->stream));
+                                        static_cast<uint32_t*>(c->d_queue.p),
+                                        c->simds, uint32_t(ring ? c->queue_waves : 2), uint32_t(c->queue_split),
+                                        nodes, c->stream));
         }
     }
     return st(launch_leaf_offsets(base, off, len, perm, n, 0, false, aligned, c->leaf_load, nodes,
@@ -375,6 +378,14 @@ int nkv_ctx_set_option(nkv_ctx* c, int key, int64_t value) {
         case NKV_OPT_DEEP_PREFETCH:
             if (value < 0 || value > 3) return NKV_ERR_INVALID;
             c->deep = int(value);
+            return NKV_OK;
+        case NKV_OPT_QUEUE_SPLIT:
+            if (value < 0 || value > 0xFFFFFFFFll) return NKV_ERR_INVALID;
+            c->queue_split = int(std::min<int64_t>(value, 0x7FFFFFFF));
+            return NKV_OK;
+        case NKV_OPT_QUEUE_WAVES:
+            if (value < 1 || value > 5) return NKV_ERR_INVALID;  // 8 KiB LDS per wave: <= 20 per CU
+            c->queue_waves = int(value);
             return NKV_OK;
         default:
             return NKV_ERR_INVALID;

@@ -31,11 +31,14 @@ hipError_t launch_leaf_offsets(const uint8_t* base, const uint64_t* off, const u
                                const uint32_t* perm, uint64_t n, int top, bool fuse, bool aligned,
                                int load, uint8_t* nodes, hipStream_t s, bool deep = true);
 // Ragged batch through the work-queue leaf kernel (perm = length-sorted order,
-// longest first); q must hold queue_words(n) u32; waves = 2 x SIMDs.
+// longest first); q must hold queue_words(n) u32; split = longest chain (full
+// blocks) of a group the non-priority waves take when the longest chain bounds
+// the batch.
 uint64_t queue_words(uint64_t n);
 hipError_t launch_leaf_queue(const uint8_t* base, const uint64_t* off, const uint64_t* len,
                              const uint32_t* perm, uint64_t n, bool aligned, bool ring, uint32_t* q,
-                             uint32_t waves, uint8_t* nodes, hipStream_t s);
+                             uint32_t simds, uint32_t waves_per_simd, uint32_t split, uint8_t* nodes,
+                             hipStream_t s);
 hipError_t launch_reduce(uint8_t* nodes, uint64_t n, int from_level, int top, hipStream_t s);
 hipError_t launch_bfs_image(const uint8_t* nodes, const BfsLayout& lay, uint8_t* img,
                             hipStream_t s);

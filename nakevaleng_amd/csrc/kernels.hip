@@ -621,8 +621,14 @@ __global__ __launch_bounds__(kBlock, LOAD >= 6 ? 2 : (LOAD >= 4 ? 4 : kLeafWaves
 // chain leaves.  The two ends meet; a per-group claim flag settles the last
 // group.  Every wave exits once its end meets the other one.
 //
-// q: [0] front ticket, [1] back ticket, [2, 2 + kSimdKeys) per-SIMD arrivals,
-//    then ngroups claim flags; zeroed before the launch.
+// The other waves only take groups whose longest chain is at most split
+// blocks (group index >= q[2], found by k_queue_split): long groups all go
+// longest-first to the one raised-priority wave per SIMD, so the batch ends on
+// short groups instead of on a medium one pulled late from the short end.
+//
+// q: [0] front ticket, [1] back ticket, [2] first short group, [3] unused,
+//    [4, 4 + kSimdKeys) per-SIMD arrivals, then ngroups claim flags; zeroed
+//    before the launch.
 constexpr uint32_t kSimdKeys = 8 * 8 * 2 * 16 * 4;  // xcc, se, sh, cu, simd
 
 template <int LOAD>
@@ -640,11 +646,12 @@ __global__ __launch_bounds__(64, LOAD == 8 ? 4 : 2) void k_leaf_queue(const uint
     const uint32_t key = ((((xcc & 7) * 8 + ((hw >> 13) & 7)) * 2 + ((hw >> 12) & 1)) * 16 + ((hw >> 8) & 15)) * 4 +
                          ((hw >> 4) & 3);
     uint32_t slot = 0;
-    if (lane == 0) slot = atomicAdd(q + 2 + key, 1u);
+    if (lane == 0) slot = atomicAdd(q + 4 + key, 1u);
     slot = __builtin_amdgcn_readfirstlane(slot);
     const bool front = slot == 0;
     if (front) __builtin_amdgcn_s_setprio(3);
-    uint32_t* claimed = q + 2 + kSimdKeys;
+    const uint32_t first_short = __builtin_amdgcn_readfirstlane(q[2]);
+    uint32_t* claimed = q + 4 + kSimdKeys;
 #ifdef NKV_DIAG
     uint64_t d_t0 = __builtin_amdgcn_s_memrealtime(), d_c0 = __builtin_amdgcn_s_memtime(), d_first = 0;
     uint64_t d_groups = 0, d_blocks = 0;
@@ -655,7 +662,7 @@ __global__ __launch_bounds__(64, LOAD == 8 ? 4 : 2) void k_leaf_queue(const uint
             const uint32_t t = atomicAdd(q + (front ? 0 : 1), 1u);
             if (t < ngroups) {
                 const uint32_t c = front ? t : ngroups - 1 - t;
-                if (atomicExch(claimed + c, 1u) == 0u) g = c;
+                if ((front || c >= first_short) && atomicExch(claimed + c, 1u) == 0u) g = c;
             }
         }
         g = __builtin_amdgcn_readfirstlane(g);
@@ -879,12 +886,47 @@ hipError_t launch_leaf_offsets(const uint8_t* base, const uint64_t* off, const u
     return hipGetLastError();
 }
 
+// q[2] = first group (length-sorted, longest first) the non-priority waves may
+// take.  When the batch's work (sum over groups of their longest chain) is at
+// least twice what the longest chain alone keeps every SIMD busy for, the
+// batch is throughput-bound (e.g. equal lengths) and every wave takes any
+// group (q[2] = 0).  Otherwise the longest chain bounds the kernel and only
+// groups of at most split blocks may go to the non-priority waves.
+__global__ __launch_bounds__(256) void k_queue_split(const uint64_t* __restrict__ len,
+                                                     const uint32_t* __restrict__ perm, uint32_t ngroups,
+                                                     uint32_t split, uint32_t simds, uint32_t* __restrict__ q) {
+    __shared__ unsigned long long part[4];
+    unsigned long long w = 0;
+    for (uint32_t g = threadIdx.x; g < ngroups; g += 256) w += len[perm[uint64_t(g) * 64]] >> 6;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) w += __shfl_xor(w, o);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = w;
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    const unsigned long long work = part[0] + part[1] + part[2] + part[3];
+    const unsigned long long longest = len[perm[0]] >> 6;
+    if (work >= 2ull * simds * longest) {
+        q[2] = 0;
+        return;
+    }
+    uint32_t lo = 0, hi = ngroups;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if ((len[perm[uint64_t(mid) * 64]] >> 6) <= split) hi = mid;
+        else lo = mid + 1;
+    }
+    q[2] = lo;
+}
+
 hipError_t launch_leaf_queue(const uint8_t* base, const uint64_t* off, const uint64_t* len,
                              const uint32_t* perm, uint64_t n, bool aligned, bool ring, uint32_t* q,
-                             uint32_t waves, uint8_t* nodes, hipStream_t s) {
+                             uint32_t simds, uint32_t waves_per_simd, uint32_t split, uint8_t* nodes,
+                             hipStream_t s) {
     const uint32_t ngroups = uint32_t((n + 63) / 64);
+    const uint32_t waves = simds * waves_per_simd;
     hipError_t e = hipMemsetAsync(q, 0, queue_words(n) * sizeof(uint32_t), s);
     if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_queue_split, dim3(1), dim3(256), 0, s, len, perm, ngroups, split, simds, q);
     if (ring)
         hipLaunchKernelGGL(k_leaf_queue<8>, dim3(waves), dim3(64), 0, s, base, off, len, perm, n, ngroups, q, nodes);
     else if (aligned)
@@ -894,7 +936,7 @@ hipError_t launch_leaf_queue(const uint8_t* base, const uint64_t* off, const uin
     return hipGetLastError();
 }
 
-uint64_t queue_words(uint64_t n) { return 2 + kSimdKeys + (n + 63) / 64; }
+uint64_t queue_words(uint64_t n) { return 4 + kSimdKeys + (n + 63) / 64; }
 
 hipError_t launch_reduce(uint8_t* nodes, uint64_t n, int from_level, int top, hipStream_t s) {
     int j0 = from_level;

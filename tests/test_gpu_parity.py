@@ -159,7 +159,41 @@ def test_ragged_deep_and_queue_paths(nkv, oracle, deep, n, packed):
             want = oracle.tree_from_digests(oracle.leaf_hashes(data, off, lens, threads=8))
             assert np.array_equal(d_nodes.cpu().numpy().reshape(-1, 20), want)
     finally:
-        ctx.set_option(_lib.NKV_OPT_DEEP_PREFETCH, 1)
+        ctx.set_option(_lib.NKV_OPT_DEEP_PREFETCH, 3)
+
+
+@pytest.mark.parametrize("split", [0, 1, 32, 100000])
+@pytest.mark.parametrize("shape", ["uniform", "skewed"])
+def test_queue_split_policies(nkv, oracle, split, shape):
+    """Work-queue kernel under every split regime: equal lengths (throughput-
+    bound: every wave takes any group) and one very long value among short ones
+    (the longest chain bounds the batch: short groups only to the non-priority
+    waves), with splits that leave the non-priority waves nothing / everything."""
+    torch = _torch()
+    _lib, ctx = nkv
+    _bind(torch, ctx)
+    L = _lib.lib()
+    rng = np.random.default_rng(split + (7 if shape == "uniform" else 8))
+    n = 9000
+    if shape == "uniform":
+        lens = np.full(n, 4050, np.uint64)
+    else:
+        lens = rng.integers(0, 2000, n).astype(np.uint64)
+        lens[rng.integers(0, n, 5)] = 70000
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum(lens[:-1] + 46)
+    data = oracle.splitmix64_bytes(int(off[-1] + lens[-1]), SEED + split)
+    d_data, d_off, d_len = _dev(torch, data), _dev(torch, off), _dev(torch, lens)
+    d_nodes = torch.zeros(L.nkv_total_nodes(n) * 20, dtype=torch.uint8, device="cuda")
+    ctx.set_option(_lib.NKV_OPT_QUEUE_SPLIT, split)
+    try:
+        _lib.check(L.nkv_tree_from_values_dev(ctx.h, d_data.data_ptr(), d_off.data_ptr(), d_len.data_ptr(),
+                                              n, d_nodes.data_ptr()))
+        torch.cuda.synchronize()
+    finally:
+        ctx.set_option(_lib.NKV_OPT_QUEUE_SPLIT, 32)
+    want = oracle.tree_from_digests(oracle.leaf_hashes(data, off, lens, threads=8))
+    assert np.array_equal(d_nodes.cpu().numpy().reshape(-1, 20), want)
 
 
 @pytest.mark.parametrize("n", EDGE_N)
