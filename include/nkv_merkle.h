@@ -98,6 +98,10 @@ int nkv_ctx_sync(nkv_ctx *ctx);
                                  this many 64-B blocks may go to the non-priority waves
                                  when the longest value bounds the batch (default 32) */
 #define NKV_OPT_QUEUE_WAVES 5 /* work-queue kernel (LDS ring): waves per SIMD, 1..5 (default 4) */
+#define NKV_OPT_CRC_LOAD 6    /* record checksums: bit 0 = spans staged as aligned 64-B
+                                 chunks through an LDS ring (else per-lane loads); bits
+                                 1-2 = LDS table copies x workgroup: 0 = 8 x 256,
+                                 1 = 16 x 512, 2 = 32 x 1024 (no ring) */
 int nkv_ctx_set_option(nkv_ctx *ctx, int key, int64_t value);
 /* When enabled, the device-resident tree calls record HIP events around the
  * leaf kernel and the tree reduce on the context's stream. */

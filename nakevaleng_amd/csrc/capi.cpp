@@ -101,6 +101,7 @@ struct nkv_ctx {
     uint32_t simds = 1024;  // SIMDs on the device (CUs x 4)
     int queue_split = 32;   // NKV_OPT_QUEUE_SPLIT
     int queue_waves = 4;    // NKV_OPT_QUEUE_WAVES
+    int crc_load = 1;       // NKV_OPT_CRC_LOAD
     bool timing = false;
     bool timed = false;
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
@@ -382,6 +383,10 @@ int nkv_ctx_set_option(nkv_ctx* c, int key, int64_t value) {
         case NKV_OPT_QUEUE_SPLIT:
             if (value < 0 || value > 0xFFFFFFFFll) return NKV_ERR_INVALID;
             c->queue_split = int(std::min<int64_t>(value, 0x7FFFFFFF));
+            return NKV_OK;
+        case NKV_OPT_CRC_LOAD:
+            if (value < 0 || value > 5) return NKV_ERR_INVALID;
+            c->crc_load = int(value);
             return NKV_OK;
         case NKV_OPT_QUEUE_WAVES:
             if (value < 1 || value > 5) return NKV_ERR_INVALID;  // 8 KiB LDS per wave: <= 20 per CU
@@ -763,7 +768,7 @@ int nkv_crc32_dev(nkv_ctx* c, const void* d_base, const uint64_t* d_off, const u
     TRY(bind(c));
     if (n == 0) return NKV_OK;
     if (!d_base || !d_off || !d_len || !d_crc) return NKV_ERR_INVALID;
-    return st(launch_crc_spans(static_cast<const uint8_t*>(d_base), d_off, d_len, n, d_crc, c->stream));
+    return st(launch_crc_spans(static_cast<const uint8_t*>(d_base), d_off, d_len, n, d_crc, c->crc_load, c->stream));
 }
 
 int nkv_record_crc_dev(nkv_ctx* c, const void* d_stream, uint64_t stream_len, const uint64_t* d_rec_off,
@@ -784,7 +789,7 @@ int nkv_record_crc_dev(nkv_ctx* c, const void* d_stream, uint64_t stream_len, co
         stats = static_cast<unsigned long long*>(c->d_stats.p);
     }
     return st(launch_record_crc(static_cast<const uint8_t*>(d_stream), stream_len, d_rec_off, n, d_crc, stats,
-                                c->stream));
+                                c->crc_load, c->stream));
 }
 
 int nkv_fill_splitmix64_dev(nkv_ctx* c, void* d_buf, uint64_t nbytes, uint64_t seed) {

@@ -45,22 +45,22 @@ constexpr CrcTables make_crc_tables() {
 
 __constant__ CrcTables c_crc = make_crc_tables();
 
-constexpr int kCrcCopies = 8;
-constexpr int kCrcBlock = 256;
-
-// tab: this lane's copy (LDS base + lane % kCrcCopies)
+// tab: this lane's copy (LDS base + lane % C), C copies interleaved
+template <int C>
 __device__ __forceinline__ uint32_t crc_lut(const uint32_t* tab, int k, uint32_t e) {
-    return tab[(uint32_t(k) * 256u + e) * kCrcCopies];
+    return tab[(uint32_t(k) * 256u + e) * C];
 }
 
+template <int C>
 __device__ __forceinline__ uint32_t crc_word(uint32_t crc, uint32_t w, const uint32_t* tab) {
     const uint32_t x = crc ^ w;
-    return crc_lut(tab, 3, x & 0xFFu) ^ crc_lut(tab, 2, (x >> 8) & 0xFFu) ^ crc_lut(tab, 1, (x >> 16) & 0xFFu) ^
-           crc_lut(tab, 0, x >> 24);
+    return crc_lut<C>(tab, 3, x & 0xFFu) ^ crc_lut<C>(tab, 2, (x >> 8) & 0xFFu) ^
+           crc_lut<C>(tab, 1, (x >> 16) & 0xFFu) ^ crc_lut<C>(tab, 0, x >> 24);
 }
 
+template <int C>
 __device__ __forceinline__ uint32_t crc_byte(uint32_t crc, uint32_t b, const uint32_t* tab) {
-    return crc_lut(tab, 0, (crc ^ b) & 0xFFu) ^ (crc >> 8);
+    return crc_lut<C>(tab, 0, (crc ^ b) & 0xFFu) ^ (crc >> 8);
 }
 
 __device__ __forceinline__ uint64_t crc_ld_le64(const uint8_t* p) {
@@ -78,6 +78,7 @@ __device__ __forceinline__ uint32_t crc_wave_max(uint32_t v) {
 
 // CRC-32/IEEE of [s, s + len) (finalised).  Every lane of the wave calls it
 // (dead lanes with len 0).
+template <int C>
 __device__ __forceinline__ uint32_t crc_span(const uint8_t* s, uint64_t len, const uint32_t* tab) {
     uint32_t crc = 0xFFFFFFFFu;
     const uint64_t sa = uint64_t(reinterpret_cast<uintptr_t>(s));
@@ -85,7 +86,7 @@ __device__ __forceinline__ uint32_t crc_span(const uint8_t* s, uint64_t len, con
     const uint64_t s4 = (sa + 3) & ~uint64_t(3);
     const uint64_t e4 = ea & ~uint64_t(3);
     const uint64_t hb = s4 < ea ? s4 : ea;
-    for (uint64_t a = sa; a < hb; ++a) crc = crc_byte(crc, s[a - sa], tab);
+    for (uint64_t a = sa; a < hb; ++a) crc = crc_byte<C>(crc, s[a - sa], tab);
     const uint64_t A = s4 & ~uint64_t(63);
     const uint32_t nch = e4 > s4 ? uint32_t((e4 - A + 63) >> 6) : 0u;
     const uint32_t nmax = crc_wave_max(nch);
@@ -101,20 +102,89 @@ __device__ __forceinline__ uint32_t crc_span(const uint8_t* s, uint64_t len, con
             const uint64_t b0 = A + 64ull * c;
             if (b0 >= s4 && b0 + 64 <= e4) {
 #pragma unroll
-                for (int j = 0; j < 16; ++j) crc = crc_word(crc, w[j], tab);
+                for (int j = 0; j < 16; ++j) crc = crc_word<C>(crc, w[j], tab);
             } else {
                 const uint64_t lo = s4 > b0 ? (s4 - b0) >> 2 : 0;
                 const uint64_t hi = e4 - b0 >= 64 ? 16 : (e4 - b0) >> 2;
 #pragma unroll
                 for (int j = 0; j < 16; ++j) {
-                    const uint32_t u = crc_word(crc, w[j], tab);
+                    const uint32_t u = crc_word<C>(crc, w[j], tab);
                     crc = (uint64_t(j) >= lo && uint64_t(j) < hi) ? u : crc;
                 }
             }
         }
     }
     const uint64_t tb = e4 > hb ? e4 : hb;
-    for (uint64_t a = tb; a < ea; ++a) crc = crc_byte(crc, s[a - sa], tab);
+    for (uint64_t a = tb; a < ea; ++a) crc = crc_byte<C>(crc, s[a - sa], tab);
+    return ~crc;
+}
+
+// Same checksum, span bytes staged through a wave-private LDS ring of aligned
+// 64-B chunks (two 4 KiB slots, chunk c in slot c & 1) by wave-cooperative
+// DMA: instruction k moves one chunk of spans 16k .. 16k+15, 64 contiguous
+// bytes each (16 segments per wave-instruction instead of 64 scattered 16-B
+// pieces when every lane reads its own span).  Each lane then reads its own
+// chunk's four quads.  Chunk c+2 goes into chunk c's slot once c is read.
+// Only chunks holding span bytes are fetched (an aligned chunk with one valid
+// byte lies in that byte's page).
+template <int C>
+__device__ __forceinline__ uint32_t crc_span_ring(const uint8_t* s, uint64_t len, const uint32_t* tab,
+                                                  uint8_t* wbuf) {
+    const int lane = threadIdx.x & 63;
+    uint32_t crc = 0xFFFFFFFFu;
+    const uint32_t o = uint32_t(reinterpret_cast<uintptr_t>(s)) & 63u;
+    const uint32_t nch = len ? uint32_t((o + len + 63) >> 6) : 0u;
+    const uint32_t dq = (uint32_t(lane) & 3u) ^ ((uint32_t(lane) >> 4) & 3u);
+    const uint8_t* src[4];
+    uint32_t nc[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int j = 16 * k + (lane >> 2);
+        const uint64_t aj = uint64_t(__shfl(int64_t(reinterpret_cast<uintptr_t>(s - o)), j));
+        src[k] = reinterpret_cast<const uint8_t*>(aj) + 16 * dq;
+        nc[k] = uint32_t(__shfl(int(nch), j));
+    }
+    const uint32_t nmax = crc_wave_max(nch);
+    if (nmax == 0) return 0u;
+    auto issue = [&](uint32_t c) {
+        uint8_t* dst = wbuf + 4096 * (c & 1u);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (c < nc[k]) __builtin_amdgcn_global_load_lds(src[k] + 64ull * c, dst + 1024 * k, 16, 0, 0);
+    };
+    const uint32_t swz = (uint32_t(lane) >> 2) & 3u;
+    const uint64_t e = uint64_t(o) + len;  // span end, relative to the first chunk
+    issue(0u);
+    issue(1u);
+    for (uint32_t c = 0; c < nmax; ++c) {
+        const uint8_t* rd = wbuf + 4096 * (c & 1u) + 64 * lane;
+        uint4 v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = *reinterpret_cast<const uint4*>(rd + 16 * (uint32_t(i) ^ swz));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot reads done before refill
+        if (c + 2 < nmax) issue(c + 2);
+        if (c < nch) {
+            const uint32_t w[16] = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w,
+                                    v[2].x, v[2].y, v[2].z, v[2].w, v[3].x, v[3].y, v[3].z, v[3].w};
+            const uint64_t b0 = 64ull * c;  // chunk start, relative
+            if (b0 >= o && b0 + 64 <= e) {
+#pragma unroll
+                for (int j = 0; j < 16; ++j) crc = crc_word<C>(crc, w[j], tab);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    const uint64_t a = b0 + 4 * j;
+                    const uint32_t lo = a >= o ? 0u : (o - a >= 4 ? 4u : uint32_t(o - a));
+                    const uint32_t hi = a >= e ? 0u : (e - a >= 4 ? 4u : uint32_t(e - a));
+                    if (lo == 0u && hi == 4u) {
+                        crc = crc_word<C>(crc, w[j], tab);
+                    } else {
+                        for (uint32_t b = lo; b < hi; ++b) crc = crc_byte<C>(crc, (w[j] >> (8 * b)) & 0xFFu, tab);
+                    }
+                }
+            }
+        }
+    }
     return ~crc;
 }
 
@@ -122,17 +192,16 @@ __device__ __forceinline__ uint32_t crc_span(const uint8_t* s, uint64_t len, con
 // checked against stream_len; stats[0] += records whose stored Crc differs,
 // stats[1] = min such index, stats[2] |= 1 on a header outside the stream.
 // Otherwise span i = [base + off[i], + len[i]).
-template <bool RECORDS>
-__global__ __launch_bounds__(kCrcBlock) void k_crc(const uint8_t* __restrict__ base,
-                                                   const uint64_t* __restrict__ off,
-                                                   const uint64_t* __restrict__ len, uint64_t stream_len,
-                                                   uint64_t n, uint32_t* __restrict__ out,
-                                                   unsigned long long* __restrict__ stats) {
-    __shared__ uint32_t tab[4 * 256 * kCrcCopies];
-    for (int i = threadIdx.x; i < 4 * 256 * kCrcCopies; i += kCrcBlock) tab[i] = (&c_crc.t[0][0])[i / kCrcCopies];
+template <bool RECORDS, bool RING, int C, int B>
+__global__ __launch_bounds__(B) void k_crc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
+                                           const uint64_t* __restrict__ len, uint64_t stream_len, uint64_t n,
+                                           uint32_t* __restrict__ out, unsigned long long* __restrict__ stats) {
+    __shared__ uint32_t tab[4 * 256 * C];
+    __shared__ __attribute__((aligned(16))) uint8_t ring[RING ? B / 64 : 1][RING ? 8192 : 16];
+    for (int i = threadIdx.x; i < 4 * 256 * C; i += B) tab[i] = (&c_crc.t[0][0])[i / C];
     __syncthreads();
-    const uint32_t* mytab = tab + (threadIdx.x % kCrcCopies);
-    const uint64_t i = uint64_t(blockIdx.x) * kCrcBlock + threadIdx.x;
+    const uint32_t* mytab = tab + (threadIdx.x % C);
+    const uint64_t i = uint64_t(blockIdx.x) * B + threadIdx.x;
     const uint8_t* s = base;
     uint64_t L = 0;
     uint32_t stored = 0;
@@ -159,7 +228,7 @@ __global__ __launch_bounds__(kCrcBlock) void k_crc(const uint8_t* __restrict__ b
             L = len[i];
         }
     }
-    const uint32_t crc = crc_span(s, L, mytab);
+    const uint32_t crc = RING ? crc_span_ring<C>(s, L, mytab, ring[threadIdx.x >> 6]) : crc_span<C>(s, L, mytab);
     if (!live) return;
     if (out) out[i] = crc;
     if (RECORDS && stats) {
@@ -171,22 +240,41 @@ __global__ __launch_bounds__(kCrcBlock) void k_crc(const uint8_t* __restrict__ b
     }
 }
 
+// variant: bit 0 = LDS chunk ring; bits 1-2 = table copies x workgroup size:
+// 0 = 8 x 256, 1 = 16 x 512, 2 = 32 x 1024.
+template <bool RECORDS>
+static void launch_crc(int variant, const uint8_t* base, const uint64_t* off, const uint64_t* len,
+                       uint64_t stream_len, uint64_t n, uint32_t* out, unsigned long long* stats, hipStream_t s) {
+    const bool ring = variant & 1;
+    const int cfg = (variant >> 1) & 3;
+    const int B = cfg == 0 ? 256 : (cfg == 1 ? 512 : 1024);
+    const dim3 grid(uint32_t((n + B - 1) / B)), block(B);
+#define NKV_CRC_LAUNCH(R, C, BB) \
+    hipLaunchKernelGGL((k_crc<RECORDS, R, C, BB>), grid, block, 0, s, base, off, len, stream_len, n, out, stats)
+    if (cfg == 0) {
+        if (ring) NKV_CRC_LAUNCH(true, 8, 256);
+        else NKV_CRC_LAUNCH(false, 8, 256);
+    } else if (cfg == 1) {
+        if (ring) NKV_CRC_LAUNCH(true, 16, 512);
+        else NKV_CRC_LAUNCH(false, 16, 512);
+    } else {
+        NKV_CRC_LAUNCH(false, 32, 1024);  // 128 KiB of tables: no room for a ring
+    }
+#undef NKV_CRC_LAUNCH
+}
+
 hipError_t launch_crc_spans(const uint8_t* base, const uint64_t* off, const uint64_t* len, uint64_t n,
-                            uint32_t* out, hipStream_t s) {
-    const uint64_t grid = (n + kCrcBlock - 1) / kCrcBlock;
-    hipLaunchKernelGGL(k_crc<false>, dim3(uint32_t(grid)), dim3(kCrcBlock), 0, s, base, off, len, uint64_t(0), n,
-                       out, nullptr);
+                            uint32_t* out, int variant, hipStream_t s) {
+    launch_crc<false>(variant, base, off, len, 0, n, out, nullptr, s);
     return hipGetLastError();
 }
 
 hipError_t launch_record_crc(const uint8_t* stream, uint64_t stream_len, const uint64_t* rec_off, uint64_t n,
-                             uint32_t* out, unsigned long long* stats, hipStream_t s) {
+                             uint32_t* out, unsigned long long* stats, int variant, hipStream_t s) {
     hipError_t e = hipMemsetAsync(stats, 0, 3 * sizeof(unsigned long long), s);
     if (e == hipSuccess) e = hipMemsetAsync(stats + 1, 0xFF, sizeof(unsigned long long), s);
     if (e != hipSuccess) return e;
-    const uint64_t grid = (n + kCrcBlock - 1) / kCrcBlock;
-    hipLaunchKernelGGL(k_crc<true>, dim3(uint32_t(grid)), dim3(kCrcBlock), 0, s, stream, rec_off,
-                       static_cast<const uint64_t*>(nullptr), stream_len, n, out, stats);
+    launch_crc<true>(variant, stream, rec_off, nullptr, stream_len, n, out, stats, s);
     return hipGetLastError();
 }
 

@@ -52,10 +52,12 @@ hipError_t sort_by_length_desc(const uint64_t* len, uint64_t n, uint32_t* keys, 
                                void* tmp, size_t* tmp_bytes, hipStream_t s);
 // crc.hip: CRC-32/IEEE of byte spans / of records' Key ++ Value (stats: 3 x u64,
 // initialised by the launcher).
+// variant: NKV_OPT_CRC_LOAD (bit 0 LDS chunk ring; bits 1-2 table copies x
+// workgroup size).
 hipError_t launch_crc_spans(const uint8_t* base, const uint64_t* off, const uint64_t* len, uint64_t n,
-                            uint32_t* out, hipStream_t s);
+                            uint32_t* out, int variant, hipStream_t s);
 hipError_t launch_record_crc(const uint8_t* stream, uint64_t stream_len, const uint64_t* rec_off, uint64_t n,
-                             uint32_t* out, unsigned long long* stats, hipStream_t s);
+                             uint32_t* out, unsigned long long* stats, int variant, hipStream_t s);
 hipError_t launch_fill(uint8_t* buf, uint64_t nbytes, uint64_t seed, hipStream_t s);
 
 }  // namespace nkv

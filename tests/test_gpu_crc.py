@@ -30,9 +30,11 @@ def _stream(rng, n, kmax=40, vmax=3000):
     return recs, np.frombuffer(stream, np.uint8).copy(), sizes, off
 
 
-def test_crc32_spans_every_alignment_and_length(nkv, oracle):
+@pytest.mark.parametrize("load", [0, 1, 2, 3, 4])
+def test_crc32_spans_every_alignment_and_length(nkv, oracle, load):
     torch = _torch()
     _lib, ctx = nkv
+    ctx.set_option(_lib.NKV_OPT_CRC_LOAD, load)
     ctx.set_stream(torch.cuda.current_stream().cuda_stream)
     L = _lib.lib()
     rng = np.random.default_rng(21)
@@ -47,6 +49,7 @@ def test_crc32_spans_every_alignment_and_length(nkv, oracle):
     torch.cuda.synchronize()
     got = d_out.cpu().numpy().view(np.uint32)
     want = [oracle.crc32(data[int(o):int(o + l)]) for o, l in zip(off, lens)]
+    ctx.set_option(_lib.NKV_OPT_CRC_LOAD, 1)
     assert got.tolist() == want
 
 
@@ -63,10 +66,12 @@ def test_crc32_check_value(nkv):
     assert int(out.cpu().numpy().view(np.uint32)[0]) == 0xCBF43926
 
 
+@pytest.mark.parametrize("load", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 257, 3000])
-def test_record_crc_device_matches_oracle_and_stored(nkv, oracle, n):
+def test_record_crc_device_matches_oracle_and_stored(nkv, oracle, n, load):
     torch = _torch()
     _lib, ctx = nkv
+    ctx.set_option(_lib.NKV_OPT_CRC_LOAD, load)
     ctx.set_stream(torch.cuda.current_stream().cuda_stream)
     L = _lib.lib()
     rng = np.random.default_rng(n)
@@ -88,6 +93,7 @@ def test_record_crc_device_matches_oracle_and_stored(nkv, oracle, n):
     assert int(stats[0]) == want_bad == len(bad_idx)
     assert int(stats[1]) == (bad_idx[0] if bad_idx else 2**64 - 1)
     assert int(stats[2]) == 0
+    ctx.set_option(_lib.NKV_OPT_CRC_LOAD, 1)
 
 
 def test_record_crc_host_api_and_mirror(nkv, oracle):

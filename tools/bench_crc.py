@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--verify", action="store_true")
+    ap.add_argument("--crc-load", type=int, default=-1, help="NKV_OPT_CRC_LOAD override")
     args = ap.parse_args()
     n, rb, ks = args.records, args.rec_bytes, args.key_bytes
     vs = rb - 30 - ks
@@ -40,6 +41,8 @@ def main():
     ctx = _lib.Context(0)
     s = torch.cuda.current_stream()
     ctx.set_stream(s.cuda_stream)
+    if args.crc_load >= 0:
+        ctx.set_option(_lib.NKV_OPT_CRC_LOAD, args.crc_load)
     data = torch.empty(n * rb, dtype=torch.uint8, device="cuda")
     _lib.check(L.nkv_fill_splitmix64_dev(ctx.h, data.data_ptr(), n * rb, 0x6E616B65))
     v = data.view(n, rb)
@@ -69,6 +72,7 @@ def main():
     span_bytes = n * (ks + vs)
     gbs = span_bytes / (ms * 1e-3) / 1e9
     out = {"metric": "record CRC-32 (Key || Value) verify, GB/s of checksummed bytes", "value": round(gbs, 1),
+           "load": args.crc_load,
            "unit": "GB/s", "ms_per_launch": round(ms, 4), "records": n, "record_bytes": rb,
            "bad_records": st[0], "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
                                               "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4)}}
