@@ -735,8 +735,10 @@ __global__ __launch_bounds__(kBlock) void k_bucket_keys(const uint64_t* __restri
                                                          uint32_t* __restrict__ idx) {
     const uint64_t t = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
     if (t >= n) return;
-    const uint64_t blocks = (len[t] + 8) / 64 + 1;  // SHA-1 compressions of the value
-    keys[t] = blocks > 0xFFFFFFFFull ? 0xFFFFFFFFu : uint32_t(blocks);
+    // SHA-1 compressions of the value, clamped to 16 bits (values past 4 MiB
+    // sort as equals): a 16-bit radix sort is half the passes of a 32-bit one
+    const uint64_t blocks = (len[t] + 8) / 64 + 1;
+    keys[t] = blocks > 0xFFFFull ? 0xFFFFu : uint32_t(blocks);
     idx[t] = uint32_t(t);
 }
 
@@ -896,26 +898,28 @@ __global__ __launch_bounds__(256) void k_queue_split(const uint64_t* __restrict_
                                                      const uint32_t* __restrict__ perm, uint32_t ngroups,
                                                      uint32_t split, uint32_t simds, uint32_t* __restrict__ q) {
     __shared__ unsigned long long part[4];
+    __shared__ uint32_t first[4];
     unsigned long long w = 0;
-    for (uint32_t g = threadIdx.x; g < ngroups; g += 256) w += len[perm[uint64_t(g) * 64]] >> 6;
+    uint32_t b = ngroups;  // first group with a longest chain <= split (groups are longest first)
+    for (uint32_t g = threadIdx.x; g < ngroups; g += 256) {
+        const uint64_t blocks = len[perm[uint64_t(g) * 64]] >> 6;
+        w += blocks;
+        if (blocks <= split && g < b) b = g;
+    }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) w += __shfl_xor(w, o);
-    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = w;
+    for (int o = 32; o > 0; o >>= 1) {
+        w += __shfl_xor(w, o);
+        b = min(b, uint32_t(__shfl_xor(int(b), o)));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        part[threadIdx.x >> 6] = w;
+        first[threadIdx.x >> 6] = b;
+    }
     __syncthreads();
     if (threadIdx.x != 0) return;
     const unsigned long long work = part[0] + part[1] + part[2] + part[3];
     const unsigned long long longest = len[perm[0]] >> 6;
-    if (work >= 2ull * simds * longest) {
-        q[2] = 0;
-        return;
-    }
-    uint32_t lo = 0, hi = ngroups;
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if ((len[perm[uint64_t(mid) * 64]] >> 6) <= split) hi = mid;
-        else lo = mid + 1;
-    }
-    q[2] = lo;
+    q[2] = work >= 2ull * simds * longest ? 0u : min(min(first[0], first[1]), min(first[2], first[3]));
 }
 
 hipError_t launch_leaf_queue(const uint8_t* base, const uint64_t* off, const uint64_t* len,
@@ -983,12 +987,12 @@ hipError_t sort_by_length_desc(const uint64_t* len, uint64_t n, uint32_t* keys, 
     // keys: 2n u32 (in | out), perm: 2n u32 (iota in | permutation out)
     if (tmp == nullptr)
         return hipcub::DeviceRadixSort::SortPairsDescending(nullptr, *tmp_bytes, keys, keys + n, perm,
-                                                            perm + n, int(n), 0, 32, s);
+                                                            perm + n, int(n), 0, 16, s);
     hipLaunchKernelGGL(k_bucket_keys, dim3(grid_for(n)), dim3(kBlock), 0, s, len, n, keys, perm);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     return hipcub::DeviceRadixSort::SortPairsDescending(tmp, *tmp_bytes, keys, keys + n, perm, perm + n,
-                                                        int(n), 0, 32, s);
+                                                        int(n), 0, 16, s);
 }
 
 hipError_t launch_fill(uint8_t* buf, uint64_t nbytes, uint64_t seed, hipStream_t s) {
