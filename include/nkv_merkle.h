@@ -22,6 +22,11 @@
  *   (*MerkleTree).Validate  ds/merkletree/merkletree.go:162-171 nkv_tree_build / nkv_tree_generic
  *                           ds/merkletree/merklenode.go:99-108    + 20-byte root compare
  *   record value location   core/record/record.go:191-199       nkv_locate_values_dev
+ *   bloomfilter.New sizing  ds/bloomfilter/bloomfilter.go:18-24 nkv_bloom_params
+ *   makeFilter / Insert     core/sstable/sstable.go:49-56,      nkv_bloom_build /
+ *                           ds/bloomfilter/bloomfilter.go:76-91 nkv_bloom_from_records /
+ *                                                               nkv_bloom_insert[_records]_dev
+ *   (*BloomFilter).Query    ds/bloomfilter/bloomfilter.go:93-111 nkv_bloom_query_dev
  *   record checksum         core/record/record.go:51 (New),     nkv_record_crc /
  *     crc32.ChecksumIEEE    :163-169 (Deserialize check)        nkv_record_crc_dev /
  *     over Key ++ Value                                         nkv_crc32_dev
@@ -168,6 +173,22 @@ int nkv_record_crc(nkv_ctx *ctx, const uint8_t *stream, uint64_t stream_len,
                    const uint64_t *rec_size, uint64_t n, uint32_t *crc_out, uint64_t *n_bad,
                    uint64_t *first_bad);
 
+/* SSTable filter.  bloomfilter.New(n, p)'s sizing: m bits,
+ * k hash functions (bloomfilter.go:18-24; n > 0, 0 < p < 1).  Hash j of a key is
+ * MurmurHash3_x86_32(key, seed0 + j) % m (spaolacci/murmur3 Sum32; the reference
+ * draws seed0 = uint32(time.Now().UnixNano()), bloomfilter.go:31 -- here it is
+ * an argument).  Bit idx is Contents[idx / 8] & (1 << (idx % 8)). */
+int nkv_bloom_params(uint64_t n, double p, uint32_t *m, uint32_t *k);
+/* makeFilter over n keys (key i = keys + off[i], len[i]): bits_out receives
+ * Contents, ceil(m / 8) bytes (bloomfilter.go:67). */
+int nkv_bloom_build(nkv_ctx *ctx, const uint8_t *keys, const uint64_t *off, const uint64_t *len,
+                    uint64_t n, uint32_t m, uint32_t k, uint32_t seed0, uint8_t *bits_out);
+/* makeFilter over the keys of serialized records (stream and rec_size as for
+ * nkv_tree_from_records; sstable.go:51-53 inserts KeyContext.Key). */
+int nkv_bloom_from_records(nkv_ctx *ctx, const uint8_t *stream, uint64_t stream_len,
+                           const uint64_t *rec_size, uint64_t n, uint32_t m, uint32_t k,
+                           uint32_t seed0, uint8_t *bits_out);
+
 /* Serialize()'s file semantics: open O_WRONLY|O_CREAT (mode 0666) WITHOUT
  * O_TRUNC (merkletree.go:68), write len bytes at offset 0, close. */
 int nkv_write_file(const char *fname, const uint8_t *data, uint64_t len);
@@ -207,6 +228,21 @@ int nkv_crc32_dev(nkv_ctx *ctx, const void *d_base, const uint64_t *d_off, const
  * (UINT64_MAX if none), [2] 1 if a header points outside the stream. */
 int nkv_record_crc_dev(nkv_ctx *ctx, const void *d_stream, uint64_t stream_len,
                        const uint64_t *d_rec_off, uint64_t n, uint32_t *d_crc, uint64_t *d_stats);
+/* Bloom filter bits on the device: d_bits holds ((m + 31) / 32) * 4 bytes
+ * (Contents padded to whole 32-bit words, zero the padding); bits are OR-ed in,
+ * so several calls build one filter. */
+int nkv_bloom_insert_dev(nkv_ctx *ctx, const void *d_keys, const uint64_t *d_off,
+                         const uint64_t *d_len, uint64_t n, uint32_t m, uint32_t k, uint32_t seed0,
+                         void *d_bits);
+/* keys of the records at d_stream + d_rec_off[i]; NKV_ERR_INVALID (after a
+ * sync) if a header points outside the stream */
+int nkv_bloom_insert_records_dev(nkv_ctx *ctx, const void *d_stream, uint64_t stream_len,
+                                 const uint64_t *d_rec_off, uint64_t n, uint32_t m, uint32_t k,
+                                 uint32_t seed0, void *d_bits);
+/* d_out[i] = 1 if key i may be in the filter (every bit set), else 0 */
+int nkv_bloom_query_dev(nkv_ctx *ctx, const void *d_keys, const uint64_t *d_off,
+                        const uint64_t *d_len, uint64_t n, uint32_t m, uint32_t k, uint32_t seed0,
+                        const void *d_bits, uint8_t *d_out);
 /* synthetic input: byte j = byte (j % 8) of splitmix64(seed, j / 8) */
 int nkv_fill_splitmix64_dev(nkv_ctx *ctx, void *d_buf, uint64_t nbytes, uint64_t seed);
 

@@ -61,6 +61,12 @@ SIGNATURES = {
     "nkv_tree_generic": (_int, [_vp, _u8p, _u64p, _u64p, _u64, _u8p, _u8p, _u8p]),
     "nkv_tree_from_records": (_int, [_vp, _u8p, _u64, _u64p, _u64, _u8p, _u8p, _u8p]),
     "nkv_record_crc": (_int, [_vp, _u8p, _u64, _u64p, _u64, ctypes.POINTER(ctypes.c_uint32), _u64p, _u64p]),
+    "nkv_bloom_params": (_int, [_u64, ctypes.c_double, ctypes.POINTER(ctypes.c_uint32),
+                                ctypes.POINTER(ctypes.c_uint32)]),
+    "nkv_bloom_build": (_int, [_vp, _u8p, _u64p, _u64p, _u64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                               _u8p]),
+    "nkv_bloom_from_records": (_int, [_vp, _u8p, _u64, _u64p, _u64, ctypes.c_uint32, ctypes.c_uint32,
+                                      ctypes.c_uint32, _u8p]),
     "nkv_write_file": (_int, [ctypes.c_char_p, _u8p, _u64]),
     "nkv_leaf_hash_dev": (_int, [_vp, _vp, _vp, _vp, _u64, _vp]),
     "nkv_leaf_hash_strided_dev": (_int, [_vp, _vp, _u64, _u64, _u64, _vp]),
@@ -72,6 +78,12 @@ SIGNATURES = {
     "nkv_locate_values_dev": (_int, [_vp, _vp, _u64, _vp, _u64, _vp, _vp]),
     "nkv_crc32_dev": (_int, [_vp, _vp, _vp, _vp, _u64, _vp]),
     "nkv_record_crc_dev": (_int, [_vp, _vp, _u64, _vp, _u64, _vp, _vp]),
+    "nkv_bloom_insert_dev": (_int, [_vp, _vp, _vp, _vp, _u64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                    _vp]),
+    "nkv_bloom_insert_records_dev": (_int, [_vp, _vp, _u64, _vp, _u64, ctypes.c_uint32, ctypes.c_uint32,
+                                            ctypes.c_uint32, _vp]),
+    "nkv_bloom_query_dev": (_int, [_vp, _vp, _vp, _vp, _u64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                   _vp, _vp]),
     "nkv_fill_splitmix64_dev": (_int, [_vp, _vp, _u64, _u64]),
 }
 

@@ -9,7 +9,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 SO = os.path.join(PKG, "libnkvmerkle.so")
-SOURCES = ["kernels.hip", "crc.hip", "capi.cpp"]
+SOURCES = ["kernels.hip", "crc.hip", "bloom.hip", "capi.cpp"]
 HEADERS = ["internal.hpp", "sha1_dev.hpp"]
 ARCH = os.environ.get("NKV_OFFLOAD_ARCH", "gfx950")
 

@@ -10,6 +10,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cmath>
 #include <vector>
 
 #include "internal.hpp"
@@ -660,6 +661,74 @@ int nkv_record_crc(nkv_ctx* c, const uint8_t* stream, uint64_t stream_len, const
     return NKV_OK;
 }
 
+int nkv_bloom_params(uint64_t n, double p, uint32_t* m, uint32_t* k) {
+    if (!m || !k || n == 0 || !(p > 0.0 && p < 1.0)) return NKV_ERR_INVALID;
+    const double ln2 = std::log(2.0);  // bloomfilter.go:18-24
+    const double mm = std::ceil(double(n) * std::fabs(std::log(p)) / std::pow(ln2, 2.0));
+    if (!(mm >= 1.0 && mm <= 4294967295.0)) return NKV_ERR_INVALID;
+    *m = uint32_t(mm);
+    *k = uint32_t(std::ceil((double(*m) / double(n)) * ln2));
+    return NKV_OK;
+}
+
+static uint64_t bloom_words(uint32_t m) { return (uint64_t(m) + 31) / 32; }
+
+int nkv_bloom_build(nkv_ctx* c, const uint8_t* keys, const uint64_t* off, const uint64_t* len, uint64_t n,
+                    uint32_t m, uint32_t k, uint32_t seed0, uint8_t* bits_out) {
+    TRY(bind(c));
+    if (m == 0 || !bits_out || (n && (!keys || !off || !len))) return NKV_ERR_INVALID;
+    const uint64_t nbytes = (uint64_t(m) + 7) / 8, wbytes = 4 * bloom_words(m);
+    TRY(grow(c->d_img, wbytes));
+    HIPTRY(hipMemsetAsync(c->d_img.p, 0, wbytes, c->stream));
+    if (n) {
+        uint64_t total = 0;
+        for (uint64_t i = 0; i < n; ++i) total = std::max(total, off[i] + len[i]);
+        TRY(grow_host(c, std::max<uint64_t>(total + 16 * n, wbytes)));
+        TRY(grow(c->d_data, total + 1));
+        TRY(grow(c->d_off, 8 * n));
+        TRY(grow(c->d_len, 8 * n));
+        uint8_t* h = static_cast<uint8_t*>(c->h_stage);
+        memcpy(h, keys, total);
+        memcpy(h + total, off, 8 * n);
+        memcpy(h + total + 8 * n, len, 8 * n);
+        HIPTRY(hipMemcpyAsync(c->d_data.p, h, total, hipMemcpyHostToDevice, c->stream));
+        HIPTRY(hipMemcpyAsync(c->d_off.p, h + total, 8 * n, hipMemcpyHostToDevice, c->stream));
+        HIPTRY(hipMemcpyAsync(c->d_len.p, h + total + 8 * n, 8 * n, hipMemcpyHostToDevice, c->stream));
+        TRY(nkv_bloom_insert_dev(c, c->d_data.p, static_cast<const uint64_t*>(c->d_off.p),
+                                 static_cast<const uint64_t*>(c->d_len.p), n, m, k, seed0, c->d_img.p));
+    }
+    HIPTRY(hipMemcpyAsync(bits_out, c->d_img.p, nbytes, hipMemcpyDeviceToHost, c->stream));
+    return st(hipStreamSynchronize(c->stream));
+}
+
+int nkv_bloom_from_records(nkv_ctx* c, const uint8_t* stream, uint64_t stream_len, const uint64_t* rec_size,
+                           uint64_t n, uint32_t m, uint32_t k, uint32_t seed0, uint8_t* bits_out) {
+    TRY(bind(c));
+    if (m == 0 || !bits_out || (n && (!stream || !rec_size))) return NKV_ERR_INVALID;
+    const uint64_t nbytes = (uint64_t(m) + 7) / 8, wbytes = 4 * bloom_words(m);
+    TRY(grow(c->d_img, wbytes));
+    HIPTRY(hipMemsetAsync(c->d_img.p, 0, wbytes, c->stream));
+    if (n) {
+        uint64_t sum = 0;
+        for (uint64_t i = 0; i < n; ++i) sum += rec_size[i];
+        if (sum > stream_len) return NKV_ERR_INVALID;
+        TRY(grow_host(c, stream_len + 8 * n));
+        TRY(grow(c->d_data, stream_len));
+        TRY(grow(c->d_aux, 8 * n));
+        TRY(grow(c->d_len, 8 * n));
+        uint8_t* h = static_cast<uint8_t*>(c->h_stage);
+        memcpy(h, stream, stream_len);
+        memcpy(h + stream_len, rec_size, 8 * n);
+        HIPTRY(hipMemcpyAsync(c->d_data.p, h, stream_len, hipMemcpyHostToDevice, c->stream));
+        HIPTRY(hipMemcpyAsync(c->d_aux.p, h + stream_len, 8 * n, hipMemcpyHostToDevice, c->stream));
+        uint64_t* rec_off = static_cast<uint64_t*>(c->d_len.p);
+        TRY(nkv_record_offsets_dev(c, static_cast<const uint64_t*>(c->d_aux.p), n, rec_off));
+        TRY(nkv_bloom_insert_records_dev(c, c->d_data.p, stream_len, rec_off, n, m, k, seed0, c->d_img.p));
+    }
+    HIPTRY(hipMemcpyAsync(bits_out, c->d_img.p, nbytes, hipMemcpyDeviceToHost, c->stream));
+    return st(hipStreamSynchronize(c->stream));
+}
+
 int nkv_write_file(const char* fname, const uint8_t* data, uint64_t len) {
     if (!fname || (!data && len)) return NKV_ERR_INVALID;
     int fd = open(fname, O_WRONLY | O_CREAT, 0666);  // no O_TRUNC: merkletree.go:68
@@ -790,6 +859,45 @@ int nkv_record_crc_dev(nkv_ctx* c, const void* d_stream, uint64_t stream_len, co
     }
     return st(launch_record_crc(static_cast<const uint8_t*>(d_stream), stream_len, d_rec_off, n, d_crc, stats,
                                 c->crc_load, c->stream));
+}
+
+int nkv_bloom_insert_dev(nkv_ctx* c, const void* d_keys, const uint64_t* d_off, const uint64_t* d_len, uint64_t n,
+                         uint32_t m, uint32_t k, uint32_t seed0, void* d_bits) {
+    TRY(bind(c));
+    if (m == 0 || !d_bits) return NKV_ERR_INVALID;
+    if (n == 0) return NKV_OK;
+    if (!d_keys || !d_off || !d_len) return NKV_ERR_INVALID;
+    return st(launch_bloom(0, false, static_cast<const uint8_t*>(d_keys), d_off, d_len, 0, n, m, k, seed0,
+                           static_cast<uint32_t*>(d_bits), nullptr, nullptr, c->stream));
+}
+
+int nkv_bloom_insert_records_dev(nkv_ctx* c, const void* d_stream, uint64_t stream_len, const uint64_t* d_rec_off,
+                                 uint64_t n, uint32_t m, uint32_t k, uint32_t seed0, void* d_bits) {
+    TRY(bind(c));
+    if (m == 0 || !d_bits) return NKV_ERR_INVALID;
+    if (n == 0) return NKV_OK;
+    if (!d_stream || !d_rec_off) return NKV_ERR_INVALID;
+    TRY(grow(c->d_err, 4));
+    unsigned int* err = static_cast<unsigned int*>(c->d_err.p);
+    HIPTRY(hipMemsetAsync(err, 0, 4, c->stream));
+    HIPTRY(launch_bloom(1, false, static_cast<const uint8_t*>(d_stream), d_rec_off, nullptr, stream_len, n, m, k,
+                        seed0, static_cast<uint32_t*>(d_bits), nullptr, err, c->stream));
+    unsigned int h = 0;
+    HIPTRY(hipMemcpyAsync(&h, err, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPTRY(hipStreamSynchronize(c->stream));
+    return h ? NKV_ERR_INVALID : NKV_OK;
+}
+
+int nkv_bloom_query_dev(nkv_ctx* c, const void* d_keys, const uint64_t* d_off, const uint64_t* d_len, uint64_t n,
+                        uint32_t m, uint32_t k, uint32_t seed0, const void* d_bits, uint8_t* d_out) {
+    TRY(bind(c));
+    if (m == 0 || !d_bits) return NKV_ERR_INVALID;
+    if (n == 0) return NKV_OK;
+    if (!d_keys || !d_off || !d_len || !d_out) return NKV_ERR_INVALID;
+    if (k == 0) return st(hipMemsetAsync(d_out, 1, n, c->stream));  // Query with no hashes: true
+    return st(launch_bloom(0, true, static_cast<const uint8_t*>(d_keys), d_off, d_len, 0, n, m, k, seed0,
+                           const_cast<uint32_t*>(static_cast<const uint32_t*>(d_bits)), d_out, nullptr,
+                           c->stream));
 }
 
 int nkv_fill_splitmix64_dev(nkv_ctx* c, void* d_buf, uint64_t nbytes, uint64_t seed) {

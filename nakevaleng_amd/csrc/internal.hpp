@@ -58,6 +58,11 @@ hipError_t launch_crc_spans(const uint8_t* base, const uint64_t* off, const uint
                             uint32_t* out, int variant, hipStream_t s);
 hipError_t launch_record_crc(const uint8_t* stream, uint64_t stream_len, const uint64_t* rec_off, uint64_t n,
                              uint32_t* out, unsigned long long* stats, int variant, hipStream_t s);
+// bloom.hip: mode 0 = keys at base + off[i], len[i]; 1 = keys of the records at
+// base + off[i].  query: out[i] = all k bits set; else OR the bits in.
+hipError_t launch_bloom(int mode, bool query, const uint8_t* base, const uint64_t* off, const uint64_t* len,
+                        uint64_t stream_len, uint64_t n, uint32_t m, uint32_t k, uint32_t seed0, uint32_t* bits,
+                        uint8_t* out, unsigned int* err, hipStream_t s);
 hipError_t launch_fill(uint8_t* buf, uint64_t nbytes, uint64_t seed, hipStream_t s);
 
 }  // namespace nkv

@@ -4,10 +4,12 @@
   make_table_secondaries     Merkle part of MakeTableSecondaries   sstable.go:35-47
   make_metadata_from_records the same, hashing Values in place inside the
                              serialized Data table
+  make_filter_contents       the bits of sstable.makeFilter  sstable.go:49-56 (8f row 4)
+  make_filter_from_records   the same over the keys of a serialized Data table
   table_filename             util/filename.Table             filename.go:58-65, 300-309
 
-Everything else the writer produces (Data, Index, Summary, Filter files) is
-outside this path and unchanged.
+Everything else the writer produces (Data, Index, Summary files; the Filter's
+gob encoding) is outside this path and unchanged.
 """
 from __future__ import annotations
 
@@ -67,3 +69,33 @@ def make_metadata_from_records(path: str, dbname: str, level: int, run: int, str
     fname = table_filename(path, dbname, level, run)
     _lib.check(L.nkv_write_file(fname.encode(), _lib.p8(img), img.size), f"Serialize({fname})")
     return root.tobytes()
+
+
+def make_filter_contents(keys, seed: int, false_positive_rate: float = 0.01, ctx=None):
+    """sstable.makeFilter (sstable.go:49-56) minus the gob file: bloomfilter.New(
+    len(keys), 0.01), Insert(key) for every key, on the device.  Returns the
+    filter (M, K, HashSeeds, Contents).  The reference's seed is the clock."""
+    from . import bloomfilter
+    bf = bloomfilter.New(len(keys), false_positive_rate, seed=seed, ctx=ctx)
+    bf.InsertMany(keys)
+    bf.Contents  # noqa: B018 -- one device batch
+    return bf
+
+
+def make_filter_from_records(stream, rec_sizes, seed: int, false_positive_rate: float = 0.01, ctx=None):
+    """makeFilter over the keys of a serialized Data table (KeyContext.Key is the
+    record's Key), hashed in place on the device (nkv_bloom_from_records)."""
+    import ctypes
+    from . import bloomfilter
+    sizes = np.ascontiguousarray(rec_sizes, dtype=np.uint64)
+    bf = bloomfilter.New(int(sizes.size), false_positive_rate, seed=seed, ctx=ctx)
+    buf = np.frombuffer(bytes(stream), np.uint8) if not isinstance(stream, np.ndarray) else stream
+    buf = np.ascontiguousarray(buf, dtype=np.uint8)
+    bits = np.zeros((bf.M + 7) // 8, np.uint8)
+    ctx = ctx or _lib.default_context()
+    _lib.check(_lib.lib().nkv_bloom_from_records(ctx.h, _lib.p8(buf if buf.size else np.zeros(1, np.uint8)),
+                                                 buf.size, _lib.p64(sizes if sizes.size else np.zeros(1, np.uint64)),
+                                                 sizes.size, bf.M, bf.K, bf.HashSeeds[0] if bf.K else 0,
+                                                 _lib.p8(bits)))
+    bf._contents = bytearray(bits.tobytes())
+    return bf

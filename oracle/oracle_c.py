@@ -21,7 +21,7 @@ u64p = ctypes.POINTER(ctypes.c_uint64)
 
 
 def build() -> str:
-    srcs = [os.path.join(_HERE, f) for f in ("merkle_oracle.c", "record_crc_oracle.c")]
+    srcs = [os.path.join(_HERE, f) for f in ("merkle_oracle.c", "record_crc_oracle.c", "bloom_oracle.c")]
     if not os.path.exists(_SO) or os.path.getmtime(_SO) < max(os.path.getmtime(s) for s in srcs):
         subprocess.check_call(["make", "-s", "-C", _HERE, "liboracle.so"])
     return _SO
@@ -52,6 +52,14 @@ def lib():
         L.nkvo_crc32.restype = ctypes.c_uint32
         L.nkvo_record_crcs.argtypes = [u8p, u64p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint32), u8p]
         L.nkvo_record_crcs.restype = ctypes.c_uint64
+        L.nkvo_murmur3_32.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint32]
+        L.nkvo_murmur3_32.restype = ctypes.c_uint32
+        L.nkvo_bloom_params.argtypes = [ctypes.c_uint64, ctypes.c_double, ctypes.POINTER(ctypes.c_uint32),
+                                        ctypes.POINTER(ctypes.c_uint32)]
+        L.nkvo_bloom_insert.argtypes = [u8p, u64p, u64p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                        ctypes.c_uint32, u8p]
+        L.nkvo_bloom_query.argtypes = [u8p, u64p, u64p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                       ctypes.c_uint32, u8p, u8p]
         _lib = L
     return _lib
 
@@ -157,3 +165,37 @@ def record_crcs(stream: np.ndarray, rec_off: np.ndarray):
     bad = lib().nkvo_record_crcs(_p8(stream), _p64(off if n else np.zeros(1, np.uint64)), n,
                                  crc.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), _p8(ok))
     return crc[:n], ok[:n].astype(bool), int(bad)
+
+
+def murmur3_32(data, seed: int) -> int:
+    """MurmurHash3_x86_32 as spaolacci/murmur3 Sum32 (bloomfilter.go:79-81)."""
+    a = np.frombuffer(bytes(data), np.uint8) if not isinstance(data, np.ndarray) else data
+    a = np.ascontiguousarray(a, dtype=np.uint8)
+    buf = a if a.size else np.zeros(1, np.uint8)
+    return int(lib().nkvo_murmur3_32(_p8(buf), a.size, seed & 0xFFFFFFFF))
+
+
+def bloom_params(n: int, p: float):
+    m, k = ctypes.c_uint32(0), ctypes.c_uint32(0)
+    lib().nkvo_bloom_params(n, p, ctypes.byref(m), ctypes.byref(k))
+    return m.value, k.value
+
+
+def bloom_insert(base: np.ndarray, off: np.ndarray, ln: np.ndarray, m: int, k: int, seed0: int) -> np.ndarray:
+    bits = np.zeros((m + 7) // 8, np.uint8)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    ln = np.ascontiguousarray(ln, dtype=np.uint64)
+    buf = base if base.size else np.zeros(1, np.uint8)
+    lib().nkvo_bloom_insert(_p8(buf), _p64(off), _p64(ln), off.size, m, k, seed0 & 0xFFFFFFFF, _p8(bits))
+    return bits
+
+
+def bloom_query(base: np.ndarray, off: np.ndarray, ln: np.ndarray, m: int, k: int, seed0: int,
+                bits: np.ndarray) -> np.ndarray:
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    ln = np.ascontiguousarray(ln, dtype=np.uint64)
+    out = np.zeros(max(off.size, 1), np.uint8)
+    buf = base if base.size else np.zeros(1, np.uint8)
+    lib().nkvo_bloom_query(_p8(buf), _p64(off), _p64(ln), off.size, m, k, seed0 & 0xFFFFFFFF,
+                           _p8(np.ascontiguousarray(bits)), _p8(out))
+    return out[:off.size].astype(bool)

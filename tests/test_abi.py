@@ -103,3 +103,18 @@ def test_no_cpu_fallback_without_device(lib):
         pytest.skip("a device is visible")
     with pytest.raises(lib.NkvError):
         lib.Context(0)
+
+
+def test_bloom_params_host_function_matches_oracle(oracle):
+    """nkv_bloom_params is pure host math (no device): bloomfilter.go:18-24."""
+    import ctypes
+    from nakevaleng_amd import _lib
+    L = _lib.lib()
+    for n in (1, 7, 100, 4096, 1 << 20):
+        for p in (0.01, 0.2, 0.001):
+            m, k = ctypes.c_uint32(0), ctypes.c_uint32(0)
+            assert L.nkv_bloom_params(n, p, ctypes.byref(m), ctypes.byref(k)) == 0
+            assert (m.value, k.value) == oracle.bloom_params(n, p)
+    m, k = ctypes.c_uint32(0), ctypes.c_uint32(0)
+    assert L.nkv_bloom_params(0, 0.01, ctypes.byref(m), ctypes.byref(k)) == _lib.NKV_ERR_INVALID
+    assert L.nkv_bloom_params(10, 1.5, ctypes.byref(m), ctypes.byref(k)) == _lib.NKV_ERR_INVALID

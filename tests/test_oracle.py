@@ -147,3 +147,58 @@ def test_record_crcs_on_serialized_stream(oracle):
     buf[int(off[3]) + 30] ^= 1  # corrupt record 3's first key byte
     crc2, ok2, bad2 = oracle.record_crcs(buf, off)
     assert bad2 == 1 and not ok2[3] and ok2[[i for i in range(len(recs)) if i != 3]].all()
+
+
+# --- SSTable filter: murmur3 Bloom inserts ---
+
+MURMUR3_VECTORS = [  # published MurmurHash3_x86_32 vectors (input, seed, hash)
+    (b"", 0, 0x00000000), (b"", 1, 0x514E28B7), (b"", 0xFFFFFFFF, 0x81F16F39),
+    (b"\x00\x00\x00\x00", 0, 0x2362F9DE), (b"\xff\xff\xff\xff", 0, 0x76293B50),
+    (b"\x21\x43\x65\x87", 0, 0xF55B516B), (b"\x21\x43\x65\x87", 0x5082EDEE, 0x2362F9DE),
+    (b"\x21\x43\x65", 0, 0x7E4A8634), (b"\x21\x43", 0, 0xA0F7B07A), (b"\x21", 0, 0x72661CF4),
+    (b"aaaa", 0x9747B28C, 0x5A97808A), (b"Hello, world!", 0x9747B28C, 0x24884CBA),
+    (b"The quick brown fox jumps over the lazy dog", 0x9747B28C, 0x2FA826CD),
+]
+
+
+@pytest.mark.parametrize("data,seed,want", MURMUR3_VECTORS)
+def test_murmur3_published_vectors(oracle, data, seed, want):
+    assert oracle.murmur3_32(data, seed) == want
+
+
+def test_murmur3_matches_sklearn(oracle):
+    from sklearn.utils import murmurhash3_32
+    rng = np.random.default_rng(13)
+    for n in list(range(0, 40)) + [100, 1000]:
+        d = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        seed = int(rng.integers(0, 2**32))
+        assert oracle.murmur3_32(d, seed) == murmurhash3_32(d, seed=seed, positive=True)
+
+
+def test_bloom_params_match_reference_formula(oracle):
+    import math
+    for n in (1, 2, 10, 100, 1000, 12345, 1 << 20):
+        for p in (0.01, 0.1, 0.2, 0.001):
+            m = math.ceil(n * abs(math.log(p)) / math.pow(math.log(2), 2))
+            k = math.ceil((m / n) * math.log(2))
+            assert oracle.bloom_params(n, p) == (m, k)
+    assert oracle.bloom_params(1 << 20, 0.01) == (10050663, 7)
+
+
+def test_bloom_insert_then_query(oracle):
+    rng = np.random.default_rng(14)
+    n = 2000
+    ln = rng.integers(0, 40, n).astype(np.uint64)
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum(ln[:-1])
+    keys = rng.integers(0, 256, int(ln.sum()) + 1, dtype=np.uint8)
+    m, k = oracle.bloom_params(n, 0.01)
+    bits = oracle.bloom_insert(keys, off, ln, m, k, 12345)
+    assert oracle.bloom_query(keys, off, ln, m, k, 12345, bits).all()  # no false negatives
+    # the reference's bit numbering: Contents[idx / 8] |= 1 << (idx % 8)
+    idx = oracle.murmur3_32(keys[int(off[0]):int(off[0] + ln[0])], 12345) % m
+    assert bits[idx // 8] >> (idx % 8) & 1
+    other = rng.integers(0, 256, 64 * 1000, dtype=np.uint8)
+    qoff = np.arange(1000, dtype=np.uint64) * 64
+    fp = oracle.bloom_query(other, qoff, np.full(1000, 64, np.uint64), m, k, 12345, bits).mean()
+    assert fp < 0.05
