@@ -40,8 +40,9 @@ def test_bloom_insert_device_matches_oracle(nkv, oracle, m, k):
     seed0 = int(rng.integers(0, 2**32))
     words = ((m + 31) // 32) * 4
     d_bits = torch.zeros(words, dtype=torch.uint8, device="cuda")
-    _lib.check(L.nkv_bloom_insert_dev(ctx.h, _dev(torch, data).data_ptr(), _dev(torch, off).data_ptr(),
-                                      _dev(torch, ln).data_ptr(), ln.size, m, k, seed0, d_bits.data_ptr()))
+    d_data, d_off, d_len = _dev(torch, data), _dev(torch, off), _dev(torch, ln)  # held until the kernel ran
+    _lib.check(L.nkv_bloom_insert_dev(ctx.h, d_data.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), ln.size,
+                                      m, k, seed0, d_bits.data_ptr()))
     torch.cuda.synchronize()
     got = d_bits.cpu().numpy()
     want = oracle.bloom_insert(data, off, ln, m, k, seed0)
@@ -63,9 +64,9 @@ def test_bloom_query_device_matches_oracle(nkv, oracle):
     words[:bits.size] = bits
     for d, o, l_ in ((data, off, ln), (qdata, qoff, qln)):
         out = torch.zeros(l_.size, dtype=torch.uint8, device="cuda")
-        _lib.check(L.nkv_bloom_query_dev(ctx.h, _dev(torch, d).data_ptr(), _dev(torch, o).data_ptr(),
-                                         _dev(torch, l_).data_ptr(), l_.size, m, k, 99, _dev(torch, words).data_ptr(),
-                                         out.data_ptr()))
+        held = [_dev(torch, a) for a in (d, o, l_, words)]  # alive until the kernel ran
+        _lib.check(L.nkv_bloom_query_dev(ctx.h, held[0].data_ptr(), held[1].data_ptr(), held[2].data_ptr(),
+                                         l_.size, m, k, 99, held[3].data_ptr(), out.data_ptr()))
         torch.cuda.synchronize()
         assert np.array_equal(out.cpu().numpy().astype(bool), oracle.bloom_query(d, o, l_, m, k, 99, bits))
 
@@ -127,8 +128,9 @@ def test_bloom_sstable_shape_1m_keys(nkv, oracle):
     ln = np.full(n, 16, np.uint64)
     m, k = oracle.bloom_params(n, 0.01)
     d_bits = torch.zeros(((m + 31) // 32) * 4, dtype=torch.uint8, device="cuda")
-    _lib.check(L.nkv_bloom_insert_dev(ctx.h, _dev(torch, data).data_ptr(), _dev(torch, off).data_ptr(),
-                                      _dev(torch, ln).data_ptr(), n, m, k, 0xABCD1234, d_bits.data_ptr()))
+    d_data, d_off, d_len = _dev(torch, data), _dev(torch, off), _dev(torch, ln)  # held until the kernel ran
+    _lib.check(L.nkv_bloom_insert_dev(ctx.h, d_data.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n,
+                                      m, k, 0xABCD1234, d_bits.data_ptr()))
     torch.cuda.synchronize()
     want = oracle.bloom_insert(data, off, ln, m, k, 0xABCD1234)
     assert np.array_equal(d_bits.cpu().numpy()[:want.size], want)
