@@ -44,7 +44,8 @@
  *     (nkv_bfs_size(n) bytes for 20-byte leaves).
  *   - Host-pointer functions are synchronous: outputs are written before
  *     return, and no caller pointer is retained (cgo rule).  Inputs are
- *     staged through library-owned pinned memory.
+ *     staged through library-owned pinned memory: a pool of host threads
+ *     gathers chunk k+1 while chunk k is copied to the device.
  *   - *_dev functions take device pointers and are asynchronous on the
  *     context's stream (nkv_ctx_set_stream); nkv_ctx_sync() waits.
  *   - Thread safety: distinct contexts may be used concurrently; one context
@@ -107,6 +108,11 @@ int nkv_ctx_sync(nkv_ctx *ctx);
                                  chunks through an LDS ring (else per-lane loads); bits
                                  1-2 = LDS table copies x workgroup: 0 = 8 x 256,
                                  1 = 16 x 512, 2 = 32 x 1024 (no ring) */
+#define NKV_OPT_HOST_THREADS 7 /* host-buffer API: threads that gather caller bytes into the
+                                  pinned staging chunks (0 = default: min(16, cores), or
+                                  the NKV_HOST_THREADS environment variable) */
+#define NKV_OPT_STAGE_CHUNK 8  /* host-buffer API: bytes per pinned staging chunk (multiple of
+                                  4096, default 32 MiB; three chunks are in flight) */
 int nkv_ctx_set_option(nkv_ctx *ctx, int key, int64_t value);
 /* When enabled, the device-resident tree calls record HIP events around the
  * leaf kernel and the tree reduce on the context's stream. */

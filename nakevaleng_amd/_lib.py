@@ -26,6 +26,8 @@ NKV_OPT_DEEP_PREFETCH = 3
 NKV_OPT_QUEUE_SPLIT = 4
 NKV_OPT_QUEUE_WAVES = 5
 NKV_OPT_CRC_LOAD = 6
+NKV_OPT_HOST_THREADS = 7
+NKV_OPT_STAGE_CHUNK = 8
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)
 _u64p = ctypes.POINTER(ctypes.c_uint64)

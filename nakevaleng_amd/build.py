@@ -9,8 +9,8 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 SO = os.path.join(PKG, "libnkvmerkle.so")
-SOURCES = ["kernels.hip", "crc.hip", "bloom.hip", "capi.cpp"]
-HEADERS = ["internal.hpp", "sha1_dev.hpp"]
+SOURCES = ["kernels.hip", "crc.hip", "bloom.hip", "capi.cpp", "host_stage.cpp"]
+HEADERS = ["internal.hpp", "sha1_dev.hpp", "host_stage.hpp"]
 ARCH = os.environ.get("NKV_OFFLOAD_ARCH", "gfx950")
 
 
@@ -32,7 +32,7 @@ def build(force: bool = False, verbose: bool = False, diag: bool = False) -> str
         return SO
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     tmp = so + ".tmp"
-    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread",
            "-Wall", "-Wno-unused-result", "-I", os.path.join(ROOT, "include"), "-I", CSRC]
     if diag:
         cmd.append("-DNKV_DIAG")

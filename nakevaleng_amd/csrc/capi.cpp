@@ -13,6 +13,7 @@
 #include <cmath>
 #include <vector>
 
+#include "host_stage.hpp"
 #include "internal.hpp"
 #include "nkv_merkle.h"
 
@@ -110,8 +111,9 @@ struct nkv_ctx {
     std::vector<hipEvent_t> ring;
     size_t ring_used = 0;
     DevBuf d_data, d_off, d_len, d_nodes, d_img, d_tmp, d_err, d_aux, d_keys, d_perm, d_stmp, d_queue, d_stats;
-    void* h_stage = nullptr;
+    void* h_stage = nullptr;  // small pinned staging (offsets, lengths, stats)
     size_t h_cap = 0;
+    Stager stage;  // pipelined pinned staging of bulk bytes (host_stage.hpp)
 };
 
 namespace {
@@ -172,9 +174,10 @@ int grow_host(nkv_ctx* c, size_t bytes) {
 
 uint64_t align16(uint64_t x) { return (x + 15) & ~uint64_t(15); }
 
-// Pack n host values into the pinned stage at 16-byte aligned offsets
-// (lib-owned copy: no caller pointer is kept) and upload them with their
-// packed offsets/lengths to d_data / d_off / d_len.
+// Pack n host values into d_data at 16-byte aligned offsets and upload their
+// packed offsets/lengths to d_off / d_len.  The bytes go through the pipelined
+// pinned stager (a pool of host threads gathers chunk k+1 while chunk k is in
+// flight); no caller pointer is kept.
 int stage_values(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint64_t* len,
                  uint64_t n) {
     uint64_t total = 0;
@@ -182,24 +185,34 @@ int stage_values(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uin
         if (len[i] > (uint64_t(1) << 62) || total > (uint64_t(1) << 62)) return NKV_ERR_INVALID;
         total += align16(len[i]);
     }
-    const uint64_t meta = 16 * n;
-    TRY(grow_host(c, total + meta));
+    TRY(grow_host(c, 16 * n));
     TRY(grow(c->d_data, total));
     TRY(grow(c->d_off, 8 * n));
     TRY(grow(c->d_len, 8 * n));
-    uint8_t* h = static_cast<uint8_t*>(c->h_stage);
-    uint64_t* hoff = reinterpret_cast<uint64_t*>(h + total);
+    uint64_t* hoff = static_cast<uint64_t*>(c->h_stage);
     uint64_t* hlen = hoff + n;
     uint64_t p = 0;
     for (uint64_t i = 0; i < n; ++i) {
-        if (len[i]) memcpy(h + p, base + off[i], len[i]);
         hoff[i] = p;
         hlen[i] = len[i];
         p += align16(len[i]);
     }
-    HIPTRY(hipMemcpyAsync(c->d_data.p, h, total, hipMemcpyHostToDevice, c->stream));
+    const Segments seg{base, off, len, hoff, n};
+    HIPTRY(c->stage.upload(seg, total, static_cast<uint8_t*>(c->d_data.p), c->stream));
     HIPTRY(hipMemcpyAsync(c->d_off.p, hoff, 8 * n, hipMemcpyHostToDevice, c->stream));
     HIPTRY(hipMemcpyAsync(c->d_len.p, hlen, 8 * n, hipMemcpyHostToDevice, c->stream));
+    return NKV_OK;
+}
+
+// Contiguous host bytes -> d (bulk path) plus n u64 -> d64 (through h_stage).
+int stage_stream(nkv_ctx* c, const uint8_t* src, uint64_t bytes, DevBuf& d, const uint64_t* v64,
+                 uint64_t n, DevBuf& d64) {
+    TRY(grow(d, bytes));
+    TRY(grow(d64, 8 * n));
+    TRY(grow_host(c, 8 * n));
+    HIPTRY(c->stage.upload(src, bytes, static_cast<uint8_t*>(d.p), c->stream));
+    memcpy(c->h_stage, v64, 8 * n);
+    HIPTRY(hipMemcpyAsync(d64.p, c->h_stage, 8 * n, hipMemcpyHostToDevice, c->stream));
     return NKV_OK;
 }
 
@@ -210,10 +223,9 @@ int finish_tree(nkv_ctx* c, uint8_t* nodes, uint64_t n, uint8_t* root20, uint8_t
         BfsLayout lay = layout_of(counts_of(n));
         TRY(grow(c->d_img, lay.total));
         HIPTRY(launch_bfs_image(nodes, lay, static_cast<uint8_t*>(c->d_img.p), c->stream));
-        HIPTRY(hipMemcpyAsync(img_out, c->d_img.p, lay.total, hipMemcpyDeviceToHost, c->stream));
+        HIPTRY(c->stage.download(img_out, static_cast<const uint8_t*>(c->d_img.p), lay.total, c->stream));
     }
-    if (nodes_out)
-        HIPTRY(hipMemcpyAsync(nodes_out, nodes, 20 * tot, hipMemcpyDeviceToHost, c->stream));
+    if (nodes_out) HIPTRY(c->stage.download(nodes_out, nodes, 20 * tot, c->stream));
     if (root20)
         HIPTRY(hipMemcpyAsync(root20, nodes + 20 * (tot - 1), 20, hipMemcpyDeviceToHost, c->stream));
     HIPTRY(hipStreamSynchronize(c->stream));
@@ -389,6 +401,15 @@ int nkv_ctx_set_option(nkv_ctx* c, int key, int64_t value) {
             if (value < 0 || value > 5) return NKV_ERR_INVALID;
             c->crc_load = int(value);
             return NKV_OK;
+        case NKV_OPT_HOST_THREADS:
+            if (value < 0 || value > 256) return NKV_ERR_INVALID;
+            c->stage.want_threads = int(value);
+            return NKV_OK;
+        case NKV_OPT_STAGE_CHUNK:
+            if (value < 4096 || value > (int64_t(1) << 32) || (value & 4095)) return NKV_ERR_INVALID;
+            if (c->stage.drain() != hipSuccess) return NKV_ERR_DEVICE;
+            c->stage.chunk = size_t(value);
+            return NKV_OK;
         case NKV_OPT_QUEUE_WAVES:
             if (value < 1 || value > 5) return NKV_ERR_INVALID;  // 8 KiB LDS per wave: <= 20 per CU
             c->queue_waves = int(value);
@@ -481,7 +502,7 @@ int nkv_leaf_hash(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const ui
     uint8_t* nodes = static_cast<uint8_t*>(c->d_nodes.p);
     TRY(leaf_level(c, static_cast<const uint8_t*>(c->d_data.p), static_cast<const uint64_t*>(c->d_off.p),
                    static_cast<const uint64_t*>(c->d_len.p), n, true, nodes));
-    HIPTRY(hipMemcpyAsync(out20, nodes, 20 * n, hipMemcpyDeviceToHost, c->stream));
+    HIPTRY(c->stage.download(out20, nodes, 20 * n, c->stream));
     return st(hipStreamSynchronize(c->stream));
 }
 
@@ -492,9 +513,7 @@ int nkv_tree_build(nkv_ctx* c, const uint8_t* leaf20, uint64_t n, uint8_t* root2
     if (!leaf20) return NKV_ERR_INVALID;
     TRY(grow(c->d_nodes, 20 * total_of(n)));
     uint8_t* nodes = static_cast<uint8_t*>(c->d_nodes.p);
-    TRY(grow_host(c, 20 * n));
-    memcpy(c->h_stage, leaf20, 20 * n);
-    HIPTRY(hipMemcpyAsync(nodes, c->h_stage, 20 * n, hipMemcpyHostToDevice, c->stream));
+    HIPTRY(c->stage.upload(leaf20, 20 * n, nodes, c->stream));
     HIPTRY(launch_reduce(nodes, n, 0, levels_of(n) - 1, c->stream));
     return finish_tree(c, nodes, n, root20, nodes_out, img_out);
 }
@@ -556,8 +575,7 @@ int nkv_tree_generic(nkv_ctx* c, const uint8_t* data, const uint64_t* off, const
     TRY(leaf_level(c, static_cast<const uint8_t*>(c->d_data.p), static_cast<const uint64_t*>(c->d_off.p),
                    static_cast<const uint64_t*>(c->d_len.p), n1, true, up));
     if (n1 > 1) HIPTRY(launch_reduce(up, n1, 0, levels_of(n1) - 1, c->stream));
-    if (upper_out)
-        HIPTRY(hipMemcpyAsync(upper_out, up, 20 * up_total, hipMemcpyDeviceToHost, c->stream));
+    if (upper_out) HIPTRY(c->stage.download(upper_out, up, 20 * up_total, c->stream));
     if (root20)
         HIPTRY(hipMemcpyAsync(root20, up + 20 * (up_total - 1), 20, hipMemcpyDeviceToHost,
                               c->stream));
@@ -571,7 +589,7 @@ int nkv_tree_generic(nkv_ctx* c, const uint8_t* data, const uint64_t* off, const
         upper_img = lay.total;
         TRY(grow(c->d_img, lay.total));
         HIPTRY(launch_bfs_image(up, lay, static_cast<uint8_t*>(c->d_img.p), c->stream));
-        HIPTRY(hipMemcpyAsync(img_out, c->d_img.p, lay.total, hipMemcpyDeviceToHost, c->stream));
+        HIPTRY(c->stage.download(img_out, static_cast<const uint8_t*>(c->d_img.p), lay.total, c->stream));
     }
     HIPTRY(hipStreamSynchronize(c->stream));
     if (img_out) {
@@ -599,14 +617,7 @@ int nkv_tree_from_records(nkv_ctx* c, const uint8_t* stream, uint64_t stream_len
     uint64_t sum = 0;
     for (uint64_t i = 0; i < n; ++i) sum += rec_size[i];
     if (sum > stream_len) return NKV_ERR_INVALID;
-    TRY(grow_host(c, stream_len + 8 * n));
-    TRY(grow(c->d_data, stream_len));
-    TRY(grow(c->d_aux, 8 * n));
-    uint8_t* h = static_cast<uint8_t*>(c->h_stage);
-    memcpy(h, stream, stream_len);
-    memcpy(h + stream_len, rec_size, 8 * n);
-    HIPTRY(hipMemcpyAsync(c->d_data.p, h, stream_len, hipMemcpyHostToDevice, c->stream));
-    HIPTRY(hipMemcpyAsync(c->d_aux.p, h + stream_len, 8 * n, hipMemcpyHostToDevice, c->stream));
+    TRY(stage_stream(c, stream, stream_len, c->d_data, rec_size, n, c->d_aux));
     TRY(grow(c->d_off, 8 * n));
     TRY(grow(c->d_len, 8 * n));
     // d_len doubles as the record-offset scratch before it receives lengths
@@ -633,31 +644,24 @@ int nkv_record_crc(nkv_ctx* c, const uint8_t* stream, uint64_t stream_len, const
     uint64_t sum = 0;
     for (uint64_t i = 0; i < n; ++i) sum += rec_size[i];
     if (sum > stream_len) return NKV_ERR_INVALID;
-    TRY(grow_host(c, std::max<uint64_t>(stream_len + 8 * n, 4 * n + 24)));
-    TRY(grow(c->d_data, stream_len));
-    TRY(grow(c->d_aux, 8 * n));
+    TRY(stage_stream(c, stream, stream_len, c->d_data, rec_size, n, c->d_aux));
     TRY(grow(c->d_len, 8 * n));
     TRY(grow(c->d_off, 4 * n));
-    uint8_t* h = static_cast<uint8_t*>(c->h_stage);
-    memcpy(h, stream, stream_len);
-    memcpy(h + stream_len, rec_size, 8 * n);
-    HIPTRY(hipMemcpyAsync(c->d_data.p, h, stream_len, hipMemcpyHostToDevice, c->stream));
-    HIPTRY(hipMemcpyAsync(c->d_aux.p, h + stream_len, 8 * n, hipMemcpyHostToDevice, c->stream));
     uint64_t* rec_off = static_cast<uint64_t*>(c->d_len.p);
     TRY(nkv_record_offsets_dev(c, static_cast<const uint64_t*>(c->d_aux.p), n, rec_off));
     TRY(grow(c->d_stats, 24));
     uint32_t* d_crc = static_cast<uint32_t*>(c->d_off.p);
     uint64_t* d_stats = static_cast<uint64_t*>(c->d_stats.p);
     TRY(nkv_record_crc_dev(c, c->d_data.p, stream_len, rec_off, n, d_crc, d_stats));
-    // the staging copies above have been consumed once the stream reaches here
-    uint64_t* hs = reinterpret_cast<uint64_t*>(h);
+    // the rec_size copy in h_stage has been consumed once the stream reaches here
+    uint64_t* hs = static_cast<uint64_t*>(c->h_stage);
     HIPTRY(hipMemcpyAsync(hs, d_stats, 24, hipMemcpyDeviceToHost, c->stream));
-    if (crc_out) HIPTRY(hipMemcpyAsync(h + 24, d_crc, 4 * n, hipMemcpyDeviceToHost, c->stream));
     HIPTRY(hipStreamSynchronize(c->stream));
     if (hs[2]) return NKV_ERR_INVALID;
     if (n_bad) *n_bad = hs[0];
     if (first_bad) *first_bad = hs[1];
-    if (crc_out) memcpy(crc_out, h + 24, 4 * n);
+    if (crc_out) HIPTRY(c->stage.download(reinterpret_cast<uint8_t*>(crc_out), reinterpret_cast<const uint8_t*>(d_crc),
+                                          4 * n, c->stream));
     return NKV_OK;
 }
 
@@ -683,21 +687,20 @@ int nkv_bloom_build(nkv_ctx* c, const uint8_t* keys, const uint64_t* off, const 
     if (n) {
         uint64_t total = 0;
         for (uint64_t i = 0; i < n; ++i) total = std::max(total, off[i] + len[i]);
-        TRY(grow_host(c, std::max<uint64_t>(total + 16 * n, wbytes)));
+        TRY(grow_host(c, 16 * n));
         TRY(grow(c->d_data, total + 1));
         TRY(grow(c->d_off, 8 * n));
         TRY(grow(c->d_len, 8 * n));
         uint8_t* h = static_cast<uint8_t*>(c->h_stage);
-        memcpy(h, keys, total);
-        memcpy(h + total, off, 8 * n);
-        memcpy(h + total + 8 * n, len, 8 * n);
-        HIPTRY(hipMemcpyAsync(c->d_data.p, h, total, hipMemcpyHostToDevice, c->stream));
-        HIPTRY(hipMemcpyAsync(c->d_off.p, h + total, 8 * n, hipMemcpyHostToDevice, c->stream));
-        HIPTRY(hipMemcpyAsync(c->d_len.p, h + total + 8 * n, 8 * n, hipMemcpyHostToDevice, c->stream));
+        HIPTRY(c->stage.upload(keys, total, static_cast<uint8_t*>(c->d_data.p), c->stream));
+        memcpy(h, off, 8 * n);
+        memcpy(h + 8 * n, len, 8 * n);
+        HIPTRY(hipMemcpyAsync(c->d_off.p, h, 8 * n, hipMemcpyHostToDevice, c->stream));
+        HIPTRY(hipMemcpyAsync(c->d_len.p, h + 8 * n, 8 * n, hipMemcpyHostToDevice, c->stream));
         TRY(nkv_bloom_insert_dev(c, c->d_data.p, static_cast<const uint64_t*>(c->d_off.p),
                                  static_cast<const uint64_t*>(c->d_len.p), n, m, k, seed0, c->d_img.p));
     }
-    HIPTRY(hipMemcpyAsync(bits_out, c->d_img.p, nbytes, hipMemcpyDeviceToHost, c->stream));
+    HIPTRY(c->stage.download(bits_out, static_cast<const uint8_t*>(c->d_img.p), nbytes, c->stream));
     return st(hipStreamSynchronize(c->stream));
 }
 
@@ -712,20 +715,13 @@ int nkv_bloom_from_records(nkv_ctx* c, const uint8_t* stream, uint64_t stream_le
         uint64_t sum = 0;
         for (uint64_t i = 0; i < n; ++i) sum += rec_size[i];
         if (sum > stream_len) return NKV_ERR_INVALID;
-        TRY(grow_host(c, stream_len + 8 * n));
-        TRY(grow(c->d_data, stream_len));
-        TRY(grow(c->d_aux, 8 * n));
+        TRY(stage_stream(c, stream, stream_len, c->d_data, rec_size, n, c->d_aux));
         TRY(grow(c->d_len, 8 * n));
-        uint8_t* h = static_cast<uint8_t*>(c->h_stage);
-        memcpy(h, stream, stream_len);
-        memcpy(h + stream_len, rec_size, 8 * n);
-        HIPTRY(hipMemcpyAsync(c->d_data.p, h, stream_len, hipMemcpyHostToDevice, c->stream));
-        HIPTRY(hipMemcpyAsync(c->d_aux.p, h + stream_len, 8 * n, hipMemcpyHostToDevice, c->stream));
         uint64_t* rec_off = static_cast<uint64_t*>(c->d_len.p);
         TRY(nkv_record_offsets_dev(c, static_cast<const uint64_t*>(c->d_aux.p), n, rec_off));
         TRY(nkv_bloom_insert_records_dev(c, c->d_data.p, stream_len, rec_off, n, m, k, seed0, c->d_img.p));
     }
-    HIPTRY(hipMemcpyAsync(bits_out, c->d_img.p, nbytes, hipMemcpyDeviceToHost, c->stream));
+    HIPTRY(c->stage.download(bits_out, static_cast<const uint8_t*>(c->d_img.p), nbytes, c->stream));
     return st(hipStreamSynchronize(c->stream));
 }
 
