@@ -56,15 +56,19 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", choices=["sstable4k", "mixed"], default="sstable4k",
-                    help="sstable4k = BASELINE configs[1] (the metric); mixed = configs[2]")
+    ap.add_argument("--config", choices=["sstable4k", "mixed", "records"], default="sstable4k",
+                    help="sstable4k = BASELINE configs[1] (the metric); mixed = configs[2]; records = the "
+                         "compaction form: 1 Mi serialized 4 KiB records in a Data table, values located "
+                         "from the record headers and hashed in place")
     ap.add_argument("--mixed-bytes", type=int, default=4 << 30, help="payload of the mixed config")
-    ap.add_argument("--no-bucket", action="store_true", help="mixed: hash in input order")
+    ap.add_argument("--no-bucket", action="store_true", help="hash ragged values in input order (--bucket 0)")
+    ap.add_argument("--bucket", type=int, default=-1, help="NKV_OPT_BUCKET override (0 input order, 1 sorted, 2 auto)")
     ap.add_argument("--leaf-load", type=int, default=0, help="NKV_OPT_LEAF_LOAD override (0 = library default)")
     ap.add_argument("--deep", type=int, default=-1,
                     help="NKV_OPT_DEEP_PREFETCH override for ragged batches (-1 = library default)")
     ap.add_argument("--queue-split", type=int, default=-1, help="NKV_OPT_QUEUE_SPLIT override")
     ap.add_argument("--queue-waves", type=int, default=0, help="NKV_OPT_QUEUE_WAVES override")
+    ap.add_argument("--queue-ring", type=int, default=0, help="NKV_OPT_QUEUE_RING override (2, 3, 4)")
     ap.add_argument("--leaves", type=int, default=1 << 20)
     ap.add_argument("--value-bytes", type=int, default=4096)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -139,11 +143,35 @@ def main():
         ctx.set_option(_lib.NKV_OPT_QUEUE_SPLIT, args.queue_split)
     if args.queue_waves:
         ctx.set_option(_lib.NKV_OPT_QUEUE_WAVES, args.queue_waves)
+    if args.queue_ring:
+        ctx.set_option(_lib.NKV_OPT_QUEUE_RING, args.queue_ring)
     if args.no_bucket:
         ctx.set_option(_lib.NKV_OPT_BUCKET, 0)
+    elif args.bucket >= 0:
+        ctx.set_option(_lib.NKV_OPT_BUCKET, args.bucket)
     roots = torch.empty(world * 20, dtype=torch.uint8, device="cuda")
     mixed = args.config == "mixed"
-    if not mixed:
+    records = args.config == "records"
+    if records:
+        import numpy as np
+        n, rb = args.leaves, args.value_bytes
+        ks = 16
+        vlen = rb - 30 - ks  # record.go:191-199 header 30 B, 16-B key, the rest is the Value
+        stream_len = n * rb
+        data = torch.empty(stream_len, dtype=torch.uint8, device="cuda")
+        _lib.check(L.nkv_fill_splitmix64_dev(ctx.h, data.data_ptr(), stream_len, SEED + rank))
+        v = data.view(n, rb)
+        v[:, 14:22] = torch.from_numpy(np.frombuffer(np.uint64(ks).tobytes(), np.uint8).copy()).cuda()
+        v[:, 22:30] = torch.from_numpy(np.frombuffer(np.uint64(vlen).tobytes(), np.uint8).copy()).cuda()
+        d_roff = torch.arange(n, dtype=torch.int64, device="cuda") * rb
+        d_err = torch.zeros(1, dtype=torch.int32, device="cuda")
+        nbytes = n * vlen  # payload: the hashed Values
+        nodes = torch.empty(L.nkv_total_nodes(n) * 20, dtype=torch.uint8, device="cuda")
+
+        def tree():
+            _lib.check(L.nkv_tree_from_records_dev(ctx.h, data.data_ptr(), stream_len, d_roff.data_ptr(), n,
+                                                   nodes.data_ptr(), d_err.data_ptr()))
+    elif not mixed:
         n, vlen = args.leaves, args.value_bytes
         nbytes = n * vlen
         data = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
@@ -221,6 +249,11 @@ def main():
         if mixed:
             host = oc.splitmix64_bytes(nbytes, SEED_MIXED)
             want = oc.tree_from_digests(oc.leaf_hashes(host, off_h, lens_h, threads=16))
+        elif records:
+            host = data.cpu().numpy()
+            voff = np.arange(n, dtype=np.uint64) * rb + 30 + ks
+            want = oc.tree_from_digests(oc.leaf_hashes(host, voff, np.full(n, vlen, np.uint64), threads=16))
+            assert int(d_err.item()) == 0
         else:
             host = oc.splitmix64_bytes(nbytes, SEED)
             want = oc.tree_from_digests(oc.leaf_hashes_strided(host, vlen, vlen, n, threads=16))
@@ -228,7 +261,7 @@ def main():
         del host
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not mixed:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "sstable4k":
         cpu = cpu_baseline(min(args.cpu_sample_leaves, n), vlen)
 
     if rank == 0:
@@ -237,7 +270,7 @@ def main():
         achieved = nbytes / (leaf_ms * 1e-3) / 1e9  # algorithmic payload bytes per K1 launch
         traffic, traffic_bounds = None, None
         pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc_path) and not mixed:
+        if os.path.exists(pmc_path) and args.config == "sstable4k":
             with open(pmc_path) as f:
                 pmc = json.load(f)
             if pmc.get("leaves") == n and pmc.get("value_bytes") == vlen:
@@ -259,6 +292,9 @@ def main():
             "config": {
                 "workload": ("BASELINE configs[2]: mixed 64 B - 64 KiB log-uniform values packed back to back, "
                              + ("input order" if args.no_bucket else "length-bucketed")) if mixed else
+                            (f"compaction form: {n} serialized {rb}-B records (16-B key, {vlen}-B value) in a "
+                             "Data table in HBM; values located from the headers and hashed in place, full tree")
+                            if records else
                             "BASELINE configs[1]: single SSTable flush, 1 Mi x 4 KiB values, "
                             "leaf SHA-1 + full tree reduce (one table per GPU; roots all-gathered over RCCL when N>1)",
                 "leaves_per_gpu": n,
@@ -268,7 +304,7 @@ def main():
             "roofline": {
                 "bound": "hbm",
                 "kernel": ("leaf phase: length sort + ragged leaf SHA-1 (%s)" % LEAF_KERNEL.get(args.deep, "default"))
-                          if mixed else "k_leaf<strided,fused,aligned> (leaf SHA-1 + first 8 levels)",
+                          if (mixed or records) else "k_leaf<strided,fused,aligned> (leaf SHA-1 + first 8 levels)",
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

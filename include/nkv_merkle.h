@@ -17,7 +17,7 @@
  *   (*MerkleTree).Serialize ds/merkletree/merkletree.go:67-92   image from the calls above +
  *                           ds/merkletree/merklenode.go:37-63   nkv_write_file
  *   MakeTableSecondaries    core/sstable/sstable.go:35-47       nkv_tree_from_values /
- *     (Merkle part) + lsmtree.merge leaf collection               nkv_tree_from_records
+ *     (Merkle part) + lsmtree.merge leaf collection               nkv_tree_from_records[_dev]
  *                           core/lsmtree/lsmtree.go:146,211
  *   (*MerkleTree).Validate  ds/merkletree/merkletree.go:162-171 nkv_tree_build / nkv_tree_generic
  *                           ds/merkletree/merklenode.go:99-108    + 20-byte root compare
@@ -91,9 +91,12 @@ int nkv_ctx_sync(nkv_ctx *ctx);
 #define NKV_OPT_LEAF_LOAD 1 /* leaf-kernel load path for 16-byte aligned values:
                                1 = LDS-DMA stage, 2 = direct loads, 3 = direct non-temporal,
                                4 / 5 = direct loads in 128 / 256-byte runs per lane */
-#define NKV_OPT_BUCKET 2    /* 1 (default) = hash ragged values (nkv_tree_from_values*,
-                               nkv_tree_from_records) in length-sorted order; 0 = in
-                               input order, fused with the first tree levels */
+#define NKV_OPT_BUCKET 2    /* ragged values (nkv_tree_from_values*, nkv_tree_from_records*):
+                               1 = hash in length-sorted order (work queue); 0 = in input
+                               order, fused with the first tree levels; 2 (default) = auto:
+                               input order when the full-block counts of a batch of >= 4096
+                               values lie within max(1, min/16) of each other (one 8-byte
+                               read-back), else sorted */
 #define NKV_OPT_DEEP_PREFETCH 3 /* length-sorted ragged batches: 0 = one block of
                                    lookahead; 1 = several blocks; 2 = several blocks in a
                                    work-queue kernel that spreads the longest chains one
@@ -113,6 +116,12 @@ int nkv_ctx_sync(nkv_ctx *ctx);
                                   the NKV_HOST_THREADS environment variable) */
 #define NKV_OPT_STAGE_CHUNK 8  /* host-buffer API: bytes per pinned staging chunk (multiple of
                                   4096, default 32 MiB; three chunks are in flight) */
+#define NKV_OPT_QUEUE_RING 9   /* work-queue kernel: LDS ring of aligned chunks with 2 slots
+                                  (one block of DMA lookahead), 3 / 4 = pipelined ring
+                                  with 1 / 2 blocks of lookahead; 12 / 13 / 14 = pipelined
+                                  ring of value-relative chunks (no funnel) with 2 / 3 / 4
+                                  slots (default 13).  3 and 13 allow 3 waves per SIMD, 4
+                                  and 14 two */
 int nkv_ctx_set_option(nkv_ctx *ctx, int key, int64_t value);
 /* When enabled, the device-resident tree calls record HIP events around the
  * leaf kernel and the tree reduce on the context's stream. */
@@ -224,6 +233,14 @@ int nkv_record_offsets_dev(nkv_ctx *ctx, const uint64_t *d_rec_size, uint64_t n,
 int nkv_locate_values_dev(nkv_ctx *ctx, const void *d_stream, uint64_t stream_len,
                           const uint64_t *d_rec_off, uint64_t n, uint64_t *d_voff,
                           uint64_t *d_vlen);
+/* Merkle step of a device-resident Data table (compaction, lsmtree.go:211 /
+ * sstable.go:41-46), asynchronous: the Value of each record at d_stream +
+ * d_rec_off[i] (record.go:191-199) is located and hashed in place, and the full
+ * tree goes to d_nodes.  d_err (nullable, 4 bytes on the device) receives 1 if
+ * a header points outside the stream (that leaf hashes the empty value); with
+ * d_err NULL the call synchronizes and returns NKV_ERR_INVALID instead. */
+int nkv_tree_from_records_dev(nkv_ctx *ctx, const void *d_stream, uint64_t stream_len,
+                              const uint64_t *d_rec_off, uint64_t n, void *d_nodes, uint32_t *d_err);
 /* CRC-32/IEEE (Go crc32.ChecksumIEEE) of n byte spans d_base + d_off[i],
  * d_len[i] (any alignment) into d_crc[i] */
 int nkv_crc32_dev(nkv_ctx *ctx, const void *d_base, const uint64_t *d_off, const uint64_t *d_len,

@@ -28,6 +28,7 @@ NKV_OPT_QUEUE_WAVES = 5
 NKV_OPT_CRC_LOAD = 6
 NKV_OPT_HOST_THREADS = 7
 NKV_OPT_STAGE_CHUNK = 8
+NKV_OPT_QUEUE_RING = 9
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)
 _u64p = ctypes.POINTER(ctypes.c_uint64)
@@ -78,6 +79,7 @@ SIGNATURES = {
     "nkv_bfs_image_dev": (_int, [_vp, _vp, _u64, _vp]),
     "nkv_record_offsets_dev": (_int, [_vp, _vp, _u64, _vp]),
     "nkv_locate_values_dev": (_int, [_vp, _vp, _u64, _vp, _u64, _vp, _vp]),
+    "nkv_tree_from_records_dev": (_int, [_vp, _vp, _u64, _vp, _u64, _vp, _vp]),
     "nkv_crc32_dev": (_int, [_vp, _vp, _vp, _vp, _u64, _vp]),
     "nkv_record_crc_dev": (_int, [_vp, _vp, _u64, _vp, _u64, _vp, _vp]),
     "nkv_bloom_insert_dev": (_int, [_vp, _vp, _vp, _vp, _u64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,

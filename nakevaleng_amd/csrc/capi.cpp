@@ -98,11 +98,12 @@ struct nkv_ctx {
     hipStream_t own = nullptr;
     hipStream_t stream = nullptr;
     int leaf_load = 1;  // NKV_OPT_LEAF_LOAD
-    int bucket = 1;     // NKV_OPT_BUCKET
+    int bucket = 2;     // NKV_OPT_BUCKET
     int deep = 3;       // NKV_OPT_DEEP_PREFETCH (2, 3 = work-queue kernel)
     uint32_t simds = 1024;  // SIMDs on the device (CUs x 4)
     int queue_split = 32;   // NKV_OPT_QUEUE_SPLIT
     int queue_waves = 4;    // NKV_OPT_QUEUE_WAVES
+    int queue_ring = 13;    // NKV_OPT_QUEUE_RING
     int crc_load = 1;       // NKV_OPT_CRC_LOAD
     bool timing = false;
     bool timed = false;
@@ -110,8 +111,10 @@ struct nkv_ctx {
     // per-call event triples (leaf start, leaf end / reduce start, reduce end)
     std::vector<hipEvent_t> ring;
     size_t ring_used = 0;
-    DevBuf d_data, d_off, d_len, d_nodes, d_img, d_tmp, d_err, d_aux, d_keys, d_perm, d_stmp, d_queue, d_stats;
+    DevBuf d_data, d_off, d_len, d_nodes, d_img, d_tmp, d_err, d_aux, d_keys, d_perm, d_stmp, d_queue, d_stats,
+        d_range;
     void* h_stage = nullptr;  // small pinned staging (offsets, lengths, stats)
+    unsigned int* h_small = nullptr;  // 64 pinned bytes for device-to-host decisions
     size_t h_cap = 0;
     Stager stage;  // pipelined pinned staging of bulk bytes (host_stage.hpp)
 };
@@ -253,42 +256,98 @@ int mark(nkv_ctx* c, int which) {
     return NKV_OK;
 }
 
-// Level 0 only: the leaf kernel over the length-sorted order when bucketing
-// (ragged values), else in input order.  Not fused with tree levels.
-int leaf_level(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint64_t* len,
-               uint64_t n, bool aligned, uint8_t* nodes) {
-    const uint32_t* perm = nullptr;
-    if (c->bucket && n > 64) {
-        if (n > 0x7fffffffull) return NKV_ERR_INVALID;
-        TRY(grow(c->d_keys, 8 * n));
-        TRY(grow(c->d_perm, 8 * n));
-        uint32_t* keys = static_cast<uint32_t*>(c->d_keys.p);
-        uint32_t* pp = static_cast<uint32_t*>(c->d_perm.p);
-        size_t tb = 0;
-        HIPTRY(sort_by_length_desc(len, n, keys, pp, nullptr, &tb, c->stream));
-        TRY(grow(c->d_stmp, tb));
-        HIPTRY(sort_by_length_desc(len, n, keys, pp, c->d_stmp.p, &tb, c->stream));
-        perm = pp + n;
-        if (c->deep >= 2) {
-            TRY(grow(c->d_queue, 4 * queue_words(n)));
-            const bool ring = c->deep == 3;
-            return st(launch_leaf_queue(base, off, len, perm, n, aligned, ring,
-                                        static_cast<uint32_t*>(c->d_queue.p),
-                                        c->simds, uint32_t(ring ? c->queue_waves : 2), uint32_t(c->queue_split),
-                                        nodes, c->stream));
+// Order of a ragged batch for the leaf kernel (NKV_OPT_BUCKET): input order
+// (fused tree levels, no sort), length-sorted (work queue), or both kernels
+// launched behind a device-side Gate.  Auto mode (2) sorts batches of fewer than
+// 4096 values; for larger ones a narrow range of full-block counts
+// (max <= min + max(1, min / 16), e.g. SSTable records of one size) gains
+// nothing from sorting.  With the lengths on the host the choice is made here;
+// with device lengths only, k_len_range measures the range and the two leaf
+// kernels read it (no host read-back, so device-resident calls stay
+// asynchronous; the sort then runs either way).
+enum Plan { kInputOrder = 0, kSorted = 1, kGated = 2 };
+
+int plan_of(nkv_ctx* c, const uint64_t* len, const uint64_t* host_len, uint64_t n, int* plan, Gate* gate) {
+    *plan = (c->bucket != 0 && n > 64) ? kSorted : kInputOrder;
+    *gate = Gate{};
+    if (c->bucket != 2 || n < 4096) return NKV_OK;
+    if (host_len) {
+        uint64_t lo = ~uint64_t(0), hi = 0;
+        for (uint64_t i = 0; i < n; ++i) {
+            const uint64_t b = host_len[i] >> 6;
+            lo = std::min(lo, b);
+            hi = std::max(hi, b);
         }
+        *plan = hi <= lo + std::max<uint64_t>(1, lo / 16) ? kInputOrder : kSorted;
+        return NKV_OK;
     }
-    return st(launch_leaf_offsets(base, off, len, perm, n, 0, false, aligned, c->leaf_load, nodes,
-                                  c->stream, c->deep != 0));
+    TRY(grow(c->d_range, 8));
+    unsigned int* d = static_cast<unsigned int*>(c->d_range.p);
+    HIPTRY(launch_len_range(len, n, d, c->stream));
+    gate->range = d;
+    *plan = kGated;
+    return NKV_OK;
 }
 
-int tree_from_device_values(nkv_ctx* c, const uint8_t* base, const uint64_t* off,
-                            const uint64_t* len, uint64_t n, bool aligned, uint8_t* nodes) {
+// Level 0 in the order plan_of chose.  Gated plans also launch the input-order
+// kernel (it runs when the range is narrow), fused with levels 1..min(top, 6)
+// when narrow_top > 0.
+int leaf_level(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint64_t* len, uint64_t n,
+               bool aligned, uint8_t* nodes, int plan, Gate range, int narrow_top = 0) {
+    if (plan == kInputOrder)
+        return st(launch_leaf_offsets(base, off, len, nullptr, n, 0, false, aligned, c->leaf_load, nodes,
+                                      c->stream, c->deep != 0));
+    if (n > 0x7fffffffull) return NKV_ERR_INVALID;
+    const Gate wide{range.range, plan == kGated ? 2 : 0};
+    TRY(grow(c->d_keys, 4 * sort_hist_words(n)));
+    TRY(grow(c->d_perm, 4 * n));
+    uint32_t* perm = static_cast<uint32_t*>(c->d_perm.p);
+    HIPTRY(sort_by_length_desc(len, n, perm, static_cast<uint32_t*>(c->d_keys.p), c->stream, wide));
+    if (c->deep >= 2) {
+        TRY(grow(c->d_queue, 4 * queue_words(n)));
+        const int ring = c->deep == 3 ? c->queue_ring : 0;
+        // LDS per CU (160 KiB) holds 20 / 13 / 10 rings of 2 / 3 / 4 slots
+        const int slots = ring % 10;
+        const int max_waves = slots == 4 ? 2 : (slots == 3 ? 3 : 5);
+        const int waves = ring ? std::min(c->queue_waves, max_waves) : 2;
+        HIPTRY(launch_leaf_queue(base, off, len, perm, n, aligned, ring, static_cast<uint32_t*>(c->d_queue.p),
+                                 c->simds, uint32_t(waves), uint32_t(c->queue_split), nodes, c->stream, wide));
+    } else {
+        HIPTRY(launch_leaf_offsets(base, off, len, perm, n, 0, false, aligned, c->leaf_load, nodes, c->stream,
+                                   c->deep != 0, wide));
+    }
+    if (plan == kGated)
+        HIPTRY(launch_leaf_offsets(base, off, len, nullptr, n, narrow_top, narrow_top > 0, aligned, c->leaf_load,
+                                   nodes, c->stream, c->deep != 0, Gate{range.range, 1}));
+    return NKV_OK;
+}
+
+int leaf_level(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint64_t* len, uint64_t n,
+               bool aligned, uint8_t* nodes, const uint64_t* host_len) {
+    int plan = kInputOrder;
+    Gate g;
+    TRY(plan_of(c, len, host_len, n, &plan, &g));
+    return leaf_level(c, base, off, len, n, aligned, nodes, plan, g);
+}
+
+// host_len (nullable): the value lengths on the host, when the caller has them.
+int tree_from_device_values(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint64_t* len,
+                            uint64_t n, bool aligned, uint8_t* nodes, const uint64_t* host_len = nullptr) {
     const int top = levels_of(n) - 1;
+    int plan = kInputOrder;
+    Gate g;
+    TRY(plan_of(c, len, host_len, n, &plan, &g));
     TRY(mark(c, 0));
-    if (c->bucket && n > 64) {
+    if (plan == kGated) {
+        // sorted (wide range) or input order with fused levels (narrow), picked
+        // on the device; each reduce sequence runs for its own branch only
+        TRY(leaf_level(c, base, off, len, n, aligned, nodes, plan, g, top));
+        TRY(mark(c, 1));
+        HIPTRY(launch_reduce(nodes, n, 0, top, c->stream, Gate{g.range, 2}));
+        HIPTRY(launch_reduce(nodes, n, std::min(top, kWaveLevels), top, c->stream, Gate{g.range, 1}));
+    } else if (plan == kSorted) {
         // a permuted wave does not own a subtree: reduce everything from level 0
-        TRY(leaf_level(c, base, off, len, n, aligned, nodes));
+        TRY(leaf_level(c, base, off, len, n, aligned, nodes, plan, g));
         TRY(mark(c, 1));
         HIPTRY(launch_reduce(nodes, n, 0, top, c->stream));
     } else {
@@ -338,6 +397,7 @@ int nkv_ctx_create(int device, nkv_ctx** out) {
     c->device = device;
     int rc = st(hipSetDevice(device));
     if (rc == NKV_OK) rc = st(hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking));
+    if (rc == NKV_OK) rc = st(hipHostMalloc(reinterpret_cast<void**>(&c->h_small), 64, hipHostMallocDefault));
     for (int i = 0; i < 3 && rc == NKV_OK; ++i) rc = st(hipEventCreate(&c->ev[i]));
     if (rc != NKV_OK) {
         nkv_ctx_destroy(c);
@@ -356,9 +416,11 @@ void nkv_ctx_destroy(nkv_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (DevBuf* b : {&c->d_data, &c->d_off, &c->d_len, &c->d_nodes, &c->d_img, &c->d_tmp,
-                      &c->d_err, &c->d_aux, &c->d_keys, &c->d_perm, &c->d_stmp, &c->d_queue, &c->d_stats})
+                      &c->d_err, &c->d_aux, &c->d_keys, &c->d_perm, &c->d_stmp, &c->d_queue, &c->d_stats,
+                      &c->d_range})
         if (b->p) (void)hipFree(b->p);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
+    if (c->h_small) (void)hipHostFree(c->h_small);
     for (hipEvent_t e : c->ev)
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->ring) (void)hipEventDestroy(e);
@@ -386,7 +448,7 @@ int nkv_ctx_set_option(nkv_ctx* c, int key, int64_t value) {
             c->leaf_load = int(value);
             return NKV_OK;
         case NKV_OPT_BUCKET:
-            if (value < 0 || value > 1) return NKV_ERR_INVALID;
+            if (value < 0 || value > 2) return NKV_ERR_INVALID;
             c->bucket = int(value);
             return NKV_OK;
         case NKV_OPT_DEEP_PREFETCH:
@@ -400,6 +462,10 @@ int nkv_ctx_set_option(nkv_ctx* c, int key, int64_t value) {
         case NKV_OPT_CRC_LOAD:
             if (value < 0 || value > 5) return NKV_ERR_INVALID;
             c->crc_load = int(value);
+            return NKV_OK;
+        case NKV_OPT_QUEUE_RING:
+            if (!((value >= 2 && value <= 4) || (value >= 12 && value <= 14))) return NKV_ERR_INVALID;
+            c->queue_ring = int(value);
             return NKV_OK;
         case NKV_OPT_HOST_THREADS:
             if (value < 0 || value > 256) return NKV_ERR_INVALID;
@@ -501,7 +567,7 @@ int nkv_leaf_hash(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const ui
     TRY(grow(c->d_nodes, 20 * n));
     uint8_t* nodes = static_cast<uint8_t*>(c->d_nodes.p);
     TRY(leaf_level(c, static_cast<const uint8_t*>(c->d_data.p), static_cast<const uint64_t*>(c->d_off.p),
-                   static_cast<const uint64_t*>(c->d_len.p), n, true, nodes));
+                   static_cast<const uint64_t*>(c->d_len.p), n, true, nodes, len));
     HIPTRY(c->stage.download(out20, nodes, 20 * n, c->stream));
     return st(hipStreamSynchronize(c->stream));
 }
@@ -528,7 +594,7 @@ int nkv_tree_from_values(nkv_ctx* c, const uint8_t* base, const uint64_t* off, c
     uint8_t* nodes = static_cast<uint8_t*>(c->d_nodes.p);
     TRY(tree_from_device_values(c, static_cast<const uint8_t*>(c->d_data.p),
                                 static_cast<const uint64_t*>(c->d_off.p),
-                                static_cast<const uint64_t*>(c->d_len.p), n, true, nodes));
+                                static_cast<const uint64_t*>(c->d_len.p), n, true, nodes, len));
     return finish_tree(c, nodes, n, root20, nodes_out, img_out);
 }
 
@@ -573,7 +639,7 @@ int nkv_tree_generic(nkv_ctx* c, const uint8_t* data, const uint64_t* off, const
     TRY(grow(c->d_nodes, 20 * up_total));
     uint8_t* up = static_cast<uint8_t*>(c->d_nodes.p);
     TRY(leaf_level(c, static_cast<const uint8_t*>(c->d_data.p), static_cast<const uint64_t*>(c->d_off.p),
-                   static_cast<const uint64_t*>(c->d_len.p), n1, true, up));
+                   static_cast<const uint64_t*>(c->d_len.p), n1, true, up, mlen.data()));
     if (n1 > 1) HIPTRY(launch_reduce(up, n1, 0, levels_of(n1) - 1, c->stream));
     if (upper_out) HIPTRY(c->stage.download(upper_out, up, 20 * up_total, c->stream));
     if (root20)
@@ -748,7 +814,7 @@ int nkv_leaf_hash_dev(nkv_ctx* c, const void* d_base, const uint64_t* d_off,
     if (n == 0) return NKV_OK;
     if (!d_base || !d_off || !d_len || !d_nodes) return NKV_ERR_INVALID;
     return leaf_level(c, static_cast<const uint8_t*>(d_base), d_off, d_len, n, false,
-                      static_cast<uint8_t*>(d_nodes));
+                      static_cast<uint8_t*>(d_nodes), nullptr);
 }
 
 int nkv_leaf_hash_strided_dev(nkv_ctx* c, const void* d_base, uint64_t stride, uint64_t len,
@@ -822,6 +888,32 @@ int nkv_locate_values_dev(nkv_ctx* c, const void* d_stream, uint64_t stream_len,
     HIPTRY(hipMemsetAsync(err, 0, 4, c->stream));
     HIPTRY(launch_locate(static_cast<const uint8_t*>(d_stream), stream_len, d_rec_off, n, d_voff,
                          d_vlen, err, c->stream));
+    unsigned int h = 0;
+    HIPTRY(hipMemcpyAsync(&h, err, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPTRY(hipStreamSynchronize(c->stream));
+    return h ? NKV_ERR_INVALID : NKV_OK;
+}
+
+int nkv_tree_from_records_dev(nkv_ctx* c, const void* d_stream, uint64_t stream_len, const uint64_t* d_rec_off,
+                              uint64_t n, void* d_nodes, uint32_t* d_err) {
+    TRY(bind(c));
+    if (n == 0) return NKV_ERR_EMPTY;
+    if (!d_stream || !d_rec_off || !d_nodes) return NKV_ERR_INVALID;
+    TRY(grow(c->d_off, 8 * n));
+    TRY(grow(c->d_len, 8 * n));
+    unsigned int* err = reinterpret_cast<unsigned int*>(d_err);
+    if (!err) {
+        TRY(grow(c->d_err, 4));
+        err = static_cast<unsigned int*>(c->d_err.p);
+    }
+    uint64_t* voff = static_cast<uint64_t*>(c->d_off.p);
+    uint64_t* vlen = static_cast<uint64_t*>(c->d_len.p);
+    HIPTRY(hipMemsetAsync(err, 0, 4, c->stream));
+    HIPTRY(launch_locate(static_cast<const uint8_t*>(d_stream), stream_len, d_rec_off, n, voff, vlen, err,
+                         c->stream));
+    TRY(tree_from_device_values(c, static_cast<const uint8_t*>(d_stream), voff, vlen, n, false,
+                                static_cast<uint8_t*>(d_nodes)));
+    if (d_err) return NKV_OK;
     unsigned int h = 0;
     HIPTRY(hipMemcpyAsync(&h, err, 4, hipMemcpyDeviceToHost, c->stream));
     HIPTRY(hipStreamSynchronize(c->stream));

@@ -14,6 +14,21 @@ constexpr int kMaxLevels = 64;
 #endif
 constexpr int kLeafWavesPerSimd = NKV_LEAF_WAVES;  // 8 waves/SIMD <=> <= 64 VGPRs
 
+// Device-side choice between two leaf kernels launched back to back (no host
+// read-back): range = the batch's (min, max) full-block counts from
+// launch_len_range; pol 1 runs the kernel only for a narrow range (input
+// order), pol 2 only for a wide one (length-sorted work queue), 0 always.
+struct Gate {
+    const unsigned int* range = nullptr;
+    int pol = 0;
+    __device__ __forceinline__ bool open() const {
+        if (pol == 0) return true;
+        const unsigned int lo = range[0], hi = range[1];
+        const bool narrow = hi <= lo + (lo / 16 > 1u ? lo / 16 : 1u);
+        return narrow == (pol == 1);
+    }
+};
+
 // BFS image layout in image order (index 0 = top level).
 struct BfsLayout {
     int nlev;
@@ -23,23 +38,27 @@ struct BfsLayout {
     uint64_t count[kMaxLevels];       // real nodes in the level
 };
 
-// load: leaf-kernel load path for aligned values (1 LDS-DMA, 2 direct, 3 direct
-// non-temporal); unaligned values always take the register funnel (0).
+// load: leaf-kernel load path (1 LDS-DMA, 2 direct, 3 direct non-temporal, 4 / 5
+// direct 128 / 256-B runs); direct loads need 16-byte aligned values, so
+// unaligned batches take LDS-DMA from the values' own addresses (8) for load 1
+// and the register funnel (0) otherwise.
 hipError_t launch_leaf_strided(const uint8_t* base, uint64_t stride, uint64_t L, uint64_t n,
                                int top, bool fuse, int load, uint8_t* nodes, hipStream_t s);
 hipError_t launch_leaf_offsets(const uint8_t* base, const uint64_t* off, const uint64_t* len,
                                const uint32_t* perm, uint64_t n, int top, bool fuse, bool aligned,
-                               int load, uint8_t* nodes, hipStream_t s, bool deep = true);
+                               int load, uint8_t* nodes, hipStream_t s, bool deep = true, Gate gate = Gate{});
 // Ragged batch through the work-queue leaf kernel (perm = length-sorted order,
 // longest first); q must hold queue_words(n) u32; split = longest chain (full
 // blocks) of a group the non-priority waves take when the longest chain bounds
-// the batch.
+// the batch.  ring: 0 = register prefetch, 2 = LDS chunk ring, 3 / 4 = pipelined
+// ring of 3 / 4 slots, 12 / 13 / 14 = pipelined ring of value-relative chunks
+// with 2 / 3 / 4 slots.
 uint64_t queue_words(uint64_t n);
 hipError_t launch_leaf_queue(const uint8_t* base, const uint64_t* off, const uint64_t* len,
-                             const uint32_t* perm, uint64_t n, bool aligned, bool ring, uint32_t* q,
+                             const uint32_t* perm, uint64_t n, bool aligned, int ring, uint32_t* q,
                              uint32_t simds, uint32_t waves_per_simd, uint32_t split, uint8_t* nodes,
-                             hipStream_t s);
-hipError_t launch_reduce(uint8_t* nodes, uint64_t n, int from_level, int top, hipStream_t s);
+                             hipStream_t s, Gate gate = Gate{});
+hipError_t launch_reduce(uint8_t* nodes, uint64_t n, int from_level, int top, hipStream_t s, Gate gate = Gate{});
 hipError_t launch_bfs_image(const uint8_t* nodes, const BfsLayout& lay, uint8_t* img,
                             hipStream_t s);
 hipError_t launch_locate(const uint8_t* stream, uint64_t stream_len, const uint64_t* rec_off,
@@ -47,9 +66,11 @@ hipError_t launch_locate(const uint8_t* stream, uint64_t stream_len, const uint6
                          hipStream_t s);
 hipError_t scan_exclusive_u64(const uint64_t* in, uint64_t* out, uint64_t n, void* tmp,
                               size_t* tmp_bytes, hipStream_t s);
-// Two-phase (tmp == nullptr: size query).  The permutation lands in perm + n.
-hipError_t sort_by_length_desc(const uint64_t* len, uint64_t n, uint32_t* keys, uint32_t* perm,
-                               void* tmp, size_t* tmp_bytes, hipStream_t s);
+// Length-sorted order (compression count, longest first) into perm[0..n);
+// hist: sort_hist_words(n) u32 of scratch.
+uint64_t sort_hist_words(uint64_t n);
+hipError_t sort_by_length_desc(const uint64_t* len, uint64_t n, uint32_t* perm, uint32_t* hist, hipStream_t s,
+                               Gate gate = Gate{});
 // crc.hip: CRC-32/IEEE of byte spans / of records' Key ++ Value (stats: 3 x u64,
 // initialised by the launcher).
 // variant: NKV_OPT_CRC_LOAD (bit 0 LDS chunk ring; bits 1-2 table copies x
@@ -64,5 +85,7 @@ hipError_t launch_bloom(int mode, bool query, const uint8_t* base, const uint64_
                         uint64_t stream_len, uint64_t n, uint32_t m, uint32_t k, uint32_t seed0, uint32_t* bits,
                         uint8_t* out, unsigned int* err, hipStream_t s);
 hipError_t launch_fill(uint8_t* buf, uint64_t nbytes, uint64_t seed, hipStream_t s);
+// out[0] / out[1] = min / max of len[i] / 64 over the batch (2 u32 on the device)
+hipError_t launch_len_range(const uint64_t* len, uint64_t n, unsigned int* out, hipStream_t s);
 
 }  // namespace nkv

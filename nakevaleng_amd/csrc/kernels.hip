@@ -41,6 +41,13 @@ __device__ unsigned long long* g_diag = nullptr;
     } while (0)
 #endif
 
+// SHA-1 compressions of a len-byte message (FIPS 180-4 padding: + 0x80 + 8 B)
+__device__ __forceinline__ uint64_t compressions(uint64_t len) { return (len + 8) / 64 + 1; }
+
+constexpr uint32_t kLenBuckets = 640;  // counting-sort buckets (len_bucket_desc)
+constexpr int kSortItems = 16;         // values per thread of a sort tile
+constexpr uint64_t kSortTile = uint64_t(kBlock) * kSortItems;
+
 // ---------------------------------------------------------------------------
 // tree shape helpers (device side; host side mirrors them in capi.cpp)
 
@@ -497,19 +504,203 @@ __device__ __forceinline__ void sha1_blocks_ring(uint8_t* wbuf, const uint8_t* p
     }
 }
 
+// Source of the DMA lanes whose value has no chunk c: every ring issue then
+// moves exactly four wave-instructions, so vmcnt counts are static.
+__device__ __attribute__((aligned(64))) uint8_t g_ring_dummy[64];
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ u32x4 ds_read_b128_asm(uint32_t addr) {
+    u32x4 v;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr) : "memory");
+    return v;
+}
+
+// The ring above with R >= 3 slots and explicit waits, software-pipelined:
+// while block b is compressed, the DMA of chunk b+R and the LDS reads of window
+// b+1 are in flight, and chunk b+2 (read for window b+1) was issued R-2
+// blocks earlier.  The compiler's own waits would be vmcnt(0) before every LDS
+// read (it cannot tell ring slots apart), so the window reads are inline asm
+// and the waits are explicit:
+//   - vmcnt(4 (R-2)) before reading window b+1: chunks b+1, b+2 landed, the
+//     R-2 younger chunks (b+3 .. b+R, four wave-instructions each) may fly;
+//   - lgkmcnt(0) after block b's compression, carried through window b+1's
+//     registers (in/out asm operands, so no copy of them is scheduled before
+//     the wait), which also frees chunk b+1's slot for the next issue.
+// Every issue moves four wave-instructions (lanes past their value read
+// g_ring_dummy), and the ring drains (vmcnt(0)) before the slots are reused.
+template <int R>
+__device__ __forceinline__ void sha1_blocks_ring_pipe(uint8_t* wbuf, const uint8_t* p, uint32_t my_nfull,
+                                                      uint32_t h[5]) {
+    static_assert(R >= 3 && R <= 4, "ring depth");
+    const int lane = threadIdx.x & 63;
+    const uint32_t o = uint32_t(reinterpret_cast<uintptr_t>(p)) & 63u;
+    const uint32_t nch = my_nfull ? my_nfull + (o != 0u) : 0u;
+    const uint32_t dq = (uint32_t(lane) & 3u) ^ ((uint32_t(lane) >> 4) & 3u);
+    const uint8_t* src[4];
+    uint32_t nc[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int j = 16 * k + (lane >> 2);
+        const uint64_t aj = uint64_t(__shfl(int64_t(reinterpret_cast<uintptr_t>(p - o)), j));
+        src[k] = reinterpret_cast<const uint8_t*>(aj) + 16 * dq;
+        nc[k] = uint32_t(__shfl(int(nch), j));
+    }
+    const uint32_t nmax = wave_max_u32(my_nfull);
+    if (nmax == 0) return;
+    const uint8_t* dummy = g_ring_dummy + 16 * dq;
+    auto issue = [&](uint32_t c) {
+        uint8_t* dst = wbuf + 4096 * (c % R);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            __builtin_amdgcn_global_load_lds(c < nc[k] ? src[k] + 64ull * c : dummy, dst + 1024 * k, 16, 0, 0);
+    };
+    const uint32_t lds0 = uint32_t(reinterpret_cast<uintptr_t>(wbuf));
+    const uint32_t swz = (uint32_t(lane) >> 2) & 3u;
+    // quad i of window b: chunk b + (qi >> 2), quad (qi & 3) ^ swz of this lane's row
+    uint32_t qoff[5], qch[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        const uint32_t qi = (o >> 4) + uint32_t(i);
+        qch[i] = qi >> 2;
+        qoff[i] = 64u * uint32_t(lane) + 16u * ((qi & 3u) ^ swz);
+    }
+    // chunk b's slot is uniform; a lane's quads from chunk b+1 add the (uniform)
+    // distance to the next slot
+    auto read_window = [&](uint32_t b, u32x4 v[5]) {
+        const uint32_t s0 = lds0 + 4096u * (b % R);
+        const uint32_t s1 = lds0 + 4096u * ((b + 1) % R);
+#pragma unroll
+        for (int i = 0; i < 5; ++i) v[i] = ds_read_b128_asm(qoff[i] + (qch[i] ? s1 : s0));
+    };
+    const uint32_t s = o & 15u;
+#pragma unroll
+    for (uint32_t c = 0; c < uint32_t(R); ++c) issue(c);
+    if (R == 3) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    // The lgkmcnt wait names the ds_read destinations as in/out operands, so
+    // no copy or use of them can be scheduled before it.
+    u32x4 cur[5];
+    read_window(0u, cur);
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(cur[0]), "+v"(cur[1]), "+v"(cur[2]), "+v"(cur[3]), "+v"(cur[4])
+                 :
+                 : "memory");
+    for (uint32_t b = 0; b < nmax; ++b) {
+        issue(b + R);
+        if (R == 3) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        u32x4 nxt[5];
+        read_window(b + 1, nxt);
+        uint32_t d[20];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            d[4 * i] = cur[i].x;
+            d[4 * i + 1] = cur[i].y;
+            d[4 * i + 2] = cur[i].z;
+            d[4 * i + 3] = cur[i].w;
+        }
+        uint32_t w[16];
+        be16_funnel(d, s, w);
+        if (b < my_nfull) sha1_compress(h, w);
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(nxt[0]), "+v"(nxt[1]), "+v"(nxt[2]), "+v"(nxt[3]), "+v"(nxt[4])
+                     :
+                     : "memory");
+#pragma unroll
+        for (int i = 0; i < 5; ++i) cur[i] = nxt[i];
+    }
+    // every DMA must land before the slots are reused
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// Pipelined ring over VALUE-relative chunks: chunk c of a value is its bytes
+// [64c, 64c + 64), fetched by LDS-DMA from the value's own (unaligned) address,
+// so the LDS row already holds block c and no funnel is needed (16 v_perm
+// byte swaps per block instead of 52).  Only full blocks are fetched, so every
+// byte read belongs to the value.  A lane past its value's last block re-reads
+// that block (a value with none reads g_ring_dummy), so each issue is four
+// wave-instructions.  Window b = chunk b; at block b the ring holds chunks
+// b+1 .. b+R, and vmcnt(4 (R-1)) before reading window b+1 lets chunks
+// b+2 .. b+R fly (R-1 blocks of lookahead).
+template <int R>
+__device__ __forceinline__ void sha1_blocks_ring_vc(uint8_t* wbuf, const uint8_t* p, uint32_t my_nfull,
+                                                    uint32_t h[5]) {
+    static_assert(R >= 2 && R <= 4, "ring depth");
+    const int lane = threadIdx.x & 63;
+    const uint32_t dq = (uint32_t(lane) & 3u) ^ ((uint32_t(lane) >> 4) & 3u);
+    const uint8_t* src[4];
+    uint32_t lastc[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int j = 16 * k + (lane >> 2);
+        const uint64_t aj = uint64_t(__shfl(int64_t(reinterpret_cast<uintptr_t>(p)), j));
+        const uint32_t nj = uint32_t(__shfl(int(my_nfull), j));
+        src[k] = (nj ? reinterpret_cast<const uint8_t*>(aj) : g_ring_dummy) + 16 * dq;
+        lastc[k] = nj ? nj - 1 : 0u;
+    }
+    const uint32_t nmax = wave_max_u32(my_nfull);
+    if (nmax == 0) return;
+    auto issue = [&](uint32_t c) {
+        uint8_t* dst = wbuf + 4096 * (c % R);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            __builtin_amdgcn_global_load_lds(src[k] + 64ull * min(c, lastc[k]), dst + 1024 * k, 16, 0, 0);
+    };
+    const uint32_t lds0 = uint32_t(reinterpret_cast<uintptr_t>(wbuf));
+    const uint32_t row = lds0 + 64u * uint32_t(lane);
+    const uint32_t swz = (uint32_t(lane) >> 2) & 3u;
+    auto read_window = [&](uint32_t b, u32x4 v[4]) {
+        const uint32_t s0 = row + 4096u * (b % R);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = ds_read_b128_asm(s0 + 16u * (uint32_t(q) ^ swz));
+    };
+#pragma unroll
+    for (uint32_t c = 0; c < uint32_t(R); ++c) issue(c);
+    wait_vmcnt<4 * (R - 1)>();
+    u32x4 cur[4];
+    read_window(0u, cur);
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(cur[0]), "+v"(cur[1]), "+v"(cur[2]), "+v"(cur[3]) : : "memory");
+    for (uint32_t b = 0; b < nmax; ++b) {
+        issue(b + R);
+        wait_vmcnt<4 * (R - 1)>();
+        u32x4 nxt[4];
+        read_window(b + 1, nxt);
+        uint4 c4[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) c4[q] = make_uint4(cur[q].x, cur[q].y, cur[q].z, cur[q].w);
+        uint32_t w[16];
+        be16_from_raw(c4, w);
+        if (b < my_nfull) sha1_compress(h, w);
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(nxt[0]), "+v"(nxt[1]), "+v"(nxt[2]), "+v"(nxt[3]) : : "memory");
+#pragma unroll
+        for (int q = 0; q < 4; ++q) cur[q] = nxt[q];
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // MODE 0: value i at base + i*stride, length L.  MODE 1: base + off[i], len[i].
 // perm (MODE 1 only, nullable): lane i hashes leaf perm[i] (length bucketing).
 // FUSE: also build levels 1..min(8, top) of this block's subtree.
 // LOAD: 0 = any alignment (register funnel); 1 = 16-byte aligned, LDS-DMA
 // stage; 2 = aligned, direct loads; 3 = aligned, direct non-temporal loads.
 template <int MODE, bool FUSE, int LOAD>
-__global__ __launch_bounds__(kBlock, LOAD >= 6 ? 2 : (LOAD >= 4 ? 4 : kLeafWavesPerSimd)) void k_leaf(const uint8_t* __restrict__ base,
+__global__ __launch_bounds__(kBlock, (LOAD == 6 || LOAD == 7) ? 2 : ((LOAD == 4 || LOAD == 5) ? 4 : kLeafWavesPerSimd)) void k_leaf(const uint8_t* __restrict__ base,
                                                   const uint64_t* __restrict__ off,
                                                   const uint64_t* __restrict__ len, uint64_t stride,
                                                   uint64_t L, const uint32_t* __restrict__ perm,
-                                                  uint64_t n, int top, uint8_t* __restrict__ nodes) {
+                                                  uint64_t n, int top, uint8_t* __restrict__ nodes, Gate gate) {
     // 16 KiB: four wave-private 4 KiB LDS-DMA stages (LOAD == 1)
     __shared__ __attribute__((aligned(16))) uint8_t smem[kBlock * 64];
+    if (!gate.open()) return;
     NKV_STAMP(0);
     const uint64_t g = blockIdx.x;
     const uint64_t t = g * kBlock + threadIdx.x;
@@ -528,7 +719,7 @@ __global__ __launch_bounds__(kBlock, LOAD >= 6 ? 2 : (LOAD >= 4 ? 4 : kLeafWaves
             ln = len[leaf];
         }
     }
-    if (LOAD >= 2) {
+    if (LOAD >= 2 && LOAD <= 7) {
         sha1_init(h);
         if (live) {
             if (LOAD == 2) sha1_blocks_direct<false>(p, uint32_t(ln >> 6), h);
@@ -541,8 +732,11 @@ __global__ __launch_bounds__(kBlock, LOAD >= 6 ? 2 : (LOAD >= 4 ? 4 : kLeafWaves
             else sha1_tail<true>(p, ln, h);
             store_digest(nodes, leaf, h);
         }
-    } else if (LOAD == 1) {
-        // wave-cooperative LDS-DMA stream of the full blocks, then the tail
+    } else if (LOAD == 1 || LOAD == 8) {
+        // wave-cooperative LDS-DMA stream of the full blocks, then the tail.
+        // The DMA reads each value's own blocks at the value's address, so it
+        // serves any alignment (LOAD 8: unaligned values, unaligned tail); only
+        // full blocks are fetched, so every byte read belongs to the value.
         const int lane = threadIdx.x & 63;
         const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
         uint8_t* wbuf = smem + 4096 * wave;
@@ -585,7 +779,7 @@ __global__ __launch_bounds__(kBlock, LOAD >= 6 ? 2 : (LOAD >= 4 ? 4 : kLeafWaves
             sha1_blocks_lds(wbuf, wave_max_u32(my_nfull), my_nfull, issue, h);
         }
         if (live) {
-            sha1_tail<true>(p, ln, h);
+            sha1_tail<LOAD == 1>(p, ln, h);
             store_digest(nodes, leaf, h);
         }
     } else if (live) {
@@ -630,15 +824,24 @@ __global__ __launch_bounds__(kBlock, LOAD >= 6 ? 2 : (LOAD >= 4 ? 4 : kLeafWaves
 //    [4, 4 + kSimdKeys) per-SIMD arrivals, then ngroups claim flags; zeroed
 //    before the launch.
 constexpr uint32_t kSimdKeys = 8 * 8 * 2 * 16 * 4;  // xcc, se, sh, cu, simd
+constexpr uint32_t kQueueHeader = 8;  // tickets, first short group, pad, work (u64), pad
 
+// LOAD 6 / 7: deep register prefetch (aligned / any alignment); 8: LDS chunk
+// ring, 2 slots; 9 / 10: pipelined LDS ring, 3 / 4 slots (12 / 16 KiB per wave);
+// 11 / 12 / 13: pipelined ring of value-relative chunks, 2 / 3 / 4 slots.
 template <int LOAD>
-__global__ __launch_bounds__(64, LOAD == 8 ? 4 : 2) void k_leaf_queue(const uint8_t* __restrict__ base,
+constexpr int queue_ring_slots() {
+    return LOAD == 8 || LOAD == 11 ? 2 : (LOAD == 9 || LOAD == 12 ? 3 : (LOAD == 10 || LOAD == 13 ? 4 : 0));
+}
+template <int LOAD>
+__global__ __launch_bounds__(64, queue_ring_slots<LOAD>() == 4 ? 2 : (queue_ring_slots<LOAD>() == 3 ? 3 : (queue_ring_slots<LOAD>() == 2 ? 4 : 2))) void k_leaf_queue(const uint8_t* __restrict__ base,
                                                        const uint64_t* __restrict__ off,
                                                        const uint64_t* __restrict__ len,
                                                        const uint32_t* __restrict__ perm, uint64_t n,
-                                                       uint32_t ngroups, uint32_t* __restrict__ q,
-                                                       uint8_t* __restrict__ nodes) {
-    __shared__ __attribute__((aligned(16))) uint8_t smem[LOAD == 8 ? 8192 : 16];
+                                                       uint32_t ngroups, uint32_t simds, uint32_t* __restrict__ q,
+                                                       uint8_t* __restrict__ nodes, Gate gate) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[queue_ring_slots<LOAD>() ? 4096 * queue_ring_slots<LOAD>() : 16];
+    if (!gate.open()) return;
     const int lane = threadIdx.x;
     uint32_t hw, xcc;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
@@ -646,12 +849,19 @@ __global__ __launch_bounds__(64, LOAD == 8 ? 4 : 2) void k_leaf_queue(const uint
     const uint32_t key = ((((xcc & 7) * 8 + ((hw >> 13) & 7)) * 2 + ((hw >> 12) & 1)) * 16 + ((hw >> 8) & 15)) * 4 +
                          ((hw >> 4) & 3);
     uint32_t slot = 0;
-    if (lane == 0) slot = atomicAdd(q + 4 + key, 1u);
+    if (lane == 0) slot = atomicAdd(q + kQueueHeader + key, 1u);
     slot = __builtin_amdgcn_readfirstlane(slot);
     const bool front = slot == 0;
     if (front) __builtin_amdgcn_s_setprio(3);
-    const uint32_t first_short = __builtin_amdgcn_readfirstlane(q[2]);
-    uint32_t* claimed = q + 4 + kSimdKeys;
+    // k_queue_split's partials: the first group short enough for the
+    // non-priority waves, and the batch's work; a throughput-bound batch (work
+    // at least twice what the longest chain keeps every SIMD busy for) lets
+    // every wave take any group
+    const uint64_t work = reinterpret_cast<const unsigned long long*>(q)[2];
+    const uint64_t longest = compressions(len[perm[0]]);
+    const uint32_t first_short = __builtin_amdgcn_readfirstlane(
+        work >= 2ull * simds * longest ? 0u : min(q[2], ngroups));
+    uint32_t* claimed = q + kQueueHeader + kSimdKeys;
 #ifdef NKV_DIAG
     uint64_t d_t0 = __builtin_amdgcn_s_memrealtime(), d_c0 = __builtin_amdgcn_s_memtime(), d_first = 0;
     uint64_t d_groups = 0, d_blocks = 0;
@@ -668,14 +878,16 @@ __global__ __launch_bounds__(64, LOAD == 8 ? 4 : 2) void k_leaf_queue(const uint
         g = __builtin_amdgcn_readfirstlane(g);
         if (g == 0xFFFFFFFFu) break;
         const uint64_t i = uint64_t(g) * 64 + lane;
-        if (LOAD == 8) {
+        if constexpr (LOAD >= 8) {
             const bool live = i < n;
             const uint64_t leaf = live ? perm[i] : 0;
             const uint8_t* p = live ? base + off[leaf] : base;
             const uint64_t ln = live ? len[leaf] : 0;
             uint32_t h[5];
             sha1_init(h);
-            sha1_blocks_ring(smem, p, uint32_t(ln >> 6), h);
+            if constexpr (LOAD == 8) sha1_blocks_ring(smem, p, uint32_t(ln >> 6), h);
+            else if constexpr (LOAD <= 10) sha1_blocks_ring_pipe<queue_ring_slots<LOAD>()>(smem, p, uint32_t(ln >> 6), h);
+            else sha1_blocks_ring_vc<queue_ring_slots<LOAD>()>(smem, p, uint32_t(ln >> 6), h);
             if (live) {
                 sha1_tail<false>(p, ln, h);
                 store_digest(nodes, leaf, h);
@@ -713,8 +925,9 @@ __global__ __launch_bounds__(64, LOAD == 8 ? 4 : 2) void k_leaf_queue(const uint
 
 // K2: reduce one level j0 (already in nodes) up to min(j0 + 8, top).
 __global__ __launch_bounds__(kBlock) void k_reduce(uint8_t* __restrict__ nodes, uint64_t n, int j0,
-                                                    int jmax) {
+                                                    int jmax, Gate gate) {
     __shared__ uint32_t lds[5][kBlock];
+    if (!gate.open()) return;
     const uint64_t lo = uint64_t(blockIdx.x) * kBlock;
     const uint64_t cnt = lvl_count(n, j0);
     const uint64_t idx = lo + threadIdx.x;
@@ -729,17 +942,76 @@ __global__ __launch_bounds__(kBlock) void k_reduce(uint8_t* __restrict__ nodes, 
 // Length bucketing for ragged values: one lane per value means a wavefront
 // runs for its longest value, so values are ordered by compression count,
 // longest first (longest-processing-time order for the dispatcher), and the
-// leaf kernel reads them through the permutation.
-__global__ __launch_bounds__(kBlock) void k_bucket_keys(const uint64_t* __restrict__ len, uint64_t n,
-                                                         uint32_t* __restrict__ keys,
-                                                         uint32_t* __restrict__ idx) {
-    const uint64_t t = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
-    if (t >= n) return;
-    // SHA-1 compressions of the value, clamped to 16 bits (values past 4 MiB
-    // sort as equals): a 16-bit radix sort is half the passes of a 32-bit one
-    const uint64_t blocks = (len[t] + 8) / 64 + 1;
-    keys[t] = blocks > 0xFFFFull ? 0xFFFFu : uint32_t(blocks);
-    idx[t] = uint32_t(t);
+// leaf kernel reads them through the permutation.  A counting sort over 640
+// buckets (exact below 256 compressions, 16 buckets per octave above, so a
+// bucket spans at most 1/16 of its length) in three gated kernels: per-tile
+// histograms, one column scan, a scatter.  Order inside a bucket is arbitrary
+// (digests are written by leaf index, so results do not depend on it).
+__device__ __forceinline__ uint32_t len_bucket_desc(uint64_t len) {
+    const uint64_t c64 = compressions(len);
+    const uint32_t c = c64 > 0xFFFFFFFFull ? 0xFFFFFFFFu : uint32_t(c64);
+    uint32_t k = c;
+    if (c >= 256) {
+        const uint32_t e = 31u - uint32_t(__clz(c));
+        k = 256u + (e - 8u) * 16u + ((c >> (e - 4u)) & 15u);
+    }
+    return kLenBuckets - 1u - k;
+}
+
+__global__ __launch_bounds__(kBlock) void k_len_hist(const uint64_t* __restrict__ len, uint64_t n,
+                                                      uint32_t* __restrict__ hist, Gate gate) {
+    __shared__ uint32_t h[kLenBuckets];
+    if (!gate.open()) return;
+    for (uint32_t i = threadIdx.x; i < kLenBuckets; i += kBlock) h[i] = 0u;
+    __syncthreads();
+    const uint64_t base = uint64_t(blockIdx.x) * kSortTile;
+#pragma unroll 4
+    for (int j = 0; j < kSortItems; ++j) {
+        const uint64_t i = base + uint64_t(j) * kBlock + threadIdx.x;
+        if (i < n) atomicAdd(&h[len_bucket_desc(len[i])], 1u);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < kLenBuckets; i += kBlock) hist[uint64_t(blockIdx.x) * kLenBuckets + i] = h[i];
+}
+
+// hist[t][k] -> first output position of tile t's bucket-k values
+__global__ __launch_bounds__(1024) void k_len_scan(uint32_t* __restrict__ hist, uint32_t tiles, Gate gate) {
+    __shared__ uint32_t tot[1024];
+    if (!gate.open()) return;
+    const uint32_t k = threadIdx.x;
+    uint32_t sum = 0;
+    if (k < kLenBuckets)
+        for (uint32_t t = 0; t < tiles; ++t) {
+            const uint32_t v = hist[uint64_t(t) * kLenBuckets + k];
+            hist[uint64_t(t) * kLenBuckets + k] = sum;
+            sum += v;
+        }
+    tot[k] = sum;
+    __syncthreads();
+    for (uint32_t o = 1; o < 1024; o <<= 1) {  // inclusive scan of the bucket totals
+        const uint32_t v = k >= o ? tot[k - o] : 0u;
+        __syncthreads();
+        tot[k] += v;
+        __syncthreads();
+    }
+    const uint32_t base = tot[k] - sum;
+    if (k < kLenBuckets && base)
+        for (uint32_t t = 0; t < tiles; ++t) hist[uint64_t(t) * kLenBuckets + k] += base;
+}
+
+__global__ __launch_bounds__(kBlock) void k_len_scatter(const uint64_t* __restrict__ len, uint64_t n,
+                                                         const uint32_t* __restrict__ hist,
+                                                         uint32_t* __restrict__ perm, Gate gate) {
+    __shared__ uint32_t cur[kLenBuckets];
+    if (!gate.open()) return;
+    for (uint32_t i = threadIdx.x; i < kLenBuckets; i += kBlock) cur[i] = hist[uint64_t(blockIdx.x) * kLenBuckets + i];
+    __syncthreads();
+    const uint64_t base = uint64_t(blockIdx.x) * kSortTile;
+#pragma unroll 4
+    for (int j = 0; j < kSortItems; ++j) {
+        const uint64_t i = base + uint64_t(j) * kBlock + threadIdx.x;
+        if (i < n) perm[atomicAdd(&cur[len_bucket_desc(len[i])], 1u)] = uint32_t(i);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -814,6 +1086,48 @@ __global__ __launch_bounds__(kBlock) void k_locate(const uint8_t* __restrict__ s
     vlen[i] = l;
 }
 
+// Range of full-block counts of a batch: out[0] = min, out[1] = max (the
+// launcher initialises them).  Lets the host choose input order (narrow
+// range: no sort, fused tree levels) or the length-sorted work queue.
+__global__ __launch_bounds__(kBlock) void k_len_range(const uint64_t* __restrict__ len, uint64_t n,
+                                                       unsigned int* __restrict__ out) {
+    __shared__ unsigned int part[2][kBlock / 64];
+    unsigned int lo = 0xFFFFFFFFu, hi = 0u;
+    for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += uint64_t(gridDim.x) * kBlock) {
+        const uint64_t b = len[i] >> 6;
+        const unsigned int bb = b > 0xFFFFFFFFull ? 0xFFFFFFFFu : unsigned(b);
+        lo = min(lo, bb);
+        hi = max(hi, bb);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        lo = min(lo, unsigned(__shfl_xor(int(lo), o)));
+        hi = max(hi, unsigned(__shfl_xor(int(hi), o)));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        part[0][threadIdx.x >> 6] = lo;
+        part[1][threadIdx.x >> 6] = hi;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {  // one atomic pair per block: same-address atomics serialise
+        for (int w = 1; w < kBlock / 64; ++w) {
+            lo = min(lo, part[0][w]);
+            hi = max(hi, part[1][w]);
+        }
+        atomicMin(out, lo);
+        atomicMax(out + 1, hi);
+    }
+}
+
+hipError_t launch_len_range(const uint64_t* len, uint64_t n, unsigned int* out, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(out, 0xFF, 4, s);
+    if (e == hipSuccess) e = hipMemsetAsync(out + 1, 0, 4, s);
+    if (e != hipSuccess) return e;
+    const uint64_t blocks = std::min<uint64_t>((n + kBlock - 1) / kBlock, 256);
+    hipLaunchKernelGGL(k_len_range, dim3(uint32_t(blocks)), dim3(kBlock), 0, s, len, n, out);
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------
 // synthetic input: byte j = byte (j % 8) of splitmix64(seed, j / 8), LE.
 __device__ __forceinline__ uint64_t splitmix64_at(uint64_t seed, uint64_t k) {
@@ -848,63 +1162,61 @@ static inline unsigned grid_for(uint64_t n) { return unsigned((n + kBlock - 1) /
 template <int MODE, bool FUSE, int LOAD>
 static void leaf_kernel(const uint8_t* base, const uint64_t* off, const uint64_t* len,
                         uint64_t stride, uint64_t L, const uint32_t* perm, uint64_t n, int top,
-                        uint8_t* nodes, hipStream_t s) {
+                        uint8_t* nodes, hipStream_t s, Gate gate) {
     hipLaunchKernelGGL((k_leaf<MODE, FUSE, LOAD>), dim3(grid_for(n)), dim3(kBlock), 0, s, base,
-                       off, len, stride, L, perm, n, top, nodes);
+                       off, len, stride, L, perm, n, top, nodes, gate);
 }
 
 template <int MODE, bool FUSE>
 static void leaf_dispatch(int load, const uint8_t* base, const uint64_t* off, const uint64_t* len,
                           uint64_t stride, uint64_t L, const uint32_t* perm, uint64_t n, int top,
-                          uint8_t* nodes, hipStream_t s) {
+                          uint8_t* nodes, hipStream_t s, Gate g) {
     switch (load) {
-        case 1: leaf_kernel<MODE, FUSE, 1>(base, off, len, stride, L, perm, n, top, nodes, s); break;
-        case 2: leaf_kernel<MODE, FUSE, 2>(base, off, len, stride, L, perm, n, top, nodes, s); break;
-        case 3: leaf_kernel<MODE, FUSE, 3>(base, off, len, stride, L, perm, n, top, nodes, s); break;
-        case 4: leaf_kernel<MODE, FUSE, 4>(base, off, len, stride, L, perm, n, top, nodes, s); break;
-        case 5: leaf_kernel<MODE, FUSE, 5>(base, off, len, stride, L, perm, n, top, nodes, s); break;
-        case 6: leaf_kernel<MODE, FUSE, 6>(base, off, len, stride, L, perm, n, top, nodes, s); break;
-        case 7: leaf_kernel<MODE, FUSE, 7>(base, off, len, stride, L, perm, n, top, nodes, s); break;
-        default: leaf_kernel<MODE, FUSE, 0>(base, off, len, stride, L, perm, n, top, nodes, s); break;
+        case 1: leaf_kernel<MODE, FUSE, 1>(base, off, len, stride, L, perm, n, top, nodes, s, g); break;
+        case 2: leaf_kernel<MODE, FUSE, 2>(base, off, len, stride, L, perm, n, top, nodes, s, g); break;
+        case 3: leaf_kernel<MODE, FUSE, 3>(base, off, len, stride, L, perm, n, top, nodes, s, g); break;
+        case 4: leaf_kernel<MODE, FUSE, 4>(base, off, len, stride, L, perm, n, top, nodes, s, g); break;
+        case 5: leaf_kernel<MODE, FUSE, 5>(base, off, len, stride, L, perm, n, top, nodes, s, g); break;
+        case 6: leaf_kernel<MODE, FUSE, 6>(base, off, len, stride, L, perm, n, top, nodes, s, g); break;
+        case 7: leaf_kernel<MODE, FUSE, 7>(base, off, len, stride, L, perm, n, top, nodes, s, g); break;
+        case 8: leaf_kernel<MODE, FUSE, 8>(base, off, len, stride, L, perm, n, top, nodes, s, g); break;
+        default: leaf_kernel<MODE, FUSE, 0>(base, off, len, stride, L, perm, n, top, nodes, s, g); break;
     }
 }
 
 hipError_t launch_leaf_strided(const uint8_t* base, uint64_t stride, uint64_t L, uint64_t n,
                                int top, bool fuse, int load, uint8_t* nodes, hipStream_t s) {
     const bool al = ((reinterpret_cast<uintptr_t>(base) | stride) & 15) == 0;
-    if (!al) load = 0;
-    if (fuse) leaf_dispatch<0, true>(load, base, nullptr, nullptr, stride, L, nullptr, n, top, nodes, s);
-    else leaf_dispatch<0, false>(load, base, nullptr, nullptr, stride, L, nullptr, n, top, nodes, s);
+    if (!al) load = load == 1 ? 8 : 0;  // LDS-DMA serves any alignment; direct loads need 16 B
+    if (fuse) leaf_dispatch<0, true>(load, base, nullptr, nullptr, stride, L, nullptr, n, top, nodes, s, Gate{});
+    else leaf_dispatch<0, false>(load, base, nullptr, nullptr, stride, L, nullptr, n, top, nodes, s, Gate{});
     return hipGetLastError();
 }
 
 hipError_t launch_leaf_offsets(const uint8_t* base, const uint64_t* off, const uint64_t* len,
                                const uint32_t* perm, uint64_t n, int top, bool fuse, bool aligned,
-                               int load, uint8_t* nodes, hipStream_t s, bool deep) {
+                               int load, uint8_t* nodes, hipStream_t s, bool deep, Gate gate) {
     if (perm && deep) load = aligned ? 6 : 7;  // ragged, length-sorted: deep prefetch
-    else if (!aligned) load = 0;
-    if (fuse && !perm) leaf_dispatch<1, true>(load, base, off, len, 0, 0, nullptr, n, top, nodes, s);
-    else leaf_dispatch<1, false>(load, base, off, len, 0, 0, perm, n, top, nodes, s);
+    else if (!aligned) load = load == 1 ? 8 : 0;  // LDS-DMA serves any alignment
+    if (fuse && !perm) leaf_dispatch<1, true>(load, base, off, len, 0, 0, nullptr, n, top, nodes, s, gate);
+    else leaf_dispatch<1, false>(load, base, off, len, 0, 0, perm, n, top, nodes, s, gate);
     return hipGetLastError();
 }
 
-// q[2] = first group (length-sorted, longest first) the non-priority waves may
-// take.  When the batch's work (sum over groups of their longest chain) is at
-// least twice what the longest chain alone keeps every SIMD busy for, the
-// batch is throughput-bound (e.g. equal lengths) and every wave takes any
-// group (q[2] = 0).  Otherwise the longest chain bounds the kernel and only
-// groups of at most split blocks may go to the non-priority waves.
-__global__ __launch_bounds__(256) void k_queue_split(const uint64_t* __restrict__ len,
+// Partials of the split decision, over all groups in parallel: q[2] = first
+// group (length-sorted, longest first) whose first value has at most split full
+// blocks (atomicMin), q[4..5] = the batch's work, sum over groups of their
+// first value's compressions (atomicAdd).  k_leaf_queue decides from them.
+__global__ __launch_bounds__(kBlock) void k_queue_split(const uint64_t* __restrict__ len,
                                                      const uint32_t* __restrict__ perm, uint32_t ngroups,
-                                                     uint32_t split, uint32_t simds, uint32_t* __restrict__ q) {
-    __shared__ unsigned long long part[4];
-    __shared__ uint32_t first[4];
+                                                     uint32_t split, uint32_t* __restrict__ q, Gate gate) {
+    if (!gate.open()) return;
     unsigned long long w = 0;
-    uint32_t b = ngroups;  // first group with a longest chain <= split (groups are longest first)
-    for (uint32_t g = threadIdx.x; g < ngroups; g += 256) {
-        const uint64_t blocks = len[perm[uint64_t(g) * 64]] >> 6;
-        w += blocks;
-        if (blocks <= split && g < b) b = g;
+    uint32_t b = 0xFFFFFFFFu;
+    for (uint32_t g = blockIdx.x * kBlock + threadIdx.x; g < ngroups; g += gridDim.x * kBlock) {
+        const uint64_t l = len[perm[uint64_t(g) * 64]];
+        w += compressions(l);
+        if ((l >> 6) <= split && g < b) b = g;
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -912,42 +1224,49 @@ __global__ __launch_bounds__(256) void k_queue_split(const uint64_t* __restrict_
         b = min(b, uint32_t(__shfl_xor(int(b), o)));
     }
     if ((threadIdx.x & 63) == 0) {
-        part[threadIdx.x >> 6] = w;
-        first[threadIdx.x >> 6] = b;
+        atomicAdd(reinterpret_cast<unsigned long long*>(q) + 2, w);
+        atomicMin(q + 2, b);
     }
-    __syncthreads();
-    if (threadIdx.x != 0) return;
-    const unsigned long long work = part[0] + part[1] + part[2] + part[3];
-    const unsigned long long longest = len[perm[0]] >> 6;
-    q[2] = work >= 2ull * simds * longest ? 0u : min(min(first[0], first[1]), min(first[2], first[3]));
 }
 
 hipError_t launch_leaf_queue(const uint8_t* base, const uint64_t* off, const uint64_t* len,
-                             const uint32_t* perm, uint64_t n, bool aligned, bool ring, uint32_t* q,
+                             const uint32_t* perm, uint64_t n, bool aligned, int ring, uint32_t* q,
                              uint32_t simds, uint32_t waves_per_simd, uint32_t split, uint8_t* nodes,
-                             hipStream_t s) {
+                             hipStream_t s, Gate gate) {
     const uint32_t ngroups = uint32_t((n + 63) / 64);
     const uint32_t waves = simds * waves_per_simd;
     hipError_t e = hipMemsetAsync(q, 0, queue_words(n) * sizeof(uint32_t), s);
+    if (e == hipSuccess) e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(q + 2), 0xFFFFFFFFu, 1, s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_queue_split, dim3(1), dim3(256), 0, s, len, perm, ngroups, split, simds, q);
-    if (ring)
-        hipLaunchKernelGGL(k_leaf_queue<8>, dim3(waves), dim3(64), 0, s, base, off, len, perm, n, ngroups, q, nodes);
+    const uint32_t sblocks = std::min<uint32_t>((ngroups + kBlock - 1) / kBlock, 256u);
+    hipLaunchKernelGGL(k_queue_split, dim3(sblocks), dim3(kBlock), 0, s, len, perm, ngroups, split, q, gate);
+    if (ring == 14)
+        hipLaunchKernelGGL(k_leaf_queue<13>, dim3(waves), dim3(64), 0, s, base, off, len, perm, n, ngroups, simds, q, nodes, gate);
+    else if (ring == 13)
+        hipLaunchKernelGGL(k_leaf_queue<12>, dim3(waves), dim3(64), 0, s, base, off, len, perm, n, ngroups, simds, q, nodes, gate);
+    else if (ring == 12)
+        hipLaunchKernelGGL(k_leaf_queue<11>, dim3(waves), dim3(64), 0, s, base, off, len, perm, n, ngroups, simds, q, nodes, gate);
+    else if (ring == 4)
+        hipLaunchKernelGGL(k_leaf_queue<10>, dim3(waves), dim3(64), 0, s, base, off, len, perm, n, ngroups, simds, q, nodes, gate);
+    else if (ring == 3)
+        hipLaunchKernelGGL(k_leaf_queue<9>, dim3(waves), dim3(64), 0, s, base, off, len, perm, n, ngroups, simds, q, nodes, gate);
+    else if (ring)
+        hipLaunchKernelGGL(k_leaf_queue<8>, dim3(waves), dim3(64), 0, s, base, off, len, perm, n, ngroups, simds, q, nodes, gate);
     else if (aligned)
-        hipLaunchKernelGGL(k_leaf_queue<6>, dim3(waves), dim3(64), 0, s, base, off, len, perm, n, ngroups, q, nodes);
+        hipLaunchKernelGGL(k_leaf_queue<6>, dim3(waves), dim3(64), 0, s, base, off, len, perm, n, ngroups, simds, q, nodes, gate);
     else
-        hipLaunchKernelGGL(k_leaf_queue<7>, dim3(waves), dim3(64), 0, s, base, off, len, perm, n, ngroups, q, nodes);
+        hipLaunchKernelGGL(k_leaf_queue<7>, dim3(waves), dim3(64), 0, s, base, off, len, perm, n, ngroups, simds, q, nodes, gate);
     return hipGetLastError();
 }
 
-uint64_t queue_words(uint64_t n) { return 4 + kSimdKeys + (n + 63) / 64; }
+uint64_t queue_words(uint64_t n) { return kQueueHeader + kSimdKeys + (n + 63) / 64; }
 
-hipError_t launch_reduce(uint8_t* nodes, uint64_t n, int from_level, int top, hipStream_t s) {
+hipError_t launch_reduce(uint8_t* nodes, uint64_t n, int from_level, int top, hipStream_t s, Gate gate) {
     int j0 = from_level;
     while (j0 < top) {
         const int jmax = (j0 + kFuseLevels < top) ? j0 + kFuseLevels : top;
         const uint64_t cnt = j0 == 0 ? n : ((n - 1) >> j0) + 1;
-        hipLaunchKernelGGL(k_reduce, dim3(grid_for(cnt)), dim3(kBlock), 0, s, nodes, n, j0, jmax);
+        hipLaunchKernelGGL(k_reduce, dim3(grid_for(cnt)), dim3(kBlock), 0, s, nodes, n, j0, jmax, gate);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
         j0 = jmax;
@@ -982,17 +1301,16 @@ extern "C" int nkv_diag_set_buffer(void* d) {
 }
 #endif
 
-hipError_t sort_by_length_desc(const uint64_t* len, uint64_t n, uint32_t* keys, uint32_t* perm,
-                               void* tmp, size_t* tmp_bytes, hipStream_t s) {
-    // keys: 2n u32 (in | out), perm: 2n u32 (iota in | permutation out)
-    if (tmp == nullptr)
-        return hipcub::DeviceRadixSort::SortPairsDescending(nullptr, *tmp_bytes, keys, keys + n, perm,
-                                                            perm + n, int(n), 0, 16, s);
-    hipLaunchKernelGGL(k_bucket_keys, dim3(grid_for(n)), dim3(kBlock), 0, s, len, n, keys, perm);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    return hipcub::DeviceRadixSort::SortPairsDescending(tmp, *tmp_bytes, keys, keys + n, perm, perm + n,
-                                                        int(n), 0, 16, s);
+uint64_t sort_hist_words(uint64_t n) { return ((n + kSortTile - 1) / kSortTile) * kLenBuckets; }
+
+hipError_t sort_by_length_desc(const uint64_t* len, uint64_t n, uint32_t* perm, uint32_t* hist, hipStream_t s,
+                               Gate gate) {
+    const uint64_t tiles = (n + kSortTile - 1) / kSortTile;
+    if (tiles == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_len_hist, dim3(uint32_t(tiles)), dim3(kBlock), 0, s, len, n, hist, gate);
+    hipLaunchKernelGGL(k_len_scan, dim3(1), dim3(1024), 0, s, hist, uint32_t(tiles), gate);
+    hipLaunchKernelGGL(k_len_scatter, dim3(uint32_t(tiles)), dim3(kBlock), 0, s, len, n, hist, perm, gate);
+    return hipGetLastError();
 }
 
 hipError_t launch_fill(uint8_t* buf, uint64_t nbytes, uint64_t seed, hipStream_t s) {

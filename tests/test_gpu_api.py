@@ -178,3 +178,40 @@ def test_device_locator_matches_host(nkv):
     assert np.array_equal(d_vlen.cpu().numpy().astype(np.uint64), ln)
     assert np.array_equal(d_roff.cpu().numpy().astype(np.uint64),
                           np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64))
+
+
+def test_tree_from_records_dev_async_and_bad_header(nkv, oracle):
+    """nkv_tree_from_records_dev: the compaction form on a device-resident Data
+    table, asynchronous with a device error flag, or synchronous without one."""
+    import torch
+    from nakevaleng_amd import record
+    _lib, ctx = nkv
+    L = _lib.lib()
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    rng = np.random.default_rng(21)
+    recs = [record.New(rng.bytes(int(rng.integers(1, 50))), rng.bytes(int(rng.integers(0, 9000))), timestamp=i)
+            for i in range(2500)]
+    stream, sizes = record.data_table(recs)
+    n = len(sizes)
+    roff = np.zeros(n, np.uint64)
+    roff[1:] = np.cumsum(np.asarray(sizes, np.uint64)[:-1])
+    off, ln = record.value_spans(stream, sizes)
+    want = oracle.tree_from_digests(oracle.leaf_hashes(np.frombuffer(stream, np.uint8), off, ln))
+    d_stream = torch.from_numpy(np.frombuffer(stream, np.uint8).copy()).cuda()
+    d_roff = torch.from_numpy(roff.view(np.int64)).cuda()
+    d_nodes = torch.zeros(L.nkv_total_nodes(n) * 20, dtype=torch.uint8, device="cuda")
+    d_err = torch.full((1,), 7, dtype=torch.int32, device="cuda")
+    _lib.check(L.nkv_tree_from_records_dev(ctx.h, d_stream.data_ptr(), len(stream), d_roff.data_ptr(), n,
+                                           d_nodes.data_ptr(), d_err.data_ptr()))
+    torch.cuda.synchronize()
+    assert int(d_err.item()) == 0
+    assert np.array_equal(d_nodes.cpu().numpy().reshape(-1, 20), want)
+    bad = np.frombuffer(stream, np.uint8).copy()
+    bad[int(roff[7]) + 22:int(roff[7]) + 30] = np.frombuffer(np.uint64(10**12).tobytes(), np.uint8)
+    d_bad = torch.from_numpy(bad).cuda()
+    _lib.check(L.nkv_tree_from_records_dev(ctx.h, d_bad.data_ptr(), len(stream), d_roff.data_ptr(), n,
+                                           d_nodes.data_ptr(), d_err.data_ptr()))
+    torch.cuda.synchronize()
+    assert int(d_err.item()) == 1
+    assert L.nkv_tree_from_records_dev(ctx.h, d_bad.data_ptr(), len(stream), d_roff.data_ptr(), n,
+                                       d_nodes.data_ptr(), None) == _lib.NKV_ERR_INVALID

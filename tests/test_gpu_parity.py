@@ -91,7 +91,7 @@ def test_leaf_hash_mixed_wave_alignment(nkv, oracle, bucket):
     torch.cuda.synchronize()
     got = d_nodes.cpu().numpy().reshape(-1, 20)
     want = oracle.tree_from_digests(oracle.leaf_hashes(data, off, lens))
-    ctx.set_option(_lib.NKV_OPT_BUCKET, 1)
+    ctx.set_option(_lib.NKV_OPT_BUCKET, 2)
     assert np.array_equal(got, want)
 
 
@@ -127,18 +127,22 @@ def test_mixed_sizes_log_uniform(nkv, oracle, load):
     assert np.array_equal(nodes, want)
 
 
-@pytest.mark.parametrize("deep", [0, 1, 2, 3])
+@pytest.mark.parametrize("deep,ring", [(0, 2), (1, 2), (2, 2), (3, 2), (3, 3), (3, 4), (3, 12), (3, 13), (3, 14)])
 @pytest.mark.parametrize("n,packed", [(1, True), (63, True), (65, False), (3001, True), (3001, False),
                                       (20000, True)])
-def test_ragged_deep_and_queue_paths(nkv, oracle, deep, n, packed):
+def test_ragged_deep_and_queue_paths(nkv, oracle, deep, ring, n, packed):
     """Length-sorted ragged batches through each NKV_OPT_DEEP_PREFETCH mode:
     0 = one-block lookahead, 1 = several blocks, 2 = the work-queue kernel (groups
     pulled from both ends, claim flags at the meeting point), 3 = the work-queue
-    kernel with the LDS chunk ring.  Packed = back to
-    back (unaligned path); otherwise 16-B aligned starts (aligned path)."""
+    kernel with the LDS chunk ring of 2 slots, or the pipelined ring of 3 / 4
+    slots (explicit vmcnt / lgkmcnt waits).  Packed = back to back (unaligned
+    path); otherwise 16-B aligned starts (aligned path)."""
     torch = _torch()
-    _lib, ctx = nkv
+    _lib, _ = nkv
+    ctx = _lib.Context(0)
     _bind(torch, ctx)
+    ctx.set_option(_lib.NKV_OPT_QUEUE_RING, ring)
+    ctx.set_option(_lib.NKV_OPT_BUCKET, 1)
     L = _lib.lib()
     rng = np.random.default_rng(1000 * n + deep)
     lens = np.floor(2.0 ** rng.uniform(0, 15, n)).astype(np.uint64)
@@ -159,19 +163,23 @@ def test_ragged_deep_and_queue_paths(nkv, oracle, deep, n, packed):
             want = oracle.tree_from_digests(oracle.leaf_hashes(data, off, lens, threads=8))
             assert np.array_equal(d_nodes.cpu().numpy().reshape(-1, 20), want)
     finally:
-        ctx.set_option(_lib.NKV_OPT_DEEP_PREFETCH, 3)
+        ctx.close()
 
 
+@pytest.mark.parametrize("ring", [2, 3, 4, 12, 13, 14])
 @pytest.mark.parametrize("split", [0, 1, 32, 100000])
 @pytest.mark.parametrize("shape", ["uniform", "skewed"])
-def test_queue_split_policies(nkv, oracle, split, shape):
+def test_queue_split_policies(nkv, oracle, split, shape, ring):
     """Work-queue kernel under every split regime: equal lengths (throughput-
     bound: every wave takes any group) and one very long value among short ones
     (the longest chain bounds the batch: short groups only to the non-priority
     waves), with splits that leave the non-priority waves nothing / everything."""
     torch = _torch()
-    _lib, ctx = nkv
+    _lib, _ = nkv
+    ctx = _lib.Context(0)
     _bind(torch, ctx)
+    ctx.set_option(_lib.NKV_OPT_QUEUE_RING, ring)
+    ctx.set_option(_lib.NKV_OPT_BUCKET, 1)  # equal lengths would take input order in auto mode
     L = _lib.lib()
     rng = np.random.default_rng(split + (7 if shape == "uniform" else 8))
     n = 9000
@@ -191,7 +199,7 @@ def test_queue_split_policies(nkv, oracle, split, shape):
                                               n, d_nodes.data_ptr()))
         torch.cuda.synchronize()
     finally:
-        ctx.set_option(_lib.NKV_OPT_QUEUE_SPLIT, 32)
+        ctx.close()
     want = oracle.tree_from_digests(oracle.leaf_hashes(data, off, lens, threads=8))
     assert np.array_equal(d_nodes.cpu().numpy().reshape(-1, 20), want)
 
@@ -339,3 +347,33 @@ def test_deterministic_repeat(nkv, oracle):
         torch.cuda.synchronize()
         outs.append(d_nodes.cpu().numpy())
     assert all(np.array_equal(outs[0], o) for o in outs[1:])
+
+
+@pytest.mark.parametrize("bucket", [0, 1, 2])
+@pytest.mark.parametrize("spread", [0, 3, 40])
+def test_bucket_modes_narrow_and_wide(nkv, oracle, bucket, spread):
+    """NKV_OPT_BUCKET 0 / 1 / 2 (auto: input order when the full-block counts lie
+    within max(1, min/16), else sorted) on batches of 6000 unaligned values whose
+    block counts spread 0, 3 and 40 around 63 blocks: every mode, same tree."""
+    torch = _torch()
+    _lib, _ = nkv
+    ctx = _lib.Context(0)
+    _bind(torch, ctx)
+    ctx.set_option(_lib.NKV_OPT_BUCKET, bucket)
+    L = _lib.lib()
+    rng = np.random.default_rng(100 * bucket + spread)
+    n = 6000
+    lens = (4050 + 64 * rng.integers(-spread, spread + 1, n)).astype(np.uint64)
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum(lens[:-1] + 46)
+    data = oracle.splitmix64_bytes(int(off[-1] + lens[-1]), SEED + spread)
+    d_data, d_off, d_len = _dev(torch, data), _dev(torch, off), _dev(torch, lens)
+    d_nodes = torch.zeros(L.nkv_total_nodes(n) * 20, dtype=torch.uint8, device="cuda")
+    try:
+        _lib.check(L.nkv_tree_from_values_dev(ctx.h, d_data.data_ptr(), d_off.data_ptr(), d_len.data_ptr(),
+                                              n, d_nodes.data_ptr()))
+        torch.cuda.synchronize()
+    finally:
+        ctx.close()
+    want = oracle.tree_from_digests(oracle.leaf_hashes(data, off, lens, threads=8))
+    assert np.array_equal(d_nodes.cpu().numpy().reshape(-1, 20), want)
