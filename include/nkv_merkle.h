@@ -110,7 +110,9 @@ int nkv_ctx_sync(nkv_ctx *ctx);
 #define NKV_OPT_CRC_LOAD 6    /* record checksums: bit 0 = spans staged as aligned 64-B
                                  chunks through an LDS ring (else per-lane loads); bits
                                  1-2 = LDS table copies x workgroup: 0 = 8 x 256,
-                                 1 = 16 x 512, 2 = 32 x 1024 (no ring) */
+                                 1 = 16 x 512, 2 = 32 x 1024 (no ring); 8 = span groups:
+                                 16 lanes per span, one 64-B chunk per lane, chunk states
+                                 combined by CRC advance tables */
 #define NKV_OPT_HOST_THREADS 7 /* host-buffer API: threads that gather caller bytes into the
                                   pinned staging chunks (0 = default: min(16, cores), or
                                   the NKV_HOST_THREADS environment variable) */

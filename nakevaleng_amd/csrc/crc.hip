@@ -23,6 +23,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "internal.hpp"
 
 namespace nkv {
@@ -240,11 +242,209 @@ __global__ __launch_bounds__(B) void k_crc(const uint8_t* __restrict__ base, con
     }
 }
 
-// variant: bit 0 = LDS chunk ring; bits 1-2 = table copies x workgroup size:
-// 0 = 8 x 256, 1 = 16 x 512, 2 = 32 x 1024.
+// ---------------------------------------------------------------------------
+// Span-group form: 16 lanes per span, one 64-byte chunk per lane.
+//
+// CRC is affine over GF(2): the state after a span is the XOR, over its
+// chunks, of each chunk's own state (chunk processed from state 0; the first
+// chunk starts from 0xFFFFFFFF at the span's first byte) advanced over the
+// bytes that follow the chunk, i.e. multiplied by x^(8d) mod P.  Chunks are
+// aligned to the span END (chunk c = [e - 64 (n - c), + 64)), so every chunk
+// but the first is a full 64 bytes and every advance is a multiple of 64 bytes:
+// a window of 16 chunks is combined in 4 butterfly levels (advance by 64, 128,
+// 256, 512 bytes, all lanes of a level by the same distance, one LDS table
+// each), and the running state advances by 1 KiB per window.  The first
+// window is padded on the left (empty chunks contribute 0), so lengths need no
+// tail case; the first chunk's bytes before the span are skipped (dword loads
+// from the span only).  Each lane reads its chunk as four 16-byte loads at the
+// chunk address (any alignment), so a group's loads cover 1 KiB contiguous.
+constexpr int kCrcGroup = 16;
+
+struct CrcShifts {
+    uint32_t t[6][4][256];  // advance by 64 << i zero bytes, i = 0..4; [5]: by 16 bytes
+};
+
+constexpr uint32_t crc_advance(const uint32_t (&t)[4][256], uint32_t v) {
+    return t[0][v & 0xFFu] ^ t[1][(v >> 8) & 0xFFu] ^ t[2][(v >> 16) & 0xFFu] ^ t[3][v >> 24];
+}
+
+constexpr CrcShifts make_crc_shifts() {
+    const CrcTables T = make_crc_tables();
+    CrcShifts r{};
+    for (int k = 0; k < 4; ++k)
+        for (uint32_t b = 0; b < 256; ++b) {
+            uint32_t v = b << (8 * k);
+            for (int w = 0; w < 16; ++w) {  // 16 zero words = 64 zero bytes (slicing-by-4 step)
+                v = T.t[3][v & 0xFFu] ^ T.t[2][(v >> 8) & 0xFFu] ^ T.t[1][(v >> 16) & 0xFFu] ^ T.t[0][v >> 24];
+                if (w == 3) r.t[5][k][b] = v;
+            }
+            r.t[0][k][b] = v;
+        }
+    for (int i = 1; i < 5; ++i)  // twice the distance = the advance applied twice
+        for (int k = 0; k < 4; ++k)
+            for (uint32_t b = 0; b < 256; ++b)
+                r.t[i][k][b] = crc_advance(r.t[i - 1], crc_advance(r.t[i - 1], b << (8 * k)));
+    return r;
+}
+
+__constant__ CrcShifts c_crc_shift = make_crc_shifts();
+
+__device__ __forceinline__ uint32_t lds_advance(const uint32_t* t, uint32_t v) {
+    return t[v & 0xFFu] ^ t[256 + ((v >> 8) & 0xFFu)] ^ t[512 + ((v >> 16) & 0xFFu)] ^ t[768 + (v >> 24)];
+}
+
+__device__ __forceinline__ uint32_t ld_u32_any(const uint8_t* p) { return *reinterpret_cast<const uint32_t*>(p); }
+
+// CRC-32 of [s, s + L) by the 16 lanes of a group (j = lane in the group).
+// Every lane of the wave calls it (wave-uniform window loop).
+template <int C>
+__device__ __forceinline__ uint32_t crc_group_span(const uint8_t* s, uint64_t L, uint32_t j, const uint32_t* tab,
+                                                   const uint32_t* sh) {
+    const uint64_t nch = (L + 63) >> 6;
+    const uint64_t W = (nch + kCrcGroup - 1) / kCrcGroup;
+    uint64_t wmax = W;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) wmax = max(wmax, uint64_t(__shfl_xor((long long)wmax, o)));
+    const uint8_t* e = s + L;
+    uint32_t R = 0;
+    for (uint64_t w = 0; w < wmax; ++w) {
+        const int64_t c = int64_t(nch) - int64_t(kCrcGroup) * (int64_t(W) - int64_t(w)) + int64_t(j);
+        uint32_t st = 0;
+        if (w < W && c >= 0) {
+            const uint8_t* cs = e - 64 * (nch - uint64_t(c));
+            const uint32_t h = c == 0 ? uint32_t(64 * nch - L) : 0u;  // chunk bytes before the span
+            if (h == 0) {
+                // four independent 16-byte sub-chunks (four dependent lookup
+                // chains of 4 instead of one of 16), joined by Horner steps of
+                // a 16-byte advance
+                const uint4* q = reinterpret_cast<const uint4*>(cs);
+                uint4 v[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) v[i] = q[i];
+                uint32_t a = c == 0 ? 0xFFFFFFFFu : 0u, b = 0u, g = 0u, d = 0u;
+                a = crc_word<C>(a, v[0].x, tab);
+                b = crc_word<C>(b, v[1].x, tab);
+                g = crc_word<C>(g, v[2].x, tab);
+                d = crc_word<C>(d, v[3].x, tab);
+                a = crc_word<C>(a, v[0].y, tab);
+                b = crc_word<C>(b, v[1].y, tab);
+                g = crc_word<C>(g, v[2].y, tab);
+                d = crc_word<C>(d, v[3].y, tab);
+                a = crc_word<C>(a, v[0].z, tab);
+                b = crc_word<C>(b, v[1].z, tab);
+                g = crc_word<C>(g, v[2].z, tab);
+                d = crc_word<C>(d, v[3].z, tab);
+                a = crc_word<C>(a, v[0].w, tab);
+                b = crc_word<C>(b, v[1].w, tab);
+                g = crc_word<C>(g, v[2].w, tab);
+                d = crc_word<C>(d, v[3].w, tab);
+                const uint32_t* s16 = sh + 5 * 1024;
+                st = lds_advance(s16, lds_advance(s16, lds_advance(s16, a) ^ b) ^ g) ^ d;
+            } else {
+                // first chunk, span starts h bytes in: 0-3 bytes up to the chunk's
+                // word grid, then whole words, all read from inside the span
+                st = 0xFFFFFFFFu;
+                const uint32_t jw = (h + 3) >> 2;
+                for (uint32_t b = 0; b < 4 * jw - h; ++b) st = crc_byte<C>(st, s[b], tab);
+                for (uint32_t i = jw; i < 16; ++i) st = crc_word<C>(st, ld_u32_any(cs + 4 * i), tab);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t other = uint32_t(__shfl_xor(int(st), 1 << k));
+            const bool right = (j >> k) & 1u;
+            st = lds_advance(sh + 1024 * k, right ? other : st) ^ (right ? st : other);
+        }
+        if (w < W) R = lds_advance(sh + 4096, R) ^ st;
+    }
+    return L ? ~R : 0u;
+}
+
+// C slicing-table copies, WG threads: 8 x 512 (56 KiB LDS, 2 workgroups per
+// CU), 4 x 512 (40 KiB, 4 per CU) or 32 x 1024 (152 KiB, one per CU; lane l
+// reads copy l % 32, so every table lookup is bank-conflict free).
+template <bool RECORDS, int C, int WG>
+__global__ __launch_bounds__(WG) void k_crc_group(const uint8_t* __restrict__ base,
+                                                      const uint64_t* __restrict__ off,
+                                                      const uint64_t* __restrict__ len, uint64_t stream_len,
+                                                      uint64_t n, uint32_t* __restrict__ out,
+                                                      unsigned long long* __restrict__ stats) {
+    __shared__ uint32_t tab[4 * 256 * C];
+    __shared__ uint32_t sh[6 * 4 * 256];
+    for (int i = threadIdx.x; i < 4 * 256 * C; i += WG) tab[i] = (&c_crc.t[0][0])[i / C];
+    for (int i = threadIdx.x; i < 6 * 4 * 256; i += WG) sh[i] = (&c_crc_shift.t[0][0][0])[i];
+    __syncthreads();
+    const uint32_t* mytab = tab + (threadIdx.x % C);
+    const uint32_t j = threadIdx.x & (kCrcGroup - 1);
+    const uint32_t gw = (threadIdx.x & 63) / kCrcGroup;  // group within the wave
+    const uint64_t stride = uint64_t(gridDim.x) * (WG / kCrcGroup);
+    // persistent: the tables are loaded once per workgroup; a wave's four groups
+    // advance together so the loop bound is wave-uniform
+    for (uint64_t i = uint64_t(blockIdx.x) * (WG / kCrcGroup) + threadIdx.x / kCrcGroup; i - gw < n;
+         i += stride) {
+        const bool live = i < n;
+        const uint8_t* s = base;
+        uint64_t L = 0;
+        uint32_t stored = 0;
+        bool hdr_bad = false;
+        if (live) {
+            if (RECORDS) {
+                const uint64_t r = off[i];
+                if (r + 30 <= stream_len) {
+                    const uint64_t ks = crc_ld_le64(base + r + 14);
+                    const uint64_t vs = crc_ld_le64(base + r + 22);
+                    if (ks <= stream_len && vs <= stream_len && r + 30 + ks + vs <= stream_len) {
+                        s = base + r + 30;
+                        L = ks + vs;
+                        stored = uint32_t(base[r]) | uint32_t(base[r + 1]) << 8 | uint32_t(base[r + 2]) << 16 |
+                                 uint32_t(base[r + 3]) << 24;
+                    } else {
+                        hdr_bad = true;
+                    }
+                } else {
+                    hdr_bad = true;
+                }
+            } else {
+                s = base + off[i];
+                L = len[i];
+            }
+        }
+        const uint32_t crc = crc_group_span<C>(s, L, j, mytab, sh);
+        if (live && j == 0) {
+            if (out) out[i] = crc;
+            if (RECORDS && stats) {
+                if (hdr_bad) atomicOr(stats + 2, 1ull);
+                else if (crc != stored) {
+                    atomicAdd(stats, 1ull);
+                    atomicMin(stats + 1, (unsigned long long)i);
+                }
+            }
+        }
+    }
+}
+
+template <bool RECORDS, int C, int WG>
+static void launch_crc_group(int per_cu, const uint8_t* base, const uint64_t* off, const uint64_t* len,
+                             uint64_t stream_len, uint64_t n, uint32_t* out, unsigned long long* stats,
+                             hipStream_t s) {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const uint64_t groups_per_wg = WG / kCrcGroup;
+    const uint64_t want = (n + groups_per_wg - 1) / groups_per_wg;
+    const uint32_t grid = uint32_t(std::min<uint64_t>(want, uint64_t(cus) * per_cu));
+    hipLaunchKernelGGL((k_crc_group<RECORDS, C, WG>), dim3(grid), dim3(WG), 0, s, base, off, len, stream_len, n,
+                       out, stats);
+}
+
+// variant 8 / 9: span-group kernel with 8 x 512 / 32 x 1024 table copies x
+// workgroup.  Else bit 0 = LDS chunk ring; bits 1-2 = table copies x workgroup
+// size: 0 = 8 x 256, 1 = 16 x 512, 2 = 32 x 1024.
 template <bool RECORDS>
 static void launch_crc(int variant, const uint8_t* base, const uint64_t* off, const uint64_t* len,
                        uint64_t stream_len, uint64_t n, uint32_t* out, unsigned long long* stats, hipStream_t s) {
+    if (variant == 8) return launch_crc_group<RECORDS, 8, 512>(2, base, off, len, stream_len, n, out, stats, s);
+    if (variant == 9) return launch_crc_group<RECORDS, 32, 1024>(1, base, off, len, stream_len, n, out, stats, s);
+    if (variant == 10) return launch_crc_group<RECORDS, 4, 512>(4, base, off, len, stream_len, n, out, stats, s);
     const bool ring = variant & 1;
     const int cfg = (variant >> 1) & 3;
     const int B = cfg == 0 ? 256 : (cfg == 1 ? 512 : 1024);

@@ -30,7 +30,7 @@ def _stream(rng, n, kmax=40, vmax=3000):
     return recs, np.frombuffer(stream, np.uint8).copy(), sizes, off
 
 
-@pytest.mark.parametrize("load", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("load", [0, 1, 2, 3, 4, 8, 9, 10])
 def test_crc32_spans_every_alignment_and_length(nkv, oracle, load):
     torch = _torch()
     _lib, ctx = nkv
@@ -66,7 +66,7 @@ def test_crc32_check_value(nkv):
     assert int(out.cpu().numpy().view(np.uint32)[0]) == 0xCBF43926
 
 
-@pytest.mark.parametrize("load", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("load", [0, 1, 2, 3, 4, 8, 9, 10])
 @pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 257, 3000])
 def test_record_crc_device_matches_oracle_and_stored(nkv, oracle, n, load):
     torch = _torch()
