@@ -133,6 +133,161 @@ __global__ __launch_bounds__(kBloomBlock) void k_bloom(const uint8_t* __restrict
 
 static uint64_t fastmod_magic(uint32_t d) { return ~uint64_t(0) / d + 1; }
 
+// ---------------------------------------------------------------------------
+// Range-privatised insert.  A filter's n*k bit updates land on m bits at
+// random: device-scope atomicOr on one shared array runs at ~24 G updates/s.
+// Instead the bit space is cut into 32768-bit ranges (4 KiB of LDS each) and
+// the updates are grouped by range with a counting sort (per-tile counts, one
+// column scan, a scatter that recomputes the hashes), then one workgroup per
+// range sets its bits with LDS atomics and ORs its 1024 words into the filter
+// (it is their only writer).
+constexpr uint32_t kBloomRangeShift = 15;
+constexpr uint32_t kBloomRangeWords = (1u << kBloomRangeShift) / 32;
+constexpr uint32_t kBloomMaxRanges = 4096;  // LDS counters of a tile
+constexpr int kBloomTileKeys = 8;           // keys per thread of a tile
+
+// key i: pointer and length (MODE 1: the record's key, header checked)
+template <int MODE>
+__device__ __forceinline__ bool bloom_key(const uint8_t* base, const uint64_t* off, const uint64_t* len,
+                                          uint64_t stream_len, uint64_t i, const uint8_t** key, uint64_t* L) {
+    if (MODE == 0) {
+        *key = base + off[i];
+        *L = len[i];
+        return true;
+    }
+    const uint64_t r = off[i];
+    if (r + 30 > stream_len) return false;
+    const uint64_t l = bl_ld_le64(base + r + 14);
+    if (l > stream_len - r - 30) return false;
+    *key = base + r + 30;
+    *L = l;
+    return true;
+}
+
+// fn(idx) for the k bit indices of key i
+template <int MODE, class F>
+__device__ __forceinline__ void bloom_indices(const uint8_t* base, const uint64_t* off, const uint64_t* len,
+                                              uint64_t stream_len, uint64_t i, uint32_t m, uint64_t M, uint32_t k,
+                                              uint32_t seed0, unsigned int* err, F fn) {
+    const uint8_t* key;
+    uint64_t L;
+    if (!bloom_key<MODE>(base, off, len, stream_len, i, &key, &L)) {
+        if (err) atomicOr(err, 1u);
+        return;
+    }
+    for (uint32_t j0 = 0; j0 < k; j0 += kBloomMaxK) {
+        const int nk = int(min(k - j0, uint32_t(kBloomMaxK)));
+        uint32_t h[kBloomMaxK];
+        mm_states(key, L, seed0 + j0, nk, h);
+#pragma unroll
+        for (int j = 0; j < kBloomMaxK; ++j)
+            if (j < nk) fn(fastmod_u32(mm_fmix(h[j] ^ uint32_t(L)), M, m));
+    }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kBloomBlock) void k_bloom_count(const uint8_t* __restrict__ base,
+                                                             const uint64_t* __restrict__ off,
+                                                             const uint64_t* __restrict__ len, uint64_t stream_len,
+                                                             uint64_t n, uint32_t m, uint64_t M, uint32_t k,
+                                                             uint32_t seed0, uint32_t nranges, uint32_t tiles,
+                                                             uint32_t* __restrict__ hist, unsigned int* err) {
+    __shared__ uint32_t cnt[kBloomMaxRanges];
+    for (uint32_t r = threadIdx.x; r < nranges; r += kBloomBlock) cnt[r] = 0u;
+    __syncthreads();
+    const uint64_t t0 = uint64_t(blockIdx.x) * kBloomBlock * kBloomTileKeys;
+    for (int q = 0; q < kBloomTileKeys; ++q) {
+        const uint64_t i = t0 + uint64_t(q) * kBloomBlock + threadIdx.x;
+        if (i < n)
+            bloom_indices<MODE>(base, off, len, stream_len, i, m, M, k, seed0, err,
+                                [&](uint32_t idx) { atomicAdd(&cnt[idx >> kBloomRangeShift], 1u); });
+    }
+    __syncthreads();
+    // range-major, so one exclusive scan gives every (range, tile) slot's first
+    // update position and range r's updates are [hist[r * tiles], hist[(r + 1) * tiles])
+    for (uint32_t r = threadIdx.x; r < nranges; r += kBloomBlock) hist[uint64_t(r) * tiles + blockIdx.x] = cnt[r];
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kBloomBlock) void k_bloom_scatter(const uint8_t* __restrict__ base,
+                                                               const uint64_t* __restrict__ off,
+                                                               const uint64_t* __restrict__ len,
+                                                               uint64_t stream_len, uint64_t n, uint32_t m, uint64_t M,
+                                                               uint32_t k, uint32_t seed0, uint32_t nranges,
+                                                               uint32_t tiles, const uint32_t* __restrict__ hist,
+                                                               uint32_t* __restrict__ upd) {
+    __shared__ uint32_t cur[kBloomMaxRanges];
+    for (uint32_t r = threadIdx.x; r < nranges; r += kBloomBlock) cur[r] = hist[uint64_t(r) * tiles + blockIdx.x];
+    __syncthreads();
+    const uint64_t t0 = uint64_t(blockIdx.x) * kBloomBlock * kBloomTileKeys;
+    for (int q = 0; q < kBloomTileKeys; ++q) {
+        const uint64_t i = t0 + uint64_t(q) * kBloomBlock + threadIdx.x;
+        if (i < n)
+            bloom_indices<MODE>(base, off, len, stream_len, i, m, M, k, seed0, nullptr,
+                                [&](uint32_t idx) { upd[atomicAdd(&cur[idx >> kBloomRangeShift], 1u)] = idx; });
+    }
+}
+
+__global__ __launch_bounds__(kBloomBlock) void k_bloom_apply(const uint32_t* __restrict__ upd,
+                                                             const uint32_t* __restrict__ hist, uint32_t tiles,
+                                                             uint32_t words, uint32_t* __restrict__ bits) {
+    __shared__ uint32_t w[kBloomRangeWords];
+    const uint32_t r = blockIdx.x;
+    for (uint32_t t = threadIdx.x; t < kBloomRangeWords; t += kBloomBlock) w[t] = 0u;
+    __syncthreads();
+    // hist holds one word past the last range: the total
+    const uint32_t lo = hist[uint64_t(r) * tiles], hi = hist[uint64_t(r + 1) * tiles];
+    for (uint32_t i = lo + threadIdx.x; i < hi; i += kBloomBlock) {
+        const uint32_t idx = upd[i];
+        atomicOr(&w[(idx >> 5) & (kBloomRangeWords - 1)], 1u << (idx & 31u));
+    }
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < kBloomRangeWords; t += kBloomBlock) {
+        const uint64_t g = uint64_t(r) * kBloomRangeWords + t;
+        if (g < words && w[t]) bits[g] |= w[t];  // range r's words have no other writer
+    }
+}
+
+uint64_t bloom_ranges_scratch_words(uint64_t n, uint32_t m, uint32_t k) {
+    const uint64_t nranges = (uint64_t(m) + (1u << kBloomRangeShift) - 1) >> kBloomRangeShift;
+    const uint64_t tiles = (n + uint64_t(kBloomBlock) * kBloomTileKeys - 1) / (uint64_t(kBloomBlock) * kBloomTileKeys);
+    if (nranges > kBloomMaxRanges || n * k > 0xFFFFFFFFull) return 0;  // the atomic kernel serves these
+    const uint64_t h = tiles * nranges + 1;
+    return h + scan_sums_words(h) + n * k;
+}
+
+hipError_t launch_bloom_ranges(int mode, const uint8_t* base, const uint64_t* off, const uint64_t* len,
+                               uint64_t stream_len, uint64_t n, uint32_t m, uint32_t k, uint32_t seed0,
+                               uint32_t* bits, unsigned int* err, uint32_t* scratch, hipStream_t s) {
+    if (n == 0 || k == 0) return hipSuccess;
+    const uint32_t nranges = (m + (1u << kBloomRangeShift) - 1) >> kBloomRangeShift;
+    const uint64_t tiles = (n + uint64_t(kBloomBlock) * kBloomTileKeys - 1) / (uint64_t(kBloomBlock) * kBloomTileKeys);
+    const uint64_t hn = tiles * nranges + 1;
+    uint32_t* hist = scratch;
+    uint32_t* sums = hist + hn;
+    uint32_t* upd = sums + scan_sums_words(hn);
+    const uint64_t M = fastmod_magic(m);
+    const uint32_t words = (m + 31) / 32;
+    const uint32_t T = uint32_t(tiles);
+    hipError_t e = hipMemsetAsync(hist + hn - 1, 0, 4, s);  // the appended zero: the scan leaves the total there
+    if (e != hipSuccess) return e;
+    if (mode == 0)
+        hipLaunchKernelGGL(k_bloom_count<0>, dim3(T), dim3(kBloomBlock), 0, s, base, off, len, stream_len, n, m, M, k,
+                           seed0, nranges, T, hist, err);
+    else
+        hipLaunchKernelGGL(k_bloom_count<1>, dim3(T), dim3(kBloomBlock), 0, s, base, off, len, stream_len, n, m, M, k,
+                           seed0, nranges, T, hist, err);
+    if ((e = scan_exclusive_u32(hist, hn, sums, s)) != hipSuccess) return e;
+    if (mode == 0)
+        hipLaunchKernelGGL(k_bloom_scatter<0>, dim3(T), dim3(kBloomBlock), 0, s, base, off, len, stream_len, n, m, M,
+                           k, seed0, nranges, T, hist, upd);
+    else
+        hipLaunchKernelGGL(k_bloom_scatter<1>, dim3(T), dim3(kBloomBlock), 0, s, base, off, len, stream_len, n, m, M,
+                           k, seed0, nranges, T, hist, upd);
+    hipLaunchKernelGGL(k_bloom_apply, dim3(nranges), dim3(kBloomBlock), 0, s, upd, hist, T, words, bits);
+    return hipGetLastError();
+}
+
 hipError_t launch_bloom(int mode, bool query, const uint8_t* base, const uint64_t* off, const uint64_t* len,
                         uint64_t stream_len, uint64_t n, uint32_t m, uint32_t k, uint32_t seed0, uint32_t* bits,
                         uint8_t* out, unsigned int* err, hipStream_t s) {

@@ -104,6 +104,7 @@ struct nkv_ctx {
     int queue_split = 32;   // NKV_OPT_QUEUE_SPLIT
     int queue_waves = 4;    // NKV_OPT_QUEUE_WAVES
     int queue_ring = 13;    // NKV_OPT_QUEUE_RING
+    int bloom_path = 1;     // NKV_OPT_BLOOM_PATH
     int crc_load = 1;       // NKV_OPT_CRC_LOAD
     bool timing = false;
     bool timed = false;
@@ -462,6 +463,10 @@ int nkv_ctx_set_option(nkv_ctx* c, int key, int64_t value) {
         case NKV_OPT_CRC_LOAD:
             if (value < 0 || (value > 5 && (value < 8 || value > 10))) return NKV_ERR_INVALID;
             c->crc_load = int(value);
+            return NKV_OK;
+        case NKV_OPT_BLOOM_PATH:
+            if (value < 0 || value > 1) return NKV_ERR_INVALID;
+            c->bloom_path = int(value);
             return NKV_OK;
         case NKV_OPT_QUEUE_RING:
             if (!((value >= 2 && value <= 4) || (value >= 12 && value <= 14))) return NKV_ERR_INVALID;
@@ -949,14 +954,28 @@ int nkv_record_crc_dev(nkv_ctx* c, const void* d_stream, uint64_t stream_len, co
                                 c->crc_load, c->stream));
 }
 
+// Filter inserts: the range-privatised build (bloom.hip) for batches of at least
+// 4096 keys when its scratch applies, else one device atomicOr per bit.
+static int bloom_insert(nkv_ctx* c, int mode, const uint8_t* base, const uint64_t* off, const uint64_t* len,
+                        uint64_t stream_len, uint64_t n, uint32_t m, uint32_t k, uint32_t seed0, uint32_t* bits,
+                        unsigned int* err) {
+    const uint64_t words = c->bloom_path == 1 && n >= 4096 ? bloom_ranges_scratch_words(n, m, k) : 0;
+    if (words) {
+        TRY(grow(c->d_tmp, 4 * words));
+        return st(launch_bloom_ranges(mode, base, off, len, stream_len, n, m, k, seed0, bits, err,
+                                      static_cast<uint32_t*>(c->d_tmp.p), c->stream));
+    }
+    return st(launch_bloom(mode, false, base, off, len, stream_len, n, m, k, seed0, bits, nullptr, err, c->stream));
+}
+
 int nkv_bloom_insert_dev(nkv_ctx* c, const void* d_keys, const uint64_t* d_off, const uint64_t* d_len, uint64_t n,
                          uint32_t m, uint32_t k, uint32_t seed0, void* d_bits) {
     TRY(bind(c));
     if (m == 0 || !d_bits) return NKV_ERR_INVALID;
     if (n == 0) return NKV_OK;
     if (!d_keys || !d_off || !d_len) return NKV_ERR_INVALID;
-    return st(launch_bloom(0, false, static_cast<const uint8_t*>(d_keys), d_off, d_len, 0, n, m, k, seed0,
-                           static_cast<uint32_t*>(d_bits), nullptr, nullptr, c->stream));
+    return bloom_insert(c, 0, static_cast<const uint8_t*>(d_keys), d_off, d_len, 0, n, m, k, seed0,
+                        static_cast<uint32_t*>(d_bits), nullptr);
 }
 
 int nkv_bloom_insert_records_dev(nkv_ctx* c, const void* d_stream, uint64_t stream_len, const uint64_t* d_rec_off,
@@ -968,8 +987,8 @@ int nkv_bloom_insert_records_dev(nkv_ctx* c, const void* d_stream, uint64_t stre
     TRY(grow(c->d_err, 4));
     unsigned int* err = static_cast<unsigned int*>(c->d_err.p);
     HIPTRY(hipMemsetAsync(err, 0, 4, c->stream));
-    HIPTRY(launch_bloom(1, false, static_cast<const uint8_t*>(d_stream), d_rec_off, nullptr, stream_len, n, m, k,
-                        seed0, static_cast<uint32_t*>(d_bits), nullptr, err, c->stream));
+    TRY(bloom_insert(c, 1, static_cast<const uint8_t*>(d_stream), d_rec_off, nullptr, stream_len, n, m, k, seed0,
+                     static_cast<uint32_t*>(d_bits), err));
     unsigned int h = 0;
     HIPTRY(hipMemcpyAsync(&h, err, 4, hipMemcpyDeviceToHost, c->stream));
     HIPTRY(hipStreamSynchronize(c->stream));

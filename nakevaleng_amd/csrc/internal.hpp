@@ -66,6 +66,9 @@ hipError_t launch_locate(const uint8_t* stream, uint64_t stream_len, const uint6
                          hipStream_t s);
 hipError_t scan_exclusive_u64(const uint64_t* in, uint64_t* out, uint64_t n, void* tmp,
                               size_t* tmp_bytes, hipStream_t s);
+// In-place exclusive scan of n u32 (gated); sums: scan_sums_words(n) u32.
+uint64_t scan_sums_words(uint64_t n);
+hipError_t scan_exclusive_u32(uint32_t* a, uint64_t n, uint32_t* sums, hipStream_t s, Gate gate = Gate{});
 // Length-sorted order (compression count, longest first) into perm[0..n);
 // hist: sort_hist_words(n) u32 of scratch.
 uint64_t sort_hist_words(uint64_t n);
@@ -84,6 +87,12 @@ hipError_t launch_record_crc(const uint8_t* stream, uint64_t stream_len, const u
 hipError_t launch_bloom(int mode, bool query, const uint8_t* base, const uint64_t* off, const uint64_t* len,
                         uint64_t stream_len, uint64_t n, uint32_t m, uint32_t k, uint32_t seed0, uint32_t* bits,
                         uint8_t* out, unsigned int* err, hipStream_t s);
+// Range-privatised insert (mode as launch_bloom); scratch: bloom_ranges_scratch_words
+// u32 (0 = not applicable: more than 4096 ranges of 32768 bits, or n * k >= 2^32).
+uint64_t bloom_ranges_scratch_words(uint64_t n, uint32_t m, uint32_t k);
+hipError_t launch_bloom_ranges(int mode, const uint8_t* base, const uint64_t* off, const uint64_t* len,
+                               uint64_t stream_len, uint64_t n, uint32_t m, uint32_t k, uint32_t seed0,
+                               uint32_t* bits, unsigned int* err, uint32_t* scratch, hipStream_t s);
 hipError_t launch_fill(uint8_t* buf, uint64_t nbytes, uint64_t seed, hipStream_t s);
 // out[0] / out[1] = min / max of len[i] / 64 over the batch (2 u32 on the device)
 hipError_t launch_len_range(const uint64_t* len, uint64_t n, unsigned int* out, hipStream_t s);

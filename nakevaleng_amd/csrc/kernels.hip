@@ -959,7 +959,7 @@ __device__ __forceinline__ uint32_t len_bucket_desc(uint64_t len) {
 }
 
 __global__ __launch_bounds__(kBlock) void k_len_hist(const uint64_t* __restrict__ len, uint64_t n,
-                                                      uint32_t* __restrict__ hist, Gate gate) {
+                                                      uint32_t* __restrict__ hist, uint32_t tiles, Gate gate) {
     __shared__ uint32_t h[kLenBuckets];
     if (!gate.open()) return;
     for (uint32_t i = threadIdx.x; i < kLenBuckets; i += kBlock) h[i] = 0u;
@@ -971,40 +971,17 @@ __global__ __launch_bounds__(kBlock) void k_len_hist(const uint64_t* __restrict_
         if (i < n) atomicAdd(&h[len_bucket_desc(len[i])], 1u);
     }
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < kLenBuckets; i += kBlock) hist[uint64_t(blockIdx.x) * kLenBuckets + i] = h[i];
-}
-
-// hist[t][k] -> first output position of tile t's bucket-k values
-__global__ __launch_bounds__(1024) void k_len_scan(uint32_t* __restrict__ hist, uint32_t tiles, Gate gate) {
-    __shared__ uint32_t tot[1024];
-    if (!gate.open()) return;
-    const uint32_t k = threadIdx.x;
-    uint32_t sum = 0;
-    if (k < kLenBuckets)
-        for (uint32_t t = 0; t < tiles; ++t) {
-            const uint32_t v = hist[uint64_t(t) * kLenBuckets + k];
-            hist[uint64_t(t) * kLenBuckets + k] = sum;
-            sum += v;
-        }
-    tot[k] = sum;
-    __syncthreads();
-    for (uint32_t o = 1; o < 1024; o <<= 1) {  // inclusive scan of the bucket totals
-        const uint32_t v = k >= o ? tot[k - o] : 0u;
-        __syncthreads();
-        tot[k] += v;
-        __syncthreads();
-    }
-    const uint32_t base = tot[k] - sum;
-    if (k < kLenBuckets && base)
-        for (uint32_t t = 0; t < tiles; ++t) hist[uint64_t(t) * kLenBuckets + k] += base;
+    // bucket-major: the exclusive scan of hist is then every (bucket, tile)
+    // slot's first output position
+    for (uint32_t i = threadIdx.x; i < kLenBuckets; i += kBlock) hist[uint64_t(i) * tiles + blockIdx.x] = h[i];
 }
 
 __global__ __launch_bounds__(kBlock) void k_len_scatter(const uint64_t* __restrict__ len, uint64_t n,
-                                                         const uint32_t* __restrict__ hist,
+                                                         const uint32_t* __restrict__ hist, uint32_t tiles,
                                                          uint32_t* __restrict__ perm, Gate gate) {
     __shared__ uint32_t cur[kLenBuckets];
     if (!gate.open()) return;
-    for (uint32_t i = threadIdx.x; i < kLenBuckets; i += kBlock) cur[i] = hist[uint64_t(blockIdx.x) * kLenBuckets + i];
+    for (uint32_t i = threadIdx.x; i < kLenBuckets; i += kBlock) cur[i] = hist[uint64_t(i) * tiles + blockIdx.x];
     __syncthreads();
     const uint64_t base = uint64_t(blockIdx.x) * kSortTile;
 #pragma unroll 4
@@ -1301,15 +1278,108 @@ extern "C" int nkv_diag_set_buffer(void* d) {
 }
 #endif
 
-uint64_t sort_hist_words(uint64_t n) { return ((n + kSortTile - 1) / kSortTile) * kLenBuckets; }
+// ---------------------------------------------------------------------------
+// In-place exclusive scan of u32 (gated): per-tile sums, one block scans the
+// sums, each tile scans itself plus its offset.  a holds n + 1 words when the
+// total is wanted (a zero appended).
+constexpr int kScanItems = 8;
+constexpr uint64_t kScanTile = uint64_t(kBlock) * kScanItems;
+
+// exclusive scan of v over the workgroup (thread order); returns the total
+__device__ __forceinline__ uint32_t block_exclusive(uint32_t& v) {
+    __shared__ uint32_t wsum[kBlock / 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = uint32_t(__shfl_up(int(x), o));
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    uint32_t before = 0, total = 0;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) {
+        if (w < wave) before += wsum[w];
+        total += wsum[w];
+    }
+    __syncthreads();
+    v = before + x - v;
+    return total;
+}
+
+__global__ __launch_bounds__(kBlock) void k_scan_sums(const uint32_t* __restrict__ a, uint64_t n,
+                                                       uint32_t* __restrict__ sums, Gate gate) {
+    if (!gate.open()) return;
+    const uint64_t base = uint64_t(blockIdx.x) * kScanTile + uint64_t(threadIdx.x) * kScanItems;
+    uint32_t s = 0;
+#pragma unroll
+    for (int j = 0; j < kScanItems; ++j)
+        if (base + j < n) s += a[base + j];
+    uint32_t v = s;
+    const uint32_t tot = block_exclusive(v);
+    if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(kBlock) void k_scan_top(uint32_t* __restrict__ sums, uint32_t nt, Gate gate) {
+    if (!gate.open()) return;
+    uint32_t carry = 0;
+    for (uint32_t b = 0; b < nt; b += kBlock) {  // one workgroup, kBlock sums per round
+        uint32_t v = b + threadIdx.x < nt ? sums[b + threadIdx.x] : 0u;
+        const uint32_t tot = block_exclusive(v);
+        if (b + threadIdx.x < nt) sums[b + threadIdx.x] = carry + v;
+        carry += tot;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_scan_down(uint32_t* __restrict__ a, uint64_t n,
+                                                       const uint32_t* __restrict__ sums, Gate gate) {
+    if (!gate.open()) return;
+    const uint64_t base = uint64_t(blockIdx.x) * kScanTile + uint64_t(threadIdx.x) * kScanItems;
+    uint32_t x[kScanItems];
+    uint32_t s = 0;
+#pragma unroll
+    for (int j = 0; j < kScanItems; ++j) {
+        x[j] = base + j < n ? a[base + j] : 0u;
+        s += x[j];
+    }
+    uint32_t v = s;
+    (void)block_exclusive(v);
+    uint32_t run = sums[blockIdx.x] + v;
+#pragma unroll
+    for (int j = 0; j < kScanItems; ++j) {
+        if (base + j < n) a[base + j] = run;
+        run += x[j];
+    }
+}
+
+uint64_t scan_sums_words(uint64_t n) { return (n + kScanTile - 1) / kScanTile; }
+
+hipError_t scan_exclusive_u32(uint32_t* a, uint64_t n, uint32_t* sums, hipStream_t s, Gate gate) {
+    const uint64_t nt = scan_sums_words(n);
+    if (nt == 0) return hipSuccess;
+    if (nt > 0xFFFFFFFFull) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_scan_sums, dim3(uint32_t(nt)), dim3(kBlock), 0, s, a, n, sums, gate);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kBlock), 0, s, sums, uint32_t(nt), gate);
+    hipLaunchKernelGGL(k_scan_down, dim3(uint32_t(nt)), dim3(kBlock), 0, s, a, n, sums, gate);
+    return hipGetLastError();
+}
+
+uint64_t sort_hist_words(uint64_t n) {
+    const uint64_t h = ((n + kSortTile - 1) / kSortTile) * kLenBuckets;
+    return h + scan_sums_words(h);
+}
 
 hipError_t sort_by_length_desc(const uint64_t* len, uint64_t n, uint32_t* perm, uint32_t* hist, hipStream_t s,
                                Gate gate) {
     const uint64_t tiles = (n + kSortTile - 1) / kSortTile;
     if (tiles == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_len_hist, dim3(uint32_t(tiles)), dim3(kBlock), 0, s, len, n, hist, gate);
-    hipLaunchKernelGGL(k_len_scan, dim3(1), dim3(1024), 0, s, hist, uint32_t(tiles), gate);
-    hipLaunchKernelGGL(k_len_scatter, dim3(uint32_t(tiles)), dim3(kBlock), 0, s, len, n, hist, perm, gate);
+    const uint64_t h = tiles * kLenBuckets;
+    hipLaunchKernelGGL(k_len_hist, dim3(uint32_t(tiles)), dim3(kBlock), 0, s, len, n, hist, uint32_t(tiles), gate);
+    hipError_t e = scan_exclusive_u32(hist, h, hist + h, s, gate);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_len_scatter, dim3(uint32_t(tiles)), dim3(kBlock), 0, s, len, n, hist, uint32_t(tiles),
+                       perm, gate);
     return hipGetLastError();
 }
 

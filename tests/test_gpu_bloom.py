@@ -134,3 +134,57 @@ def test_bloom_sstable_shape_1m_keys(nkv, oracle):
     torch.cuda.synchronize()
     want = oracle.bloom_insert(data, off, ln, m, k, 0xABCD1234)
     assert np.array_equal(d_bits.cpu().numpy()[:want.size], want)
+
+
+@pytest.mark.parametrize("path", [0, 1])
+@pytest.mark.parametrize("n,m,k", [(5000, 47924, 7), (4096, 1, 1), (20000, 5000, 20), (70000, 1 << 22, 3),
+                                   (9000, 134217728, 2)])
+def test_bloom_insert_paths_match_oracle(nkv, oracle, path, n, m, k):
+    """Both insert paths -- range-privatised (32768-bit ranges in LDS, counting
+    sort of the updates) and one atomicOr per bit -- on filters of 1 bit to
+    4096 ranges, k up to 20 (two register passes), ragged keys, bits OR-ed into
+    a non-empty filter."""
+    torch = _torch()
+    _lib, _ = nkv
+    ctx = _lib.Context(0)
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    ctx.set_option(_lib.NKV_OPT_BLOOM_PATH, path)
+    L = _lib.lib()
+    rng = np.random.default_rng(n + m + k)
+    data, off, ln = _keys(rng, n)
+    seed0 = int(rng.integers(0, 2**32))
+    words = ((m + 31) // 32) * 4
+    pre = np.zeros(words, np.uint8)
+    pre[: (m + 7) // 8] = rng.integers(0, 256, (m + 7) // 8, dtype=np.uint8) & rng.integers(0, 2, (m + 7) // 8,
+                                                                                          dtype=np.uint8)
+    if m % 8:
+        pre[(m + 7) // 8 - 1] &= (1 << (m % 8)) - 1
+    d_bits = _dev(torch, pre)
+    d_data, d_off, d_len = _dev(torch, data), _dev(torch, off), _dev(torch, ln)
+    try:
+        _lib.check(L.nkv_bloom_insert_dev(ctx.h, d_data.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n, m, k,
+                                          seed0, d_bits.data_ptr()))
+        torch.cuda.synchronize()
+    finally:
+        ctx.close()
+    got = d_bits.cpu().numpy()
+    want = oracle.bloom_insert(data, off, ln, m, k, seed0) | pre[: (m + 7) // 8]
+    assert np.array_equal(got[:want.size], want)
+    assert not got[want.size:].any()
+
+
+def test_bloom_from_records_range_path(nkv, oracle):
+    """The records form (keys at rec + 30) through the range-privatised path."""
+    from nakevaleng_amd import record, sstable
+    _lib, ctx = nkv
+    rng = np.random.default_rng(44)
+    recs = [record.New(rng.integers(0, 256, int(kk), dtype=np.uint8).tobytes(), b"v" * int(v), timestamp=1)
+            for kk, v in zip(rng.integers(1, 40, 6000), rng.integers(0, 50, 6000))]
+    stream, sizes = record.data_table(recs)
+    bf = sstable.make_filter_from_records(stream, sizes, seed=99, ctx=ctx)
+    keys = [r.Key for r in recs]
+    kd = np.frombuffer(b"".join(keys), np.uint8)
+    kl = np.array([len(x) for x in keys], np.uint64)
+    ko = np.zeros_like(kl)
+    ko[1:] = np.cumsum(kl[:-1])
+    assert bf.Contents == oracle.bloom_insert(kd, ko, kl, bf.M, bf.K, 99).tobytes()
