@@ -291,13 +291,12 @@ int plan_of(nkv_ctx* c, const uint64_t* len, const uint64_t* host_len, uint64_t 
 }
 
 // Level 0 in the order plan_of chose.  Gated plans also launch the input-order
-// kernel (it runs when the range is narrow), fused with levels 1..min(top, 6)
-// when narrow_top > 0.
+// kernel (it runs when the range is narrow).
 int leaf_level(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint64_t* len, uint64_t n,
-               bool aligned, uint8_t* nodes, int plan, Gate range, int narrow_top = 0) {
+               bool aligned, uint8_t* nodes, int plan, Gate range) {
     if (plan == kInputOrder)
-        return st(launch_leaf_offsets(base, off, len, nullptr, n, 0, false, aligned, c->leaf_load, nodes,
-                                      c->stream, c->deep != 0));
+        return st(launch_leaf_offsets(base, off, len, nullptr, n, aligned, c->leaf_load, nodes, c->stream,
+                                      c->deep != 0));
     if (n > 0x7fffffffull) return NKV_ERR_INVALID;
     const Gate wide{range.range, plan == kGated ? 2 : 0};
     TRY(grow(c->d_keys, 4 * sort_hist_words(n)));
@@ -314,12 +313,12 @@ int leaf_level(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint6
         HIPTRY(launch_leaf_queue(base, off, len, perm, n, aligned, ring, static_cast<uint32_t*>(c->d_queue.p),
                                  c->simds, uint32_t(waves), uint32_t(c->queue_split), nodes, c->stream, wide));
     } else {
-        HIPTRY(launch_leaf_offsets(base, off, len, perm, n, 0, false, aligned, c->leaf_load, nodes, c->stream,
-                                   c->deep != 0, wide));
+        HIPTRY(launch_leaf_offsets(base, off, len, perm, n, aligned, c->leaf_load, nodes, c->stream, c->deep != 0,
+                                   wide));
     }
     if (plan == kGated)
-        HIPTRY(launch_leaf_offsets(base, off, len, nullptr, n, narrow_top, narrow_top > 0, aligned, c->leaf_load,
-                                   nodes, c->stream, c->deep != 0, Gate{range.range, 1}));
+        HIPTRY(launch_leaf_offsets(base, off, len, nullptr, n, aligned, c->leaf_load, nodes, c->stream,
+                                   c->deep != 0, Gate{range.range, 1}));
     return NKV_OK;
 }
 
@@ -332,31 +331,16 @@ int leaf_level(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint6
 }
 
 // host_len (nullable): the value lengths on the host, when the caller has them.
+// Every order leaves level 0 complete, so one reduce sequence follows.
 int tree_from_device_values(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint64_t* len,
                             uint64_t n, bool aligned, uint8_t* nodes, const uint64_t* host_len = nullptr) {
-    const int top = levels_of(n) - 1;
     int plan = kInputOrder;
     Gate g;
     TRY(plan_of(c, len, host_len, n, &plan, &g));
     TRY(mark(c, 0));
-    if (plan == kGated) {
-        // sorted (wide range) or input order with fused levels (narrow), picked
-        // on the device; each reduce sequence runs for its own branch only
-        TRY(leaf_level(c, base, off, len, n, aligned, nodes, plan, g, top));
-        TRY(mark(c, 1));
-        HIPTRY(launch_reduce(nodes, n, 0, top, c->stream, Gate{g.range, 2}));
-        HIPTRY(launch_reduce(nodes, n, std::min(top, kWaveLevels), top, c->stream, Gate{g.range, 1}));
-    } else if (plan == kSorted) {
-        // a permuted wave does not own a subtree: reduce everything from level 0
-        TRY(leaf_level(c, base, off, len, n, aligned, nodes, plan, g));
-        TRY(mark(c, 1));
-        HIPTRY(launch_reduce(nodes, n, 0, top, c->stream));
-    } else {
-        HIPTRY(launch_leaf_offsets(base, off, len, nullptr, n, top, true, aligned, c->leaf_load, nodes,
-                                   c->stream));
-        TRY(mark(c, 1));
-        HIPTRY(launch_reduce(nodes, n, std::min(top, kWaveLevels), top, c->stream));
-    }
+    TRY(leaf_level(c, base, off, len, n, aligned, nodes, plan, g));
+    TRY(mark(c, 1));
+    HIPTRY(launch_reduce(nodes, n, 0, levels_of(n) - 1, c->stream));
     return mark(c, 2);
 }
 
@@ -827,7 +811,7 @@ int nkv_leaf_hash_strided_dev(nkv_ctx* c, const void* d_base, uint64_t stride, u
     TRY(bind(c));
     if (n == 0) return NKV_OK;
     if (!d_base || !d_nodes) return NKV_ERR_INVALID;
-    return st(launch_leaf_strided(static_cast<const uint8_t*>(d_base), stride, len, n, 0, false,
+    return st(launch_leaf_strided(static_cast<const uint8_t*>(d_base), stride, len, n,
                                   c->leaf_load, static_cast<uint8_t*>(d_nodes), c->stream));
 }
 
@@ -855,10 +839,10 @@ int nkv_tree_from_strided_dev(nkv_ctx* c, const void* d_base, uint64_t stride, u
     uint8_t* nodes = static_cast<uint8_t*>(d_nodes);
     const int top = levels_of(n) - 1;
     TRY(mark(c, 0));
-    HIPTRY(launch_leaf_strided(static_cast<const uint8_t*>(d_base), stride, len, n, top, true,
+    HIPTRY(launch_leaf_strided(static_cast<const uint8_t*>(d_base), stride, len, n,
                                c->leaf_load, nodes, c->stream));
     TRY(mark(c, 1));
-    HIPTRY(launch_reduce(nodes, n, std::min(top, kWaveLevels), top, c->stream));
+    HIPTRY(launch_reduce(nodes, n, 0, top, c->stream));
     return mark(c, 2);
 }
 

@@ -160,6 +160,7 @@ __device__ __forceinline__ uint32_t crc_span_ring(const uint8_t* s, uint64_t len
     issue(1u);
     for (uint32_t c = 0; c < nmax; ++c) {
         const uint8_t* rd = wbuf + 4096 * (c & 1u) + 64 * lane;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // chunk c landed (explicit LDS-DMA wait)
         uint4 v[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) v[i] = *reinterpret_cast<const uint4*>(rd + 16 * (uint32_t(i) ^ swz));

@@ -6,8 +6,13 @@
 namespace nkv {
 
 constexpr int kBlock = 256;       // threads per workgroup = leaves per K1 block
-constexpr int kFuseLevels = 8;    // log2(kBlock): levels one workgroup reduces in LDS
-constexpr int kWaveLevels = 6;    // log2(64): levels the leaf kernel's waves reduce by shuffles
+constexpr int kSlabLevels = 8;    // log2(kBlock): levels one k_reduce workgroup builds
+#ifndef NKV_REDUCE2_MIN
+#define NKV_REDUCE2_MIN 65536
+#endif
+// levels of at least this many nodes are reduced two at a time at full lane
+// use (k_reduce2) before the 8-level slabs take over
+constexpr uint64_t kReduce2Min = NKV_REDUCE2_MIN;
 constexpr int kMaxLevels = 64;
 #ifndef NKV_LEAF_WAVES
 #define NKV_LEAF_WAVES 8
@@ -42,11 +47,12 @@ struct BfsLayout {
 // direct 128 / 256-B runs); direct loads need 16-byte aligned values, so
 // unaligned batches take LDS-DMA from the values' own addresses (8) for load 1
 // and the register funnel (0) otherwise.
-hipError_t launch_leaf_strided(const uint8_t* base, uint64_t stride, uint64_t L, uint64_t n,
-                               int top, bool fuse, int load, uint8_t* nodes, hipStream_t s);
+// Level 0 (the leaf digests) only; launch_reduce builds the levels above.
+hipError_t launch_leaf_strided(const uint8_t* base, uint64_t stride, uint64_t L, uint64_t n, int load,
+                               uint8_t* nodes, hipStream_t s);
 hipError_t launch_leaf_offsets(const uint8_t* base, const uint64_t* off, const uint64_t* len,
-                               const uint32_t* perm, uint64_t n, int top, bool fuse, bool aligned,
-                               int load, uint8_t* nodes, hipStream_t s, bool deep = true, Gate gate = Gate{});
+                               const uint32_t* perm, uint64_t n, bool aligned, int load, uint8_t* nodes,
+                               hipStream_t s, bool deep = true, Gate gate = Gate{});
 // Ragged batch through the work-queue leaf kernel (perm = length-sorted order,
 // longest first); q must hold queue_words(n) u32; split = longest chain (full
 // blocks) of a group the non-priority waves take when the longest chain bounds

@@ -116,40 +116,6 @@ __device__ __forceinline__ void subtree_reduce(uint32_t (*lds)[kBlock], uint64_t
     }
 }
 
-// Subtree reduce inside one wavefront, no workgroup barrier: lane t holds
-// (state words of) node lo + t of level 0, t < 64; levels 1..jmax (<= 6) are
-// built with cross-lane shuffles and written to the global nodes buffer.
-// Used as the leaf kernel's epilogue so a finished wave never waits for the
-// other waves of its workgroup.
-__device__ __forceinline__ void wave_reduce(uint32_t h[5], uint64_t n, int jmax, uint64_t lo,
-                                            uint8_t* nodes) {
-    const int lane = threadIdx.x & 63;
-    uint64_t nprev = n;
-    uint64_t start_cur = n;
-    uint64_t lo_prev = lo;
-    int span = 64;
-    for (int j = 1; j <= jmax; ++j) {
-        const uint64_t ncur = ((nprev - 1) >> 1) + 1;
-        const uint64_t lo_cur = lo_prev >> 1;
-        span >>= 1;
-        const int src = (2 * lane) & 63;
-        uint32_t l[5], r[5];
-#pragma unroll
-        for (int k = 0; k < 5; ++k) {
-            l[k] = uint32_t(__shfl(int(h[k]), src));
-            r[k] = uint32_t(__shfl(int(h[k]), src + 1));
-        }
-        if (lane < span && lo_cur + lane < ncur) {
-            const bool lone = (2 * (lo_cur + lane) + 1) >= nprev;
-            sha1_parent(l, r, lone, h);
-            store_digest(nodes, start_cur + lo_cur + lane, h);
-        }
-        nprev = ncur;
-        start_cur += ncur;
-        lo_prev = lo_cur;
-    }
-}
-
 // ---------------------------------------------------------------------------
 // K1: leaf SHA-1.
 //
@@ -324,6 +290,10 @@ __device__ __forceinline__ void sha1_blocks_lds(const uint8_t* wbuf, uint32_t nm
     if (nmax == 0) return;
     issue(0u);
     for (uint32_t b = 0; b < nmax; ++b) {
+        // block b's DMA has landed.  Explicit: the compiler's own LDS-DMA wait
+        // depends on its alias analysis of the stage (a second __shared__
+        // object in the kernel once made it drop this wait).
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         uint4 c[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) c[q] = rd[q ^ swz];
@@ -485,6 +455,7 @@ __device__ __forceinline__ void sha1_blocks_ring(uint8_t* wbuf, const uint8_t* p
     issue(1u);
     for (uint32_t b = 0; b < nmax; ++b) {
         const uint32_t flip = (b & 1u) << 12;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // chunks b, b+1 landed (explicit, see sha1_blocks_lds)
         uint32_t d[20];
 #pragma unroll
         for (int i = 0; i < 5; ++i) {
@@ -689,15 +660,19 @@ __device__ __forceinline__ void sha1_blocks_ring_vc(uint8_t* wbuf, const uint8_t
 
 // MODE 0: value i at base + i*stride, length L.  MODE 1: base + off[i], len[i].
 // perm (MODE 1 only, nullable): lane i hashes leaf perm[i] (length bucketing).
-// FUSE: also build levels 1..min(8, top) of this block's subtree.
+// No tree level is fused here: a wave-level step costs a whole SHA-1
+// instruction stream however few lanes it keeps, so levels built inside the
+// leaf kernel (6 per wave, or the workgroup's last wave finishing its 256-leaf
+// subtree) cost 3-7 % of a 4 KiB leaf launch, more than k_reduce2 at full lane
+// use plus its launch.
 // LOAD: 0 = any alignment (register funnel); 1 = 16-byte aligned, LDS-DMA
 // stage; 2 = aligned, direct loads; 3 = aligned, direct non-temporal loads.
-template <int MODE, bool FUSE, int LOAD>
+template <int MODE, int LOAD>
 __global__ __launch_bounds__(kBlock, (LOAD == 6 || LOAD == 7) ? 2 : ((LOAD == 4 || LOAD == 5) ? 4 : kLeafWavesPerSimd)) void k_leaf(const uint8_t* __restrict__ base,
                                                   const uint64_t* __restrict__ off,
                                                   const uint64_t* __restrict__ len, uint64_t stride,
                                                   uint64_t L, const uint32_t* __restrict__ perm,
-                                                  uint64_t n, int top, uint8_t* __restrict__ nodes, Gate gate) {
+                                                  uint64_t n, uint8_t* __restrict__ nodes, Gate gate) {
     // 16 KiB: four wave-private 4 KiB LDS-DMA stages (LOAD == 1)
     __shared__ __attribute__((aligned(16))) uint8_t smem[kBlock * 64];
     if (!gate.open()) return;
@@ -787,10 +762,6 @@ __global__ __launch_bounds__(kBlock, (LOAD == 6 || LOAD == 7) ? 2 : ((LOAD == 4 
         store_digest(nodes, leaf, h);
     }
     NKV_STAMP(1);
-    if (FUSE) {
-        const int jmax = top < kWaveLevels ? top : kWaveLevels;
-        wave_reduce(h, n, jmax, g * kBlock + 64 * (threadIdx.x >> 6), nodes);
-    }
     NKV_STAMP(2);
 #ifdef NKV_DIAG
     if (g_diag && (threadIdx.x & 63) == 0) {
@@ -936,6 +907,54 @@ __global__ __launch_bounds__(kBlock) void k_reduce(uint8_t* __restrict__ nodes, 
 #pragma unroll
     for (int k = 0; k < 5; ++k) lds[k][threadIdx.x] = h[k];
     subtree_reduce(lds, n, j0, jmax, lo, nodes);
+}
+
+// K2w: the wide bottom levels at full lane use.  A wavefront takes 256 nodes
+// of level j0: their 128 parents (two per lane), then those parents' 64
+// parents (one per lane) when jmax >= j0 + 2.  A k_reduce slab runs 8 levels
+// but keeps at most half a wave busy past its first two, while the two bottom
+// levels hold three quarters of all parents: 3 wave-compressions per 256 nodes
+// here against 9 there.
+__global__ __launch_bounds__(kBlock) void k_reduce2(uint8_t* __restrict__ nodes, uint64_t n, int j0, int jmax,
+                                                     Gate gate) {
+    if (!gate.open()) return;
+    const int lane = threadIdx.x & 63;
+    const uint64_t w = uint64_t(blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6);
+    const uint64_t n0 = lvl_count(n, j0), s0 = lvl_start(n, j0);
+    const uint64_t n1 = ((n0 - 1) >> 1) + 1, s1 = s0 + n0;
+    uint32_t hp[2][5];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+#pragma unroll
+        for (int k = 0; k < 5; ++k) hp[p][k] = 0u;
+        const uint64_t i1 = 128 * w + uint64_t(lane) + 64 * p;
+        if (i1 < n1) {
+            const bool lone = 2 * i1 + 1 >= n0;
+            uint32_t l[5], r[5] = {0u, 0u, 0u, 0u, 0u};
+            load_digest(nodes, s0 + 2 * i1, l);
+            if (!lone) load_digest(nodes, s0 + 2 * i1 + 1, r);
+            sha1_parent(l, r, lone, hp[p]);
+            store_digest(nodes, s1 + i1, hp[p]);
+        }
+    }
+    if (jmax < j0 + 2) return;
+    const uint64_t n2 = ((n1 - 1) >> 1) + 1, s2 = s1 + n1;
+    const uint64_t i2 = 64 * w + uint64_t(lane);
+    // children 2 lane, 2 lane + 1 of this wave's 128: pass 0 for lane < 32
+    const int src = (2 * lane) & 63;
+    uint32_t l[5], r[5], h[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        const uint32_t l0 = uint32_t(__shfl(int(hp[0][k]), src)), l1 = uint32_t(__shfl(int(hp[1][k]), src));
+        const uint32_t r0 = uint32_t(__shfl(int(hp[0][k]), src + 1)), r1 = uint32_t(__shfl(int(hp[1][k]), src + 1));
+        l[k] = lane < 32 ? l0 : l1;
+        r[k] = lane < 32 ? r0 : r1;
+    }
+    if (i2 < n2) {
+        const bool lone = 2 * i2 + 1 >= n1;
+        sha1_parent(l, r, lone, h);
+        store_digest(nodes, s2 + i2, h);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1136,47 +1155,44 @@ __global__ __launch_bounds__(kBlock) void k_fill(uint8_t* __restrict__ buf, uint
 
 static inline unsigned grid_for(uint64_t n) { return unsigned((n + kBlock - 1) / kBlock); }
 
-template <int MODE, bool FUSE, int LOAD>
-static void leaf_kernel(const uint8_t* base, const uint64_t* off, const uint64_t* len,
-                        uint64_t stride, uint64_t L, const uint32_t* perm, uint64_t n, int top,
-                        uint8_t* nodes, hipStream_t s, Gate gate) {
-    hipLaunchKernelGGL((k_leaf<MODE, FUSE, LOAD>), dim3(grid_for(n)), dim3(kBlock), 0, s, base,
-                       off, len, stride, L, perm, n, top, nodes, gate);
+template <int MODE, int LOAD>
+static void leaf_kernel(const uint8_t* base, const uint64_t* off, const uint64_t* len, uint64_t stride, uint64_t L,
+                        const uint32_t* perm, uint64_t n, uint8_t* nodes, hipStream_t s, Gate gate) {
+    hipLaunchKernelGGL((k_leaf<MODE, LOAD>), dim3(grid_for(n)), dim3(kBlock), 0, s, base, off, len, stride, L,
+                       perm, n, nodes, gate);
 }
 
-template <int MODE, bool FUSE>
+template <int MODE>
 static void leaf_dispatch(int load, const uint8_t* base, const uint64_t* off, const uint64_t* len,
-                          uint64_t stride, uint64_t L, const uint32_t* perm, uint64_t n, int top,
-                          uint8_t* nodes, hipStream_t s, Gate g) {
+                          uint64_t stride, uint64_t L, const uint32_t* perm, uint64_t n, uint8_t* nodes,
+                          hipStream_t s, Gate g) {
     switch (load) {
-        case 1: leaf_kernel<MODE, FUSE, 1>(base, off, len, stride, L, perm, n, top, nodes, s, g); break;
-        case 2: leaf_kernel<MODE, FUSE, 2>(base, off, len, stride, L, perm, n, top, nodes, s, g); break;
-        case 3: leaf_kernel<MODE, FUSE, 3>(base, off, len, stride, L, perm, n, top, nodes, s, g); break;
-        case 4: leaf_kernel<MODE, FUSE, 4>(base, off, len, stride, L, perm, n, top, nodes, s, g); break;
-        case 5: leaf_kernel<MODE, FUSE, 5>(base, off, len, stride, L, perm, n, top, nodes, s, g); break;
-        case 6: leaf_kernel<MODE, FUSE, 6>(base, off, len, stride, L, perm, n, top, nodes, s, g); break;
-        case 7: leaf_kernel<MODE, FUSE, 7>(base, off, len, stride, L, perm, n, top, nodes, s, g); break;
-        case 8: leaf_kernel<MODE, FUSE, 8>(base, off, len, stride, L, perm, n, top, nodes, s, g); break;
-        default: leaf_kernel<MODE, FUSE, 0>(base, off, len, stride, L, perm, n, top, nodes, s, g); break;
+        case 1: leaf_kernel<MODE, 1>(base, off, len, stride, L, perm, n, nodes, s, g); break;
+        case 2: leaf_kernel<MODE, 2>(base, off, len, stride, L, perm, n, nodes, s, g); break;
+        case 3: leaf_kernel<MODE, 3>(base, off, len, stride, L, perm, n, nodes, s, g); break;
+        case 4: leaf_kernel<MODE, 4>(base, off, len, stride, L, perm, n, nodes, s, g); break;
+        case 5: leaf_kernel<MODE, 5>(base, off, len, stride, L, perm, n, nodes, s, g); break;
+        case 6: leaf_kernel<MODE, 6>(base, off, len, stride, L, perm, n, nodes, s, g); break;
+        case 7: leaf_kernel<MODE, 7>(base, off, len, stride, L, perm, n, nodes, s, g); break;
+        case 8: leaf_kernel<MODE, 8>(base, off, len, stride, L, perm, n, nodes, s, g); break;
+        default: leaf_kernel<MODE, 0>(base, off, len, stride, L, perm, n, nodes, s, g); break;
     }
 }
 
-hipError_t launch_leaf_strided(const uint8_t* base, uint64_t stride, uint64_t L, uint64_t n,
-                               int top, bool fuse, int load, uint8_t* nodes, hipStream_t s) {
+hipError_t launch_leaf_strided(const uint8_t* base, uint64_t stride, uint64_t L, uint64_t n, int load,
+                               uint8_t* nodes, hipStream_t s) {
     const bool al = ((reinterpret_cast<uintptr_t>(base) | stride) & 15) == 0;
     if (!al) load = load == 1 ? 8 : 0;  // LDS-DMA serves any alignment; direct loads need 16 B
-    if (fuse) leaf_dispatch<0, true>(load, base, nullptr, nullptr, stride, L, nullptr, n, top, nodes, s, Gate{});
-    else leaf_dispatch<0, false>(load, base, nullptr, nullptr, stride, L, nullptr, n, top, nodes, s, Gate{});
+    leaf_dispatch<0>(load, base, nullptr, nullptr, stride, L, nullptr, n, nodes, s, Gate{});
     return hipGetLastError();
 }
 
 hipError_t launch_leaf_offsets(const uint8_t* base, const uint64_t* off, const uint64_t* len,
-                               const uint32_t* perm, uint64_t n, int top, bool fuse, bool aligned,
-                               int load, uint8_t* nodes, hipStream_t s, bool deep, Gate gate) {
+                               const uint32_t* perm, uint64_t n, bool aligned, int load, uint8_t* nodes,
+                               hipStream_t s, bool deep, Gate gate) {
     if (perm && deep) load = aligned ? 6 : 7;  // ragged, length-sorted: deep prefetch
     else if (!aligned) load = load == 1 ? 8 : 0;  // LDS-DMA serves any alignment
-    if (fuse && !perm) leaf_dispatch<1, true>(load, base, off, len, 0, 0, nullptr, n, top, nodes, s, gate);
-    else leaf_dispatch<1, false>(load, base, off, len, 0, 0, perm, n, top, nodes, s, gate);
+    leaf_dispatch<1>(load, base, off, len, 0, 0, perm, n, nodes, s, gate);
     return hipGetLastError();
 }
 
@@ -1240,8 +1256,18 @@ uint64_t queue_words(uint64_t n) { return kQueueHeader + kSimdKeys + (n + 63) / 
 
 hipError_t launch_reduce(uint8_t* nodes, uint64_t n, int from_level, int top, hipStream_t s, Gate gate) {
     int j0 = from_level;
+    // wide levels two at a time (k_reduce2), then 8-level slabs
+    for (uint64_t cnt = j0 == 0 ? n : ((n - 1) >> j0) + 1; top - j0 >= 2 && cnt >= kReduce2Min;
+         cnt = ((cnt - 1) >> 2) + 1) {
+        const uint64_t waves = (cnt + 255) / 256;
+        hipLaunchKernelGGL(k_reduce2, dim3(unsigned((waves + 3) / 4)), dim3(kBlock), 0, s, nodes, n, j0, j0 + 2,
+                           gate);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        j0 += 2;
+    }
     while (j0 < top) {
-        const int jmax = (j0 + kFuseLevels < top) ? j0 + kFuseLevels : top;
+        const int jmax = (j0 + kSlabLevels < top) ? j0 + kSlabLevels : top;
         const uint64_t cnt = j0 == 0 ? n : ((n - 1) >> j0) + 1;
         hipLaunchKernelGGL(k_reduce, dim3(grid_for(cnt)), dim3(kBlock), 0, s, nodes, n, j0, jmax, gate);
         hipError_t e = hipGetLastError();

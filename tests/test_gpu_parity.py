@@ -219,9 +219,23 @@ def test_tree_build_from_digests(nkv, oracle, n):
     assert img.tobytes() == oracle.bfs_image(want, n)
 
 
+@pytest.mark.parametrize("n", [131071, 262144, 262145, 524287, 1000003])
+def test_tree_build_wide_levels(nkv, oracle, n):
+    """Levels of >= 64 Ki nodes go through k_reduce2 (two levels per launch,
+    odd counts and lone nodes at both of its levels) before the 8-level slabs."""
+    _lib, ctx = nkv
+    L = _lib.lib()
+    leaf20 = oracle.splitmix64_bytes(20 * n, SEED ^ n)
+    nodes = np.zeros((L.nkv_total_nodes(n), 20), np.uint8)
+    root = np.zeros(20, np.uint8)
+    _lib.check(L.nkv_tree_build(ctx.h, _lib.p8(leaf20), n, _lib.p8(root), _lib.p8(nodes), None))
+    want = oracle.tree_from_digests(leaf20.reshape(n, 20))
+    assert np.array_equal(nodes, want)
+
+
 @pytest.mark.parametrize("n", [1, 2, 3, 255, 256, 257, 511, 513, 1000, 4097, 65537])
-def test_tree_from_values_fused(nkv, oracle, n):
-    """Leaf kernel fused with the first 8 levels, then the level reduce."""
+def test_tree_from_values_host(nkv, oracle, n):
+    """Host API: leaf kernel, then the level reduce, then the image."""
     _lib, ctx = nkv
     L = _lib.lib()
     vlen = 100

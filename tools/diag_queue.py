@@ -30,7 +30,10 @@ def main():
     ctx.set_option(_lib.NKV_OPT_DEEP_PREFETCH, deep)
     qwaves = int(os.environ.get("QWAVES", "4"))
     ctx.set_option(_lib.NKV_OPT_QUEUE_WAVES, qwaves)
-    ctx.set_option(_lib.NKV_OPT_QUEUE_SPLIT, int(os.environ.get("QSPLIT", "256")))
+    ctx.set_option(_lib.NKV_OPT_QUEUE_SPLIT, int(os.environ.get("QSPLIT", "32")))
+    ring = int(os.environ.get("RING", "13"))
+    ctx.set_option(_lib.NKV_OPT_QUEUE_RING, ring)
+    ctx.set_option(_lib.NKV_OPT_BUCKET, 1)
     lens_h, off_h = bench.mixed_lengths(4 << 30, bench.SEED_MIXED)
     n = len(lens_h)
     nbytes = int(lens_h.sum())
@@ -40,7 +43,8 @@ def main():
     _lib.check(L.nkv_fill_splitmix64_dev(ctx.h, data.data_ptr(), nbytes, 1))
     nodes = torch.empty(L.nkv_total_nodes(n) * 20, dtype=torch.uint8, device="cuda")
     simds = torch.cuda.get_device_properties(0).multi_processor_count * 4
-    waves = (qwaves if deep == 3 else 2) * simds
+    slots = ring % 10
+    waves = (min(qwaves, 2 if slots == 4 else (3 if slots == 3 else 5)) if deep == 3 else 2) * simds
     diag = torch.zeros(waves * 8, dtype=torch.int64, device="cuda")
 
     def run():

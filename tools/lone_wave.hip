@@ -1,0 +1,98 @@
+// lone_wave.hip -- cycles per 64-byte block of ONE wave alone on its SIMD,
+// the rate that bounds a ragged batch's longest chain (DESIGN.md section 4,
+// cfg3).  Each 64-thread workgroup hashes 64 values of NBLK full blocks with
+// one of the leaf kernels' block loops; 256 workgroups = one wave per CU.
+// L2 mode: every wave reads the same 64 values (4 MiB at 1,024 blocks);
+// HBM mode: each wave its own.
+//   hipcc --offload-arch=gfx950 -O3 -I nakevaleng_amd/csrc tools/lone_wave.hip -o tools/lone_wave.bin
+#include "../nakevaleng_amd/csrc/kernels.hip"
+
+#include <stdio.h>
+#include <vector>
+
+namespace nkv {
+
+template <int V>
+__global__ __launch_bounds__(64, 1) void k_lone(const uint8_t* __restrict__ base, uint64_t vstride,
+                                                uint32_t nblk, int hbm, unsigned long long* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[4 * 4096];
+    const int lane = threadIdx.x;
+    const uint64_t v = (hbm ? uint64_t(blockIdx.x) * 64 : 0) + uint64_t(lane);
+    const uint8_t* p = base + v * vstride;
+    uint32_t h[5];
+    sha1_init(h);
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
+    if constexpr (V == 0) {
+        for (uint32_t b = 0; b < nblk; ++b) {
+            uint32_t w[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) w[i] = bswap32(uint32_t(v) + i * 0x9E3779B9u + b);
+            sha1_compress(h, w);
+        }
+    } else if constexpr (V >= 1 && V <= 3) {
+        sha1_blocks_ring_vc<V + 1>(smem, p, nblk, h);
+    } else if constexpr (V == 4) {
+        sha1_blocks_ring_pipe<3>(smem, p, nblk, h);
+    }
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
+    uint32_t x = h[0] ^ h[1] ^ h[2] ^ h[3] ^ h[4];
+    if (lane == 0) {
+        unsigned hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        out[blockIdx.x * 4 + 0] = t1 - t0;
+        out[blockIdx.x * 4 + 1] = r1 - r0;
+        out[blockIdx.x * 4 + 2] = (uint64_t(xcc) << 32) | hw;
+    }
+    if (x == 0x12345678u) out[blockIdx.x * 4 + 3] = x;
+}
+
+template <int V>
+void run(const char* name, const uint8_t* d, uint64_t vstride, uint32_t nblk, int waves, int hbm) {
+    unsigned long long* out;
+    (void)hipMalloc(&out, size_t(waves) * 32);
+    hipLaunchKernelGGL(k_lone<V>, dim3(waves), dim3(64), 0, 0, d, vstride, nblk, hbm, out);
+    (void)hipDeviceSynchronize();
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    (void)hipEventRecord(e0);
+    hipLaunchKernelGGL(k_lone<V>, dim3(waves), dim3(64), 0, 0, d, vstride, nblk, hbm, out);
+    (void)hipEventRecord(e1);
+    (void)hipEventSynchronize(e1);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    std::vector<unsigned long long> o(size_t(waves) * 4);
+    (void)hipMemcpy(o.data(), out, o.size() * 8, hipMemcpyDeviceToHost);
+    double cyc = 0, cmax = 0, ghz = 0;
+    for (int w = 0; w < waves; ++w) {
+        cyc += double(o[4 * w]);
+        cmax = std::max(cmax, double(o[4 * w]));
+        ghz += double(o[4 * w]) / (double(o[4 * w + 1]) / 100e6) / 1e9;
+    }
+    printf("%-28s %s waves=%4d nblk=%5u  %.3f ms  clk %.2f GHz  %.0f cycles/block (max %.0f)  %.3f us/block\n", name,
+           hbm ? "HBM" : "L2 ", waves, nblk, ms, ghz / waves, cyc / waves / nblk, cmax / nblk,
+           ms * 1e3 / nblk);
+    (void)hipFree(out);
+}
+
+}  // namespace nkv
+
+int main() {
+    using namespace nkv;
+    const uint32_t nblk = 1024;
+    const uint64_t vstride = 64ull * nblk;
+    const uint64_t bytes = uint64_t(2048) * 64 * vstride;
+    uint8_t* d;
+    if (hipMalloc(&d, bytes + 4096) != hipSuccess) return 1;
+    (void)hipMemset(d, 0x5a, bytes + 4096);
+    for (int hbm = 0; hbm < 2; ++hbm)
+        for (int waves : {256, 512, 1024, 2048}) {
+            run<0>("regs only", d, vstride, nblk, waves, hbm);
+            run<2>("ring_vc<3>", d, vstride, nblk, waves, hbm);
+        }
+    (void)hipFree(d);
+    return 0;
+}

@@ -16,7 +16,7 @@
                  OP(%4) "\n\t" OP(%5) "\n\t" OP(%6) "\n\t" OP(%7) "\n\t"            \
                  ".endr"                                                          \
                  : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) \
-                 : "v"(x), "v"(y))
+                 : "v"(x), "v"(y) : "vcc", "v63")
 
 #define OP_ADD(r) "v_add_u32 " #r ", " #r ", %8"
 #define OP_XOR(r) "v_xor_b32 " #r ", " #r ", %8"
@@ -48,6 +48,15 @@
                  : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) \
                  : "v"(x), "v"(y))
 #define OP_MADU24(r) "v_mad_u32_u24 " #r ", " #r ", %8, %9"
+#define OP_ADDCO(r) "v_add_co_u32 " #r ", vcc, " #r ", %8"
+#define OP_ADDC(r) "v_addc_co_u32 " #r ", vcc, " #r ", %8, vcc"
+#define OP_MOV(r) "v_mov_b32 " #r ", %8"
+#define OP_BFI(r) "v_bfi_b32 " #r ", " #r ", %8, %9"
+#define OP_ALIGNBYTE(r) "v_alignbyte_b32 " #r ", " #r ", %8, 1"
+#define OP_ROT1C(r) "v_add_co_u32 v63, vcc, " #r ", " #r "\n\tv_addc_co_u32 " #r ", vcc, " #r ", " #r ", vcc"
+#define OP_SUB(r) "v_sub_u32 " #r ", " #r ", %8"
+#define OP_AND(r) "v_and_b32 " #r ", " #r ", %8"
+#define OP_CNDMASK(r) "v_cndmask_b32 " #r ", " #r ", %8, vcc"
 
 template <int K>
 __global__ __launch_bounds__(256) void k(uint32_t* out, unsigned long long* clk, uint32_t seed) {
@@ -77,6 +86,18 @@ __global__ __launch_bounds__(256) void k(uint32_t* out, unsigned long long* clk,
         if (K == 17) BODYCL(CL_ALIGN, CL_XOR);
         if (K == 18) BODYCL(CL_BITOP, CL_XOR);
         if (K == 19) BODYCL(CL_XOR, CL_XOR);
+        if (K == 20) { if (blockIdx.x & 1) BODY8(OP_ALIGNBIT); else BODY8(OP_XOR); }
+        if (K == 21) BODY8(OP_ADDCO);
+        if (K == 22) BODY8(OP_ADDC);
+        if (K == 23) BODY8(OP_MOV);
+        if (K == 24) BODY8(OP_BFI);
+        if (K == 25) BODY8(OP_ALIGNBYTE);
+        if (K == 26) BODY8(OP_SUB);
+        if (K == 27) BODY8(OP_AND);
+        if (K == 28) BODY8(OP_CNDMASK);
+        if (K == 29) { if (blockIdx.x & 1) BODY8(OP_MIX1); else BODY8(OP_XOR); }
+        if (K == 30) { if ((blockIdx.x & 3) == 0) BODY8(OP_ALIGNBIT); else BODY8(OP_XOR); }
+        if (K == 31) BODY8(OP_ROT1C);
     }
     unsigned long long t1 = __builtin_amdgcn_s_memtime();
     unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
@@ -139,6 +160,18 @@ int main() {
         run<17>("clustered 8 alignbit + 8 xor (per 2)", blocks);
         run<18>("clustered 8 bitop3 + 8 xor (per 2)", blocks);
         run<19>("16 xor (per 2)", blocks);
+        run<20>("split blocks: pure alignbit | pure xor", blocks);
+        run<21>("v_add_co_u32", blocks);
+        run<22>("v_addc_co_u32", blocks);
+        run<23>("v_mov_b32", blocks);
+        run<24>("v_bfi_b32", blocks);
+        run<25>("v_alignbyte", blocks);
+        run<26>("v_sub_u32", blocks);
+        run<27>("v_and_b32", blocks);
+        run<28>("v_cndmask", blocks);
+        run<29>("split blocks: mix1 (2 instr) | pure xor", blocks);
+        run<30>("split 1:3 alignbit | xor", blocks);
+        run<31>("rotl1 by add_co+addc (2 instr)", blocks);
     }
     return 0;
 }
