@@ -56,10 +56,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", choices=["sstable4k", "mixed", "records"], default="sstable4k",
+    ap.add_argument("--config", choices=["sstable4k", "mixed", "records", "records_verify"], default="sstable4k",
                     help="sstable4k = BASELINE configs[1] (the metric); mixed = configs[2]; records = the "
                          "compaction form: 1 Mi serialized 4 KiB records in a Data table, values located "
-                         "from the record headers and hashed in place")
+                         "from the record headers and hashed in place; records_verify = the same plus every "
+                         "record's Crc checked (nkv_tree_verify_records_dev)")
     ap.add_argument("--mixed-bytes", type=int, default=4 << 30, help="payload of the mixed config")
     ap.add_argument("--no-bucket", action="store_true", help="hash ragged values in input order (--bucket 0)")
     ap.add_argument("--bucket", type=int, default=-1, help="NKV_OPT_BUCKET override (0 input order, 1 sorted, 2 auto)")
@@ -151,7 +152,8 @@ def main():
         ctx.set_option(_lib.NKV_OPT_BUCKET, args.bucket)
     roots = torch.empty(world * 20, dtype=torch.uint8, device="cuda")
     mixed = args.config == "mixed"
-    records = args.config == "records"
+    records = args.config in ("records", "records_verify")
+    verify_crc = args.config == "records_verify"
     if records:
         import numpy as np
         n, rb = args.leaves, args.value_bytes
@@ -167,10 +169,20 @@ def main():
         d_err = torch.zeros(1, dtype=torch.int32, device="cuda")
         nbytes = n * vlen  # payload: the hashed Values
         nodes = torch.empty(L.nkv_total_nodes(n) * 20, dtype=torch.uint8, device="cuda")
+        if verify_crc:  # store each record's right checksum (computed on the device once)
+            d_crc = torch.empty(n, dtype=torch.int32, device="cuda")
+            d_stats = torch.zeros(3, dtype=torch.int64, device="cuda")
+            _lib.check(L.nkv_record_crc_dev(ctx.h, data.data_ptr(), stream_len, d_roff.data_ptr(), n,
+                                            d_crc.data_ptr(), d_stats.data_ptr()))
+            v[:, 0:4] = d_crc.view(torch.uint8).view(n, 4)
 
-        def tree():
-            _lib.check(L.nkv_tree_from_records_dev(ctx.h, data.data_ptr(), stream_len, d_roff.data_ptr(), n,
-                                                   nodes.data_ptr(), d_err.data_ptr()))
+            def tree():
+                _lib.check(L.nkv_tree_verify_records_dev(ctx.h, data.data_ptr(), stream_len, d_roff.data_ptr(), n,
+                                                         nodes.data_ptr(), None, d_stats.data_ptr()))
+        else:
+            def tree():
+                _lib.check(L.nkv_tree_from_records_dev(ctx.h, data.data_ptr(), stream_len, d_roff.data_ptr(), n,
+                                                       nodes.data_ptr(), d_err.data_ptr()))
     elif not mixed:
         n, vlen = args.leaves, args.value_bytes
         nbytes = n * vlen
@@ -254,6 +266,8 @@ def main():
             voff = np.arange(n, dtype=np.uint64) * rb + 30 + ks
             want = oc.tree_from_digests(oc.leaf_hashes(host, voff, np.full(n, vlen, np.uint64), threads=16))
             assert int(d_err.item()) == 0
+            if verify_crc:
+                assert d_stats.cpu().tolist() == [0, -1, 0], d_stats.cpu().tolist()
         else:
             host = oc.splitmix64_bytes(nbytes, SEED)
             want = oc.tree_from_digests(oc.leaf_hashes_strided(host, vlen, vlen, n, threads=16))
@@ -292,8 +306,9 @@ def main():
             "config": {
                 "workload": ("BASELINE configs[2]: mixed 64 B - 64 KiB log-uniform values packed back to back, "
                              + ("input order" if args.no_bucket else "length-bucketed")) if mixed else
-                            (f"compaction form: {n} serialized {rb}-B records (16-B key, {vlen}-B value) in a "
-                             "Data table in HBM; values located from the headers and hashed in place, full tree")
+                            (f"compaction form: {n} serialized {rb}-B records ({ks}-B key, {vlen}-B value) in a "
+                             "Data table in HBM; values located from the headers and hashed in place, full tree"
+                             + ("; every record's Crc (Key ++ Value) checked in the same pass" if verify_crc else ""))
                             if records else
                             "BASELINE configs[1]: single SSTable flush, 1 Mi x 4 KiB values, "
                             "leaf SHA-1 + full tree reduce (one table per GPU; roots all-gathered over RCCL when N>1)",
@@ -304,7 +319,10 @@ def main():
             "roofline": {
                 "bound": "hbm",
                 "kernel": ("leaf phase: length sort + ragged leaf SHA-1 (%s)" % LEAF_KERNEL.get(args.deep, "default"))
-                          if (mixed or records) else "k_leaf<strided,fused,aligned> (leaf SHA-1 + first 8 levels)",
+                          if mixed else
+                          ("leaf phase: k_leaf_verify (record CRC + leaf SHA-1, input order)" if verify_crc else
+                           "leaf phase: k_leaf<offsets, LDS-DMA> (input order)") if records else
+                          "k_leaf<strided, LDS-DMA> (leaf SHA-1, level 0)",
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

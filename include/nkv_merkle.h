@@ -256,6 +256,15 @@ int nkv_crc32_dev(nkv_ctx *ctx, const void *d_base, const uint64_t *d_off, const
  * (UINT64_MAX if none), [2] 1 if a header points outside the stream. */
 int nkv_record_crc_dev(nkv_ctx *ctx, const void *d_stream, uint64_t stream_len,
                        const uint64_t *d_rec_off, uint64_t n, uint32_t *d_crc, uint64_t *d_stats);
+/* Compaction read of a device-resident Data table in one call, asynchronous:
+ * the Merkle tree of the records' Values into d_nodes (as
+ * nkv_tree_from_records_dev) and record.Deserialize's checksum check
+ * (record.go:163-169) of every record, d_crc / d_stats as nkv_record_crc_dev
+ * (a header outside the stream sets d_stats[2]; that leaf hashes the empty
+ * value).  Records of similar sizes are read once for both (k_leaf_verify). */
+int nkv_tree_verify_records_dev(nkv_ctx *ctx, const void *d_stream, uint64_t stream_len,
+                                const uint64_t *d_rec_off, uint64_t n, void *d_nodes, uint32_t *d_crc,
+                                uint64_t *d_stats);
 /* Bloom filter bits on the device: d_bits holds ((m + 31) / 32) * 4 bytes
  * (Contents padded to whole 32-bit words, zero the padding); bits are OR-ed in,
  * so several calls build one filter. */

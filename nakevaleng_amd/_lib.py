@@ -83,6 +83,7 @@ SIGNATURES = {
     "nkv_tree_from_records_dev": (_int, [_vp, _vp, _u64, _vp, _u64, _vp, _vp]),
     "nkv_crc32_dev": (_int, [_vp, _vp, _vp, _vp, _u64, _vp]),
     "nkv_record_crc_dev": (_int, [_vp, _vp, _u64, _vp, _u64, _vp, _vp]),
+    "nkv_tree_verify_records_dev": (_int, [_vp, _vp, _u64, _vp, _u64, _vp, _vp, _vp]),
     "nkv_bloom_insert_dev": (_int, [_vp, _vp, _vp, _vp, _u64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                     _vp]),
     "nkv_bloom_insert_records_dev": (_int, [_vp, _vp, _u64, _vp, _u64, ctypes.c_uint32, ctypes.c_uint32,

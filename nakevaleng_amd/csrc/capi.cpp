@@ -291,9 +291,10 @@ int plan_of(nkv_ctx* c, const uint64_t* len, const uint64_t* host_len, uint64_t 
 }
 
 // Level 0 in the order plan_of chose.  Gated plans also launch the input-order
-// kernel (it runs when the range is narrow).
+// kernel (it runs when the range is narrow) unless the caller has its own
+// (narrow_kernel = false: k_leaf_verify).
 int leaf_level(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint64_t* len, uint64_t n,
-               bool aligned, uint8_t* nodes, int plan, Gate range) {
+               bool aligned, uint8_t* nodes, int plan, Gate range, bool narrow_kernel = true) {
     if (plan == kInputOrder)
         return st(launch_leaf_offsets(base, off, len, nullptr, n, aligned, c->leaf_load, nodes, c->stream,
                                       c->deep != 0));
@@ -316,7 +317,7 @@ int leaf_level(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint6
         HIPTRY(launch_leaf_offsets(base, off, len, perm, n, aligned, c->leaf_load, nodes, c->stream, c->deep != 0,
                                    wide));
     }
-    if (plan == kGated)
+    if (plan == kGated && narrow_kernel)
         HIPTRY(launch_leaf_offsets(base, off, len, nullptr, n, aligned, c->leaf_load, nodes, c->stream,
                                    c->deep != 0, Gate{range.range, 1}));
     return NKV_OK;
@@ -907,6 +908,55 @@ int nkv_tree_from_records_dev(nkv_ctx* c, const void* d_stream, uint64_t stream_
     HIPTRY(hipMemcpyAsync(&h, err, 4, hipMemcpyDeviceToHost, c->stream));
     HIPTRY(hipStreamSynchronize(c->stream));
     return h ? NKV_ERR_INVALID : NKV_OK;
+}
+
+// Compaction read in one pass: the Merkle tree of the records' Values and the
+// check of every record's Crc.  Batches of similar record sizes (the range rule
+// of plan_of) run k_leaf_verify, which reads each record once for both; ragged
+// batches run the checksum kernel and the length-sorted leaf kernel instead.
+int nkv_tree_verify_records_dev(nkv_ctx* c, const void* d_stream, uint64_t stream_len, const uint64_t* d_rec_off,
+                                uint64_t n, void* d_nodes, uint32_t* d_crc, uint64_t* d_stats) {
+    TRY(bind(c));
+    if (n == 0) return NKV_ERR_EMPTY;
+    if (!d_stream || !d_rec_off || !d_nodes) return NKV_ERR_INVALID;
+    const uint8_t* stream = static_cast<const uint8_t*>(d_stream);
+    uint8_t* nodes = static_cast<uint8_t*>(d_nodes);
+    unsigned long long* stats = reinterpret_cast<unsigned long long*>(d_stats);
+    if (!stats) {
+        TRY(grow(c->d_stats, 24));
+        stats = static_cast<unsigned long long*>(c->d_stats.p);
+    }
+    HIPTRY(hipMemsetAsync(stats, 0, 24, c->stream));
+    HIPTRY(hipMemsetAsync(stats + 1, 0xFF, 8, c->stream));
+    TRY(mark(c, 0));
+    int plan = kInputOrder;
+    Gate g;
+    uint64_t* voff = nullptr;
+    uint64_t* vlen = nullptr;
+    if (c->bucket != 0 && n > 64) {
+        // the lengths decide the order (and feed the sorted branch)
+        TRY(grow(c->d_off, 8 * n));
+        TRY(grow(c->d_len, 8 * n));
+        TRY(grow(c->d_err, 4));
+        voff = static_cast<uint64_t*>(c->d_off.p);
+        vlen = static_cast<uint64_t*>(c->d_len.p);
+        unsigned int* err = static_cast<unsigned int*>(c->d_err.p);
+        HIPTRY(hipMemsetAsync(err, 0, 4, c->stream));
+        HIPTRY(launch_locate(stream, stream_len, d_rec_off, n, voff, vlen, err, c->stream));
+        TRY(plan_of(c, vlen, nullptr, n, &plan, &g));
+    }
+    if (plan != kSorted)
+        HIPTRY(launch_leaf_verify(stream, stream_len, d_rec_off, n, nodes, d_crc, stats, c->stream,
+                                  plan == kGated ? Gate{g.range, 1} : Gate{}));
+    if (plan != kInputOrder) {
+        const Gate wide = plan == kGated ? Gate{g.range, 2} : Gate{};
+        HIPTRY(launch_record_crc(stream, stream_len, d_rec_off, n, d_crc, stats, c->crc_load, c->stream, wide,
+                                 false));
+        TRY(leaf_level(c, stream, voff, vlen, n, false, nodes, plan, g, false));
+    }
+    TRY(mark(c, 1));
+    HIPTRY(launch_reduce(nodes, n, 0, levels_of(n) - 1, c->stream));
+    return mark(c, 2);
 }
 
 int nkv_crc32_dev(nkv_ctx* c, const void* d_base, const uint64_t* d_off, const uint64_t* d_len, uint64_t n,

@@ -25,45 +25,12 @@
 
 #include <algorithm>
 
+#include "crc_dev.hpp"
 #include "internal.hpp"
 
 namespace nkv {
 
-struct CrcTables {
-    uint32_t t[4][256];
-};
-
-constexpr CrcTables make_crc_tables() {
-    CrcTables r{};
-    for (uint32_t i = 0; i < 256; ++i) {
-        uint32_t c = i;
-        for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (0xEDB88320u & (0u - (c & 1u)));
-        r.t[0][i] = c;
-    }
-    for (int k = 1; k < 4; ++k)
-        for (uint32_t i = 0; i < 256; ++i) r.t[k][i] = (r.t[k - 1][i] >> 8) ^ r.t[0][r.t[k - 1][i] & 0xFFu];
-    return r;
-}
-
 __constant__ CrcTables c_crc = make_crc_tables();
-
-// tab: this lane's copy (LDS base + lane % C), C copies interleaved
-template <int C>
-__device__ __forceinline__ uint32_t crc_lut(const uint32_t* tab, int k, uint32_t e) {
-    return tab[(uint32_t(k) * 256u + e) * C];
-}
-
-template <int C>
-__device__ __forceinline__ uint32_t crc_word(uint32_t crc, uint32_t w, const uint32_t* tab) {
-    const uint32_t x = crc ^ w;
-    return crc_lut<C>(tab, 3, x & 0xFFu) ^ crc_lut<C>(tab, 2, (x >> 8) & 0xFFu) ^
-           crc_lut<C>(tab, 1, (x >> 16) & 0xFFu) ^ crc_lut<C>(tab, 0, x >> 24);
-}
-
-template <int C>
-__device__ __forceinline__ uint32_t crc_byte(uint32_t crc, uint32_t b, const uint32_t* tab) {
-    return crc_lut<C>(tab, 0, (crc ^ b) & 0xFFu) ^ (crc >> 8);
-}
 
 __device__ __forceinline__ uint64_t crc_ld_le64(const uint8_t* p) {
     uint64_t v = 0;
@@ -198,8 +165,10 @@ __device__ __forceinline__ uint32_t crc_span_ring(const uint8_t* s, uint64_t len
 template <bool RECORDS, bool RING, int C, int B>
 __global__ __launch_bounds__(B) void k_crc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
                                            const uint64_t* __restrict__ len, uint64_t stream_len, uint64_t n,
-                                           uint32_t* __restrict__ out, unsigned long long* __restrict__ stats) {
+                                           uint32_t* __restrict__ out, unsigned long long* __restrict__ stats,
+                                           Gate gate) {
     __shared__ uint32_t tab[4 * 256 * C];
+    if (!gate.open()) return;
     __shared__ __attribute__((aligned(16))) uint8_t ring[RING ? B / 64 : 1][RING ? 8192 : 16];
     for (int i = threadIdx.x; i < 4 * 256 * C; i += B) tab[i] = (&c_crc.t[0][0])[i / C];
     __syncthreads();
@@ -369,9 +338,10 @@ __global__ __launch_bounds__(WG) void k_crc_group(const uint8_t* __restrict__ ba
                                                       const uint64_t* __restrict__ off,
                                                       const uint64_t* __restrict__ len, uint64_t stream_len,
                                                       uint64_t n, uint32_t* __restrict__ out,
-                                                      unsigned long long* __restrict__ stats) {
+                                                      unsigned long long* __restrict__ stats, Gate gate) {
     __shared__ uint32_t tab[4 * 256 * C];
     __shared__ uint32_t sh[6 * 4 * 256];
+    if (!gate.open()) return;
     for (int i = threadIdx.x; i < 4 * 256 * C; i += WG) tab[i] = (&c_crc.t[0][0])[i / C];
     for (int i = threadIdx.x; i < 6 * 4 * 256; i += WG) sh[i] = (&c_crc_shift.t[0][0][0])[i];
     __syncthreads();
@@ -427,14 +397,14 @@ __global__ __launch_bounds__(WG) void k_crc_group(const uint8_t* __restrict__ ba
 template <bool RECORDS, int C, int WG>
 static void launch_crc_group(int per_cu, const uint8_t* base, const uint64_t* off, const uint64_t* len,
                              uint64_t stream_len, uint64_t n, uint32_t* out, unsigned long long* stats,
-                             hipStream_t s) {
+                             hipStream_t s, Gate gate) {
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const uint64_t groups_per_wg = WG / kCrcGroup;
     const uint64_t want = (n + groups_per_wg - 1) / groups_per_wg;
     const uint32_t grid = uint32_t(std::min<uint64_t>(want, uint64_t(cus) * per_cu));
     hipLaunchKernelGGL((k_crc_group<RECORDS, C, WG>), dim3(grid), dim3(WG), 0, s, base, off, len, stream_len, n,
-                       out, stats);
+                       out, stats, gate);
 }
 
 // variant 8 / 9: span-group kernel with 8 x 512 / 32 x 1024 table copies x
@@ -442,16 +412,17 @@ static void launch_crc_group(int per_cu, const uint8_t* base, const uint64_t* of
 // size: 0 = 8 x 256, 1 = 16 x 512, 2 = 32 x 1024.
 template <bool RECORDS>
 static void launch_crc(int variant, const uint8_t* base, const uint64_t* off, const uint64_t* len,
-                       uint64_t stream_len, uint64_t n, uint32_t* out, unsigned long long* stats, hipStream_t s) {
-    if (variant == 8) return launch_crc_group<RECORDS, 8, 512>(2, base, off, len, stream_len, n, out, stats, s);
-    if (variant == 9) return launch_crc_group<RECORDS, 32, 1024>(1, base, off, len, stream_len, n, out, stats, s);
-    if (variant == 10) return launch_crc_group<RECORDS, 4, 512>(4, base, off, len, stream_len, n, out, stats, s);
+                       uint64_t stream_len, uint64_t n, uint32_t* out, unsigned long long* stats, hipStream_t s,
+                       Gate gate) {
+    if (variant == 8) return launch_crc_group<RECORDS, 8, 512>(2, base, off, len, stream_len, n, out, stats, s, gate);
+    if (variant == 9) return launch_crc_group<RECORDS, 32, 1024>(1, base, off, len, stream_len, n, out, stats, s, gate);
+    if (variant == 10) return launch_crc_group<RECORDS, 4, 512>(4, base, off, len, stream_len, n, out, stats, s, gate);
     const bool ring = variant & 1;
     const int cfg = (variant >> 1) & 3;
     const int B = cfg == 0 ? 256 : (cfg == 1 ? 512 : 1024);
     const dim3 grid(uint32_t((n + B - 1) / B)), block(B);
 #define NKV_CRC_LAUNCH(R, C, BB) \
-    hipLaunchKernelGGL((k_crc<RECORDS, R, C, BB>), grid, block, 0, s, base, off, len, stream_len, n, out, stats)
+    hipLaunchKernelGGL((k_crc<RECORDS, R, C, BB>), grid, block, 0, s, base, off, len, stream_len, n, out, stats, gate)
     if (cfg == 0) {
         if (ring) NKV_CRC_LAUNCH(true, 8, 256);
         else NKV_CRC_LAUNCH(false, 8, 256);
@@ -466,16 +437,19 @@ static void launch_crc(int variant, const uint8_t* base, const uint64_t* off, co
 
 hipError_t launch_crc_spans(const uint8_t* base, const uint64_t* off, const uint64_t* len, uint64_t n,
                             uint32_t* out, int variant, hipStream_t s) {
-    launch_crc<false>(variant, base, off, len, 0, n, out, nullptr, s);
+    launch_crc<false>(variant, base, off, len, 0, n, out, nullptr, s, Gate{});
     return hipGetLastError();
 }
 
 hipError_t launch_record_crc(const uint8_t* stream, uint64_t stream_len, const uint64_t* rec_off, uint64_t n,
-                             uint32_t* out, unsigned long long* stats, int variant, hipStream_t s) {
-    hipError_t e = hipMemsetAsync(stats, 0, 3 * sizeof(unsigned long long), s);
-    if (e == hipSuccess) e = hipMemsetAsync(stats + 1, 0xFF, sizeof(unsigned long long), s);
-    if (e != hipSuccess) return e;
-    launch_crc<true>(variant, stream, rec_off, nullptr, stream_len, n, out, stats, s);
+                             uint32_t* out, unsigned long long* stats, int variant, hipStream_t s, Gate gate,
+                             bool init_stats) {
+    if (init_stats) {
+        hipError_t e = hipMemsetAsync(stats, 0, 3 * sizeof(unsigned long long), s);
+        if (e == hipSuccess) e = hipMemsetAsync(stats + 1, 0xFF, sizeof(unsigned long long), s);
+        if (e != hipSuccess) return e;
+    }
+    launch_crc<true>(variant, stream, rec_off, nullptr, stream_len, n, out, stats, s, gate);
     return hipGetLastError();
 }
 

@@ -86,8 +86,17 @@ hipError_t sort_by_length_desc(const uint64_t* len, uint64_t n, uint32_t* perm, 
 // workgroup size).
 hipError_t launch_crc_spans(const uint8_t* base, const uint64_t* off, const uint64_t* len, uint64_t n,
                             uint32_t* out, int variant, hipStream_t s);
+// init_stats: reset stats to {0, UINT64_MAX, 0} first (false: the caller did)
 hipError_t launch_record_crc(const uint8_t* stream, uint64_t stream_len, const uint64_t* rec_off, uint64_t n,
-                             uint32_t* out, unsigned long long* stats, int variant, hipStream_t s);
+                             uint32_t* out, unsigned long long* stats, int variant, hipStream_t s,
+                             Gate gate = Gate{}, bool init_stats = true);
+// The compaction read in one pass (kernels.hip k_leaf_verify): for the record at
+// stream + rec_off[i], the leaf digest of its Value into nodes (level 0), its
+// CRC of Key ++ Value into crc_out[i] (nullable), checked against the stored
+// Crc into stats as launch_record_crc does (stats initialised by the caller).
+hipError_t launch_leaf_verify(const uint8_t* stream, uint64_t stream_len, const uint64_t* rec_off, uint64_t n,
+                              uint8_t* nodes, uint32_t* crc_out, unsigned long long* stats, hipStream_t s,
+                              Gate gate = Gate{});
 // bloom.hip: mode 0 = keys at base + off[i], len[i]; 1 = keys of the records at
 // base + off[i].  query: out[i] = all k bits set; else OR the bits in.
 hipError_t launch_bloom(int mode, bool query, const uint8_t* base, const uint64_t* off, const uint64_t* len,

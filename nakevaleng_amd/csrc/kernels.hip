@@ -18,6 +18,7 @@
 #include <hipcub/hipcub.hpp>
 #include <stdint.h>
 
+#include "crc_dev.hpp"
 #include "internal.hpp"
 #include "sha1_dev.hpp"
 
@@ -41,8 +42,20 @@ __device__ unsigned long long* g_diag = nullptr;
     } while (0)
 #endif
 
+// little-endian u64 at any alignment (record header fields)
+__device__ __forceinline__ uint64_t ld_le64(const uint8_t* p) {
+    uint64_t v = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v |= uint64_t(p[i]) << (8 * i);
+    return v;
+}
+
 // SHA-1 compressions of a len-byte message (FIPS 180-4 padding: + 0x80 + 8 B)
 __device__ __forceinline__ uint64_t compressions(uint64_t len) { return (len + 8) / 64 + 1; }
+
+// CRC tables for k_leaf_verify (crc.hip keeps its own copy: no relocatable
+// device code, so each translation unit defines its constants)
+__constant__ CrcTables c_crc_leaf = make_crc_tables();
 
 constexpr uint32_t kLenBuckets = 640;  // counting-sort buckets (len_bucket_desc)
 constexpr int kSortItems = 16;         // values per thread of a sort tile
@@ -279,10 +292,16 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 }
 
 // issue(b) starts the four DMA instructions of block b (each lane for its DMA
-// role); nmax = the wave's largest full-block count (wave-uniform).
-template <class Issue>
+// role); nmax = the wave's largest full-block count (wave-uniform).  raw(c)
+// sees each of this lane's blocks as loaded (four little-endian quads) before
+// the byte swap (k_leaf_verify checksums them there).
+struct NoRaw {
+    __device__ __forceinline__ void operator()(const uint4*) const {}
+};
+
+template <class Issue, class Raw = NoRaw>
 __device__ __forceinline__ void sha1_blocks_lds(const uint8_t* wbuf, uint32_t nmax, uint32_t my_nfull,
-                                                Issue issue, uint32_t h[5]) {
+                                                Issue issue, uint32_t h[5], Raw raw = Raw{}) {
     const int lane = threadIdx.x & 63;
     const uint4* rd = reinterpret_cast<const uint4*>(wbuf + 64 * lane);
     const uint32_t swz = (uint32_t(lane) >> 2) & 3u;
@@ -302,7 +321,10 @@ __device__ __forceinline__ void sha1_blocks_lds(const uint8_t* wbuf, uint32_t nm
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // stage reads done before refill
             issue(b + 1);
         }
-        if (b < my_nfull) sha1_compress(h, w);
+        if (b < my_nfull) {
+            raw(c);
+            sha1_compress(h, w);
+        }
     }
 }
 
@@ -775,6 +797,100 @@ __global__ __launch_bounds__(kBlock, (LOAD == 6 || LOAD == 7) ? 2 : ((LOAD == 4 
 #endif
 }
 
+// K1v: the compaction read of a Data table in one pass.  For every record it
+// checks record.Deserialize's checksum (record.go:163-169: crc32.ChecksumIEEE
+// of Key ++ Value against the stored Crc) and computes NewLeaf(Value)
+// (merklenode.go:27-34), reading each byte once.  The value-relative LDS-DMA
+// stream of k_leaf (LOAD 8) feeds both: each 64-byte block's 16 little-endian
+// words step the CRC (slicing-by-4 from one LDS table copy) before the byte
+// swap feeds SHA-1.  The key, which precedes the value, and the value's tail
+// are checksummed bytewise from global memory.  SHA-1 is VALU-bound and leaves
+// the LDS nearly idle, so the lookups ride along.  A record whose header points
+// outside the stream sets stats[2] and gets the digest of an empty value, as
+// in nkv_tree_from_records_dev.
+__global__ __launch_bounds__(kBlock, kLeafWavesPerSimd) void k_leaf_verify(
+    const uint8_t* __restrict__ stream, uint64_t stream_len, const uint64_t* __restrict__ rec_off, uint64_t n,
+    uint8_t* __restrict__ nodes, uint32_t* __restrict__ crc_out, unsigned long long* __restrict__ stats,
+    Gate gate) {
+    // ONE LDS object (a second one can cost the DMA loop its waits): four
+    // 4 KiB wave stages, then the 4 KiB of CRC tables
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kBlock * 64 + 4096];
+    if (!gate.open()) return;
+    uint32_t* tab = reinterpret_cast<uint32_t*>(smem + kBlock * 64);
+    for (int i = threadIdx.x; i < 4 * 256; i += kBlock) tab[i] = (&c_crc_leaf.t[0][0])[i];
+    __syncthreads();
+    const uint64_t t = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const bool live = t < n;
+    const uint8_t* key = stream;
+    const uint8_t* p = stream;
+    uint64_t ks = 0, ln = 0;
+    uint32_t stored = 0;
+    bool hdr_bad = false;
+    if (live) {
+        const uint64_t r = rec_off[t];
+        if (r + 30 <= stream_len) {
+            const uint64_t k = ld_le64(stream + r + 14), v = ld_le64(stream + r + 22);
+            if (k <= stream_len && v <= stream_len && r + 30 + k + v <= stream_len) {
+                key = stream + r + 30;
+                ks = k;
+                p = key + k;
+                ln = v;
+                stored = uint32_t(stream[r]) | uint32_t(stream[r + 1]) << 8 | uint32_t(stream[r + 2]) << 16 |
+                         uint32_t(stream[r + 3]) << 24;
+            } else {
+                hdr_bad = true;
+            }
+        } else {
+            hdr_bad = true;
+        }
+    }
+    uint32_t crc = 0xFFFFFFFFu;
+    for (uint64_t j = 0; j < ks; ++j) crc = crc_byte<1>(crc, key[j], tab);
+    uint8_t* wbuf = smem + 4096 * wave;
+    const uint32_t q = (uint32_t(lane) & 3u) ^ ((uint32_t(lane) >> 4) & 3u);
+    const uint32_t my_nfull = uint32_t(ln >> 6);
+    uint32_t h[5];
+    sha1_init(h);
+    const uint8_t* src[4];
+    uint32_t nf[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int j = 16 * k + (lane >> 2);
+        const uint64_t pj = uint64_t(__shfl(int64_t(reinterpret_cast<uintptr_t>(p)), j));
+        src[k] = reinterpret_cast<const uint8_t*>(pj) + 16 * q;
+        nf[k] = uint32_t(__shfl(int(my_nfull), j));
+    }
+    auto issue = [&](uint32_t b) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (b < nf[k]) __builtin_amdgcn_global_load_lds(src[k] + 64ull * b, wbuf + 1024 * k, 16, 0, 0);
+    };
+    auto raw = [&](const uint4* c) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            crc = crc_word<1>(crc, c[i].x, tab);
+            crc = crc_word<1>(crc, c[i].y, tab);
+            crc = crc_word<1>(crc, c[i].z, tab);
+            crc = crc_word<1>(crc, c[i].w, tab);
+        }
+    };
+    sha1_blocks_lds(wbuf, wave_max_u32(my_nfull), my_nfull, issue, h, raw);
+    for (uint64_t j = uint64_t(my_nfull) * 64; j < ln; ++j) crc = crc_byte<1>(crc, p[j], tab);
+    if (!live) return;
+    sha1_tail<false>(p, ln, h);
+    store_digest(nodes, t, h);
+    crc = ~crc;
+    if (crc_out) crc_out[t] = crc;
+    if (hdr_bad) {
+        atomicOr(stats + 2, 1ull);
+    } else if (crc != stored) {
+        atomicAdd(stats, 1ull);
+        atomicMin(stats + 1, (unsigned long long)t);
+    }
+}
+
 // K1q: ragged batches, work-queue form.  Values are length-sorted, longest
 // first, and cut into 64-value groups.  A group is one wavefront's work, and a
 // group's 64 chains run as long as its longest value, so the batch can finish
@@ -1048,12 +1164,6 @@ __global__ __launch_bounds__(kBlock) void k_bfs_image(const uint8_t* __restrict_
 // Record layout (record.go:191-199, little endian): Crc u32 @0, Timestamp i64
 // @4, Status u8 @12, TypeInfo u8 @13, KeySize u64 @14, ValueSize u64 @22,
 // Key @30, Value @30+KeySize.  rec_off[i] = start of record i.
-__device__ __forceinline__ uint64_t ld_le64(const uint8_t* p) {
-    uint64_t v = 0;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) v |= uint64_t(p[i]) << (8 * i);
-    return v;
-}
 
 __global__ __launch_bounds__(kBlock) void k_locate(const uint8_t* __restrict__ stream,
                                                     uint64_t stream_len,
@@ -1193,6 +1303,13 @@ hipError_t launch_leaf_offsets(const uint8_t* base, const uint64_t* off, const u
     if (perm && deep) load = aligned ? 6 : 7;  // ragged, length-sorted: deep prefetch
     else if (!aligned) load = load == 1 ? 8 : 0;  // LDS-DMA serves any alignment
     leaf_dispatch<1>(load, base, off, len, 0, 0, perm, n, nodes, s, gate);
+    return hipGetLastError();
+}
+
+hipError_t launch_leaf_verify(const uint8_t* stream, uint64_t stream_len, const uint64_t* rec_off, uint64_t n,
+                              uint8_t* nodes, uint32_t* crc_out, unsigned long long* stats, hipStream_t s, Gate gate) {
+    hipLaunchKernelGGL(k_leaf_verify, dim3(grid_for(n)), dim3(kBlock), 0, s, stream, stream_len, rec_off, n, nodes,
+                       crc_out, stats, gate);
     return hipGetLastError();
 }
 
