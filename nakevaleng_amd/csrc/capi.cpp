@@ -113,7 +113,7 @@ struct nkv_ctx {
     std::vector<hipEvent_t> ring;
     size_t ring_used = 0;
     DevBuf d_data, d_off, d_len, d_nodes, d_img, d_tmp, d_err, d_aux, d_keys, d_perm, d_stmp, d_queue, d_stats,
-        d_range;
+        d_range, d_sync;
     void* h_stage = nullptr;  // small pinned staging (offsets, lengths, stats)
     unsigned int* h_small = nullptr;  // 64 pinned bytes for device-to-host decisions
     size_t h_cap = 0;
@@ -160,6 +160,8 @@ int grow(DevBuf& b, size_t bytes) {
     b.cap = want;
     return NKV_OK;
 }
+
+SyncSlot* sync_slot(nkv_ctx* c, SyncUse u) { return static_cast<SyncSlot*>(c->d_sync.p) + u; }
 
 int grow_host(nkv_ctx* c, size_t bytes) {
     if (bytes == 0) bytes = 16;
@@ -268,7 +270,9 @@ int mark(nkv_ctx* c, int which) {
 // asynchronous; the sort then runs either way).
 enum Plan { kInputOrder = 0, kSorted = 1, kGated = 2 };
 
-int plan_of(nkv_ctx* c, const uint64_t* len, const uint64_t* host_len, uint64_t n, int* plan, Gate* gate) {
+// dev_range (nullable): the batch's range already on the device (k_locate wrote it)
+int plan_of(nkv_ctx* c, const uint64_t* len, const uint64_t* host_len, uint64_t n, int* plan, Gate* gate,
+            const unsigned int* dev_range = nullptr) {
     *plan = (c->bucket != 0 && n > 64) ? kSorted : kInputOrder;
     *gate = Gate{};
     if (c->bucket != 2 || n < 4096) return NKV_OK;
@@ -282,9 +286,14 @@ int plan_of(nkv_ctx* c, const uint64_t* len, const uint64_t* host_len, uint64_t 
         *plan = hi <= lo + std::max<uint64_t>(1, lo / 16) ? kInputOrder : kSorted;
         return NKV_OK;
     }
+    if (dev_range) {
+        gate->range = dev_range;
+        *plan = kGated;
+        return NKV_OK;
+    }
     TRY(grow(c->d_range, 8));
     unsigned int* d = static_cast<unsigned int*>(c->d_range.p);
-    HIPTRY(launch_len_range(len, n, d, c->stream));
+    HIPTRY(launch_len_range(len, n, d, sync_slot(c, kSyncRange), c->stream));
     gate->range = d;
     *plan = kGated;
     return NKV_OK;
@@ -312,7 +321,8 @@ int leaf_level(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint6
         const int max_waves = slots == 4 ? 2 : (slots == 3 ? 3 : 5);
         const int waves = ring ? std::min(c->queue_waves, max_waves) : 2;
         HIPTRY(launch_leaf_queue(base, off, len, perm, n, aligned, ring, static_cast<uint32_t*>(c->d_queue.p),
-                                 c->simds, uint32_t(waves), uint32_t(c->queue_split), nodes, c->stream, wide));
+                                 c->simds, uint32_t(waves), uint32_t(c->queue_split), nodes,
+                                 sync_slot(c, kSyncSplit), c->stream, wide));
     } else {
         HIPTRY(launch_leaf_offsets(base, off, len, perm, n, aligned, c->leaf_load, nodes, c->stream, c->deep != 0,
                                    wide));
@@ -334,10 +344,11 @@ int leaf_level(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint6
 // host_len (nullable): the value lengths on the host, when the caller has them.
 // Every order leaves level 0 complete, so one reduce sequence follows.
 int tree_from_device_values(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint64_t* len,
-                            uint64_t n, bool aligned, uint8_t* nodes, const uint64_t* host_len = nullptr) {
+                            uint64_t n, bool aligned, uint8_t* nodes, const uint64_t* host_len = nullptr,
+                            const unsigned int* dev_range = nullptr) {
     int plan = kInputOrder;
     Gate g;
-    TRY(plan_of(c, len, host_len, n, &plan, &g));
+    TRY(plan_of(c, len, host_len, n, &plan, &g, dev_range));
     TRY(mark(c, 0));
     TRY(leaf_level(c, base, off, len, n, aligned, nodes, plan, g));
     TRY(mark(c, 1));
@@ -385,6 +396,12 @@ int nkv_ctx_create(int device, nkv_ctx** out) {
     if (rc == NKV_OK) rc = st(hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking));
     if (rc == NKV_OK) rc = st(hipHostMalloc(reinterpret_cast<void**>(&c->h_small), 64, hipHostMallocDefault));
     for (int i = 0; i < 3 && rc == NKV_OK; ++i) rc = st(hipEventCreate(&c->ev[i]));
+    if (rc == NKV_OK) rc = grow(c->d_sync, sizeof(SyncSlot) * kSyncSlots);
+    if (rc == NKV_OK) {  // the grid-fold accumulators start (and every launch leaves them) at kSyncInit
+        SyncSlot init[kSyncSlots];
+        for (SyncSlot& x : init) x = kSyncInit;
+        rc = st(hipMemcpy(c->d_sync.p, init, sizeof(init), hipMemcpyHostToDevice));
+    }
     if (rc != NKV_OK) {
         nkv_ctx_destroy(c);
         return rc;
@@ -403,7 +420,7 @@ void nkv_ctx_destroy(nkv_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (DevBuf* b : {&c->d_data, &c->d_off, &c->d_len, &c->d_nodes, &c->d_img, &c->d_tmp,
                       &c->d_err, &c->d_aux, &c->d_keys, &c->d_perm, &c->d_stmp, &c->d_queue, &c->d_stats,
-                      &c->d_range})
+                      &c->d_range, &c->d_sync})
         if (b->p) (void)hipFree(b->p);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
     if (c->h_small) (void)hipHostFree(c->h_small);
@@ -875,9 +892,8 @@ int nkv_locate_values_dev(nkv_ctx* c, const void* d_stream, uint64_t stream_len,
     if (!d_stream || !d_rec_off || !d_voff || !d_vlen) return NKV_ERR_INVALID;
     TRY(grow(c->d_err, 4));
     unsigned int* err = static_cast<unsigned int*>(c->d_err.p);
-    HIPTRY(hipMemsetAsync(err, 0, 4, c->stream));
     HIPTRY(launch_locate(static_cast<const uint8_t*>(d_stream), stream_len, d_rec_off, n, d_voff,
-                         d_vlen, err, c->stream));
+                         d_vlen, err, nullptr, sync_slot(c, kSyncLocate), c->stream));
     unsigned int h = 0;
     HIPTRY(hipMemcpyAsync(&h, err, 4, hipMemcpyDeviceToHost, c->stream));
     HIPTRY(hipStreamSynchronize(c->stream));
@@ -898,11 +914,14 @@ int nkv_tree_from_records_dev(nkv_ctx* c, const void* d_stream, uint64_t stream_
     }
     uint64_t* voff = static_cast<uint64_t*>(c->d_off.p);
     uint64_t* vlen = static_cast<uint64_t*>(c->d_len.p);
-    HIPTRY(hipMemsetAsync(err, 0, 4, c->stream));
-    HIPTRY(launch_locate(static_cast<const uint8_t*>(d_stream), stream_len, d_rec_off, n, voff, vlen, err,
-                         c->stream));
+    // the locate pass also measures the range the order choice needs
+    const bool gated = c->bucket == 2 && n >= 4096;
+    if (gated) TRY(grow(c->d_range, 8));
+    unsigned int* range = gated ? static_cast<unsigned int*>(c->d_range.p) : nullptr;
+    HIPTRY(launch_locate(static_cast<const uint8_t*>(d_stream), stream_len, d_rec_off, n, voff, vlen, err, range,
+                         sync_slot(c, kSyncLocate), c->stream));
     TRY(tree_from_device_values(c, static_cast<const uint8_t*>(d_stream), voff, vlen, n, false,
-                                static_cast<uint8_t*>(d_nodes)));
+                                static_cast<uint8_t*>(d_nodes), nullptr, range));
     if (d_err) return NKV_OK;
     unsigned int h = 0;
     HIPTRY(hipMemcpyAsync(&h, err, 4, hipMemcpyDeviceToHost, c->stream));
@@ -941,9 +960,12 @@ int nkv_tree_verify_records_dev(nkv_ctx* c, const void* d_stream, uint64_t strea
         voff = static_cast<uint64_t*>(c->d_off.p);
         vlen = static_cast<uint64_t*>(c->d_len.p);
         unsigned int* err = static_cast<unsigned int*>(c->d_err.p);
-        HIPTRY(hipMemsetAsync(err, 0, 4, c->stream));
-        HIPTRY(launch_locate(stream, stream_len, d_rec_off, n, voff, vlen, err, c->stream));
-        TRY(plan_of(c, vlen, nullptr, n, &plan, &g));
+        const bool gated = c->bucket == 2 && n >= 4096;
+        if (gated) TRY(grow(c->d_range, 8));
+        unsigned int* range = gated ? static_cast<unsigned int*>(c->d_range.p) : nullptr;
+        HIPTRY(launch_locate(stream, stream_len, d_rec_off, n, voff, vlen, err, range, sync_slot(c, kSyncLocate),
+                             c->stream));
+        TRY(plan_of(c, vlen, nullptr, n, &plan, &g, range));
     }
     if (plan != kSorted)
         HIPTRY(launch_leaf_verify(stream, stream_len, d_rec_off, n, nodes, d_crc, stats, c->stream,

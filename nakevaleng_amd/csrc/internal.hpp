@@ -34,6 +34,22 @@ struct Gate {
     }
 };
 
+// Grid-wide results without fill launches (kernels.hip grid_fold): each block
+// folds its partial into these accumulators with device-scope atomics, then
+// draws a ticket that wraps to 0; the block drawing the last one takes the
+// totals with atomicExch, which restores every word.  nkv_ctx_create writes
+// kSyncInit once; every launch leaves a slot as it found it.
+struct SyncSlot {
+    unsigned int ticket;     // 0
+    unsigned int lo;         // running min, identity 0xFFFFFFFF
+    unsigned int hi;         // running max, identity 0
+    unsigned int flag;       // running or, identity 0
+    unsigned long long sum;  // running sum, identity 0
+    unsigned long long pad;
+};
+constexpr SyncSlot kSyncInit{0u, 0xFFFFFFFFu, 0u, 0u, 0ull, 0ull};
+enum SyncUse { kSyncRange = 0, kSyncLocate = 1, kSyncSplit = 2, kSyncSlots = 4 };
+
 // BFS image layout in image order (index 0 = top level).
 struct BfsLayout {
     int nlev;
@@ -63,13 +79,16 @@ uint64_t queue_words(uint64_t n);
 hipError_t launch_leaf_queue(const uint8_t* base, const uint64_t* off, const uint64_t* len,
                              const uint32_t* perm, uint64_t n, bool aligned, int ring, uint32_t* q,
                              uint32_t simds, uint32_t waves_per_simd, uint32_t split, uint8_t* nodes,
-                             hipStream_t s, Gate gate = Gate{});
+                             SyncSlot* sync, hipStream_t s, Gate gate = Gate{});
 hipError_t launch_reduce(uint8_t* nodes, uint64_t n, int from_level, int top, hipStream_t s, Gate gate = Gate{});
 hipError_t launch_bfs_image(const uint8_t* nodes, const BfsLayout& lay, uint8_t* img,
                             hipStream_t s);
+// err (u32): 1 if any header points outside the stream, else 0; range
+// (nullable, 2 u32): min / max full-block count of the values, as
+// launch_len_range writes it.  Neither needs initialising.
 hipError_t launch_locate(const uint8_t* stream, uint64_t stream_len, const uint64_t* rec_off,
-                         uint64_t n, uint64_t* voff, uint64_t* vlen, unsigned int* err,
-                         hipStream_t s);
+                         uint64_t n, uint64_t* voff, uint64_t* vlen, unsigned int* err, unsigned int* range,
+                         SyncSlot* sync, hipStream_t s);
 hipError_t scan_exclusive_u64(const uint64_t* in, uint64_t* out, uint64_t n, void* tmp,
                               size_t* tmp_bytes, hipStream_t s);
 // In-place exclusive scan of n u32 (gated); sums: scan_sums_words(n) u32.
@@ -110,6 +129,6 @@ hipError_t launch_bloom_ranges(int mode, const uint8_t* base, const uint64_t* of
                                uint32_t* bits, unsigned int* err, uint32_t* scratch, hipStream_t s);
 hipError_t launch_fill(uint8_t* buf, uint64_t nbytes, uint64_t seed, hipStream_t s);
 // out[0] / out[1] = min / max of len[i] / 64 over the batch (2 u32 on the device)
-hipError_t launch_len_range(const uint64_t* len, uint64_t n, unsigned int* out, hipStream_t s);
+hipError_t launch_len_range(const uint64_t* len, uint64_t n, unsigned int* out, SyncSlot* sync, hipStream_t s);
 
 }  // namespace nkv

@@ -50,6 +50,66 @@ __device__ __forceinline__ uint64_t ld_le64(const uint8_t* p) {
     return v;
 }
 
+// ---------------------------------------------------------------------------
+// Block and grid folds (SyncSlot, internal.hpp).  block_fold leaves the
+// workgroup's min / max / or / sum in thread 0.  grid_fold then folds them
+// into the slot with device-scope atomics (performed at the coherence point
+// shared by all XCDs), waits for them to return, and draws a ticket with
+// atomicInc, which wraps to 0 at gridDim.x - 1; the block holding the last
+// ticket has every partial in the slot and takes the totals with atomicExch,
+// restoring the identities.  Only atomics cross workgroups, so no fence or
+// fill launch is needed; returns true in every thread of that last block.
+__device__ __forceinline__ void block_fold(uint32_t& lo, uint32_t& hi, uint32_t& flag, unsigned long long& sum) {
+    __shared__ uint32_t s_lo[kBlock / 64], s_hi[kBlock / 64], s_fl[kBlock / 64];
+    __shared__ unsigned long long s_sum[kBlock / 64];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        lo = min(lo, uint32_t(__shfl_xor(int(lo), o)));
+        hi = max(hi, uint32_t(__shfl_xor(int(hi), o)));
+        flag |= uint32_t(__shfl_xor(int(flag), o));
+        sum += __shfl_xor(sum, o);
+    }
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        s_lo[w] = lo;
+        s_hi[w] = hi;
+        s_fl[w] = flag;
+        s_sum[w] = sum;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0)
+        for (int k = 1; k < kBlock / 64; ++k) {
+            lo = min(lo, s_lo[k]);
+            hi = max(hi, s_hi[k]);
+            flag |= s_fl[k];
+            sum += s_sum[k];
+        }
+}
+
+__device__ __forceinline__ bool grid_fold(SyncSlot* slot, uint32_t lo, uint32_t hi, uint32_t flag,
+                                          unsigned long long sum, uint32_t tot[3], unsigned long long* tot_sum) {
+    __shared__ uint32_t last;
+    if (threadIdx.x == 0) {
+        uint32_t r = 0;
+        if (lo != 0xFFFFFFFFu) r |= atomicMin(&slot->lo, lo);
+        if (hi != 0u) r |= atomicMax(&slot->hi, hi);
+        if (flag) r |= atomicOr(&slot->flag, flag);
+        if (sum) r |= uint32_t(atomicAdd(&slot->sum, sum));
+        // the folds have returned, so they are performed before the ticket
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t t = atomicInc(&slot->ticket, gridDim.x - 1) + (r & 0u);
+        last = t == gridDim.x - 1 ? 1u : 0u;
+        if (last) {
+            tot[0] = atomicExch(&slot->lo, 0xFFFFFFFFu);
+            tot[1] = atomicExch(&slot->hi, 0u);
+            tot[2] = atomicExch(&slot->flag, 0u);
+            *tot_sum = atomicExch(&slot->sum, 0ull);
+        }
+    }
+    __syncthreads();
+    return last != 0u;
+}
+
 // SHA-1 compressions of a len-byte message (FIPS 180-4 padding: + 0x80 + 8 B)
 __device__ __forceinline__ uint64_t compressions(uint64_t len) { return (len + 8) / 64 + 1; }
 
@@ -1165,72 +1225,82 @@ __global__ __launch_bounds__(kBlock) void k_bfs_image(const uint8_t* __restrict_
 // @4, Status u8 @12, TypeInfo u8 @13, KeySize u64 @14, ValueSize u64 @22,
 // Key @30, Value @30+KeySize.  rec_off[i] = start of record i.
 
+// Grid-stride over at most kLocateBlocks workgroups: each block folds its
+// range once (same-address atomics serialise, so a block per 256 records would
+// cost more than the locate itself).
+constexpr uint32_t kLocateBlocks = 1024;
+
 __global__ __launch_bounds__(kBlock) void k_locate(const uint8_t* __restrict__ stream,
                                                     uint64_t stream_len,
                                                     const uint64_t* __restrict__ rec_off, uint64_t n,
                                                     uint64_t* __restrict__ voff,
                                                     uint64_t* __restrict__ vlen,
-                                                    unsigned int* __restrict__ err) {
-    const uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
-    if (i >= n) return;
-    const uint64_t r = rec_off[i];
-    uint64_t o = 0, l = 0;
-    if (r + 30 <= stream_len) {
-        const uint64_t ks = ld_le64(stream + r + 14);
-        const uint64_t vs = ld_le64(stream + r + 22);
-        o = r + 30 + ks;
-        l = vs;
-        if (ks > stream_len || vs > stream_len || o + l > stream_len) {
-            atomicOr(err, 1u);
-            o = 0;
-            l = 0;
+                                                    unsigned int* __restrict__ err, unsigned int* __restrict__ range,
+                                                    SyncSlot* __restrict__ sync) {
+    uint32_t lo = 0xFFFFFFFFu, hi = 0u, bad = 0u;
+    unsigned long long none = 0;
+    const uint64_t stride = uint64_t(gridDim.x) * kBlock;
+#pragma unroll 4
+    for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride) {
+        const uint64_t r = rec_off[i];
+        uint64_t o = 0, l = 0;
+        if (r + 30 <= stream_len) {
+            const uint64_t ks = ld_le64(stream + r + 14);
+            const uint64_t vs = ld_le64(stream + r + 22);
+            o = r + 30 + ks;
+            l = vs;
+            if (ks > stream_len || vs > stream_len || o + l > stream_len) {
+                bad = 1u;
+                o = 0;
+                l = 0;
+            }
+        } else {
+            bad = 1u;
         }
-    } else {
-        atomicOr(err, 1u);
-    }
-    voff[i] = o;
-    vlen[i] = l;
-}
-
-// Range of full-block counts of a batch: out[0] = min, out[1] = max (the
-// launcher initialises them).  Lets the host choose input order (narrow
-// range: no sort, fused tree levels) or the length-sorted work queue.
-__global__ __launch_bounds__(kBlock) void k_len_range(const uint64_t* __restrict__ len, uint64_t n,
-                                                       unsigned int* __restrict__ out) {
-    __shared__ unsigned int part[2][kBlock / 64];
-    unsigned int lo = 0xFFFFFFFFu, hi = 0u;
-    for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += uint64_t(gridDim.x) * kBlock) {
-        const uint64_t b = len[i] >> 6;
-        const unsigned int bb = b > 0xFFFFFFFFull ? 0xFFFFFFFFu : unsigned(b);
+        voff[i] = o;
+        vlen[i] = l;
+        const uint64_t b = l >> 6;
+        const uint32_t bb = b > 0xFFFFFFFFull ? 0xFFFFFFFFu : uint32_t(b);
         lo = min(lo, bb);
         hi = max(hi, bb);
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        lo = min(lo, unsigned(__shfl_xor(int(lo), o)));
-        hi = max(hi, unsigned(__shfl_xor(int(hi), o)));
-    }
-    if ((threadIdx.x & 63) == 0) {
-        part[0][threadIdx.x >> 6] = lo;
-        part[1][threadIdx.x >> 6] = hi;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {  // one atomic pair per block: same-address atomics serialise
-        for (int w = 1; w < kBlock / 64; ++w) {
-            lo = min(lo, part[0][w]);
-            hi = max(hi, part[1][w]);
+    block_fold(lo, hi, bad, none);
+    uint32_t tot[3];
+    unsigned long long tsum;
+    if (grid_fold(sync, lo, hi, bad, 0ull, tot, &tsum) && threadIdx.x == 0) {
+        *err = tot[2];
+        if (range) {
+            range[0] = tot[0];
+            range[1] = tot[1];
         }
-        atomicMin(out, lo);
-        atomicMax(out + 1, hi);
     }
 }
 
-hipError_t launch_len_range(const uint64_t* len, uint64_t n, unsigned int* out, hipStream_t s) {
-    hipError_t e = hipMemsetAsync(out, 0xFF, 4, s);
-    if (e == hipSuccess) e = hipMemsetAsync(out + 1, 0, 4, s);
-    if (e != hipSuccess) return e;
+// Range of full-block counts of a batch: out[0] = min, out[1] = max.  Lets
+// the leaf level choose input order (narrow range: no sort) or the
+// length-sorted work queue, on the device (Gate).
+__global__ __launch_bounds__(kBlock) void k_len_range(const uint64_t* __restrict__ len, uint64_t n,
+                                                       unsigned int* __restrict__ out, SyncSlot* __restrict__ sync) {
+    uint32_t lo = 0xFFFFFFFFu, hi = 0u, none = 0u;
+    unsigned long long zero = 0;
+    for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += uint64_t(gridDim.x) * kBlock) {
+        const uint64_t b = len[i] >> 6;
+        const uint32_t bb = b > 0xFFFFFFFFull ? 0xFFFFFFFFu : uint32_t(b);
+        lo = min(lo, bb);
+        hi = max(hi, bb);
+    }
+    block_fold(lo, hi, none, zero);
+    uint32_t tot[3];
+    unsigned long long tsum;
+    if (grid_fold(sync, lo, hi, 0u, 0ull, tot, &tsum) && threadIdx.x == 0) {
+        out[0] = tot[0];
+        out[1] = tot[1];
+    }
+}
+
+hipError_t launch_len_range(const uint64_t* len, uint64_t n, unsigned int* out, SyncSlot* sync, hipStream_t s) {
     const uint64_t blocks = std::min<uint64_t>((n + kBlock - 1) / kBlock, 256);
-    hipLaunchKernelGGL(k_len_range, dim3(uint32_t(blocks)), dim3(kBlock), 0, s, len, n, out);
+    hipLaunchKernelGGL(k_len_range, dim3(uint32_t(blocks)), dim3(kBlock), 0, s, len, n, out, sync);
     return hipGetLastError();
 }
 
@@ -1313,43 +1383,50 @@ hipError_t launch_leaf_verify(const uint8_t* stream, uint64_t stream_len, const 
     return hipGetLastError();
 }
 
-// Partials of the split decision, over all groups in parallel: q[2] = first
-// group (length-sorted, longest first) whose first value has at most split full
-// blocks (atomicMin), q[4..5] = the batch's work, sum over groups of their
-// first value's compressions (atomicAdd).  k_leaf_queue decides from them.
+// The queue's state for k_leaf_queue, over all groups in parallel: every block
+// zeroes its share of the per-SIMD arrivals and claim flags; the header is
+// written by the grid's last block (grid_fold): tickets 0, q[2] = first group
+// (length-sorted, longest first) whose first value has at most split full
+// blocks (0xFFFFFFFF if none), q[4..5] = the batch's work, the sum over groups
+// of their first value's compressions.  k_leaf_queue decides from them.
 __global__ __launch_bounds__(kBlock) void k_queue_split(const uint64_t* __restrict__ len,
                                                      const uint32_t* __restrict__ perm, uint32_t ngroups,
-                                                     uint32_t split, uint32_t* __restrict__ q, Gate gate) {
+                                                     uint32_t split, uint32_t* __restrict__ q, uint64_t nq,
+                                                     SyncSlot* __restrict__ sync, Gate gate) {
     if (!gate.open()) return;
+    const uint64_t stride = uint64_t(gridDim.x) * kBlock;
+    for (uint64_t i = kQueueHeader + uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < nq; i += stride) q[i] = 0u;
     unsigned long long w = 0;
-    uint32_t b = 0xFFFFFFFFu;
+    uint32_t b = 0xFFFFFFFFu, hi = 0u, none = 0u;
     for (uint32_t g = blockIdx.x * kBlock + threadIdx.x; g < ngroups; g += gridDim.x * kBlock) {
         const uint64_t l = len[perm[uint64_t(g) * 64]];
         w += compressions(l);
         if ((l >> 6) <= split && g < b) b = g;
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        w += __shfl_xor(w, o);
-        b = min(b, uint32_t(__shfl_xor(int(b), o)));
-    }
-    if ((threadIdx.x & 63) == 0) {
-        atomicAdd(reinterpret_cast<unsigned long long*>(q) + 2, w);
-        atomicMin(q + 2, b);
+    block_fold(b, hi, none, w);
+    uint32_t tot[3];
+    unsigned long long work;
+    if (grid_fold(sync, b, 0u, 0u, w, tot, &work) && threadIdx.x == 0) {
+        q[0] = 0u;
+        q[1] = 0u;
+        q[2] = tot[0];
+        q[3] = 0u;
+        reinterpret_cast<unsigned long long*>(q)[2] = work;
+        q[6] = 0u;
+        q[7] = 0u;
     }
 }
 
 hipError_t launch_leaf_queue(const uint8_t* base, const uint64_t* off, const uint64_t* len,
                              const uint32_t* perm, uint64_t n, bool aligned, int ring, uint32_t* q,
                              uint32_t simds, uint32_t waves_per_simd, uint32_t split, uint8_t* nodes,
-                             hipStream_t s, Gate gate) {
+                             SyncSlot* sync, hipStream_t s, Gate gate) {
     const uint32_t ngroups = uint32_t((n + 63) / 64);
     const uint32_t waves = simds * waves_per_simd;
-    hipError_t e = hipMemsetAsync(q, 0, queue_words(n) * sizeof(uint32_t), s);
-    if (e == hipSuccess) e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(q + 2), 0xFFFFFFFFu, 1, s);
-    if (e != hipSuccess) return e;
-    const uint32_t sblocks = std::min<uint32_t>((ngroups + kBlock - 1) / kBlock, 256u);
-    hipLaunchKernelGGL(k_queue_split, dim3(sblocks), dim3(kBlock), 0, s, len, perm, ngroups, split, q, gate);
+    const uint64_t nq = queue_words(n);
+    const uint32_t sblocks = uint32_t(std::min<uint64_t>((nq + kBlock - 1) / kBlock, 256u));
+    hipLaunchKernelGGL(k_queue_split, dim3(sblocks), dim3(kBlock), 0, s, len, perm, ngroups, split, q, nq, sync,
+                       gate);
     if (ring == 14)
         hipLaunchKernelGGL(k_leaf_queue<13>, dim3(waves), dim3(64), 0, s, base, off, len, perm, n, ngroups, simds, q, nodes, gate);
     else if (ring == 13)
@@ -1402,10 +1479,10 @@ hipError_t launch_bfs_image(const uint8_t* nodes, const BfsLayout& lay, uint8_t*
 }
 
 hipError_t launch_locate(const uint8_t* stream, uint64_t stream_len, const uint64_t* rec_off,
-                         uint64_t n, uint64_t* voff, uint64_t* vlen, unsigned int* err,
-                         hipStream_t s) {
-    hipLaunchKernelGGL(k_locate, dim3(grid_for(n)), dim3(kBlock), 0, s, stream, stream_len,
-                       rec_off, n, voff, vlen, err);
+                         uint64_t n, uint64_t* voff, uint64_t* vlen, unsigned int* err, unsigned int* range,
+                         SyncSlot* sync, hipStream_t s) {
+    hipLaunchKernelGGL(k_locate, dim3(std::min(grid_for(n), kLocateBlocks)), dim3(kBlock), 0, s, stream,
+                       stream_len, rec_off, n, voff, vlen, err, range, sync);
     return hipGetLastError();
 }
 
