@@ -71,6 +71,7 @@ def parse():
     ap.add_argument("--queue-waves", type=int, default=0, help="NKV_OPT_QUEUE_WAVES override")
     ap.add_argument("--queue-ring", type=int, default=0, help="NKV_OPT_QUEUE_RING override (2, 3, 4)")
     ap.add_argument("--leaves", type=int, default=1 << 20)
+    ap.add_argument("--key-bytes", type=int, default=16, help="records configs: KeySize (the Value starts at +30+key)")
     ap.add_argument("--value-bytes", type=int, default=4096)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-leaves", type=int, default=1 << 20)
@@ -157,7 +158,7 @@ def main():
     if records:
         import numpy as np
         n, rb = args.leaves, args.value_bytes
-        ks = 16
+        ks = args.key_bytes
         vlen = rb - 30 - ks  # record.go:191-199 header 30 B, 16-B key, the rest is the Value
         stream_len = n * rb
         data = torch.empty(stream_len, dtype=torch.uint8, device="cuda")

@@ -9,7 +9,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "gpurun_out", "prof")
 DST = os.path.join(ROOT, "profiles")
 tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
-for name in ("cfg2", "cfg3", "records", "crc", "bloom"):
+for name in ("cfg2", "cfg3", "records", "records_verify", "crc", "bloom"):
     stats = os.path.join(SRC, f"{name}_kernel_stats.csv")
     line = os.path.join(SRC, f"{name}.json")
     if os.path.exists(stats):
