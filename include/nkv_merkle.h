@@ -118,9 +118,11 @@ int nkv_ctx_sync(nkv_ctx *ctx);
                                   the NKV_HOST_THREADS environment variable) */
 #define NKV_OPT_STAGE_CHUNK 8  /* host-buffer API: bytes per pinned staging chunk (multiple of
                                   4096, default 32 MiB; three chunks are in flight) */
-#define NKV_OPT_BLOOM_PATH 10  /* filter inserts: 1 (default) = group the bit updates by 32768-bit
-                                  range (counting sort) and set them in LDS, one workgroup per
-                                  range; 0 = one device atomicOr per bit */
+#define NKV_OPT_BLOOM_PATH 10  /* filter inserts: 2 (default) = group the bit updates by 32768-bit
+                                  range from one hash pass (each tile counting-sorted in LDS and
+                                  staged), then set them in LDS, one workgroup per range; 1 = the
+                                  same grouping by a global counting sort (hashes twice); 0 = one
+                                  device atomicOr per bit */
 #define NKV_OPT_QUEUE_RING 9   /* work-queue kernel: LDS ring of aligned chunks with 2 slots
                                   (one block of DMA lookahead), 3 / 4 = pipelined ring
                                   with 1 / 2 blocks of lookahead; 12 / 13 / 14 = pipelined

@@ -288,6 +288,170 @@ hipError_t launch_bloom_ranges(int mode, const uint8_t* base, const uint64_t* of
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Staged insert (NKV_OPT_BLOOM_PATH 2): each key is loaded and hashed once.  A
+// tile of kBloomBlock x kpt keys hashes into LDS (a thread-major list of its
+// updates, counted per range), counting-sorts them by range inside LDS, and
+// writes the sorted list contiguously to its own stage area, with per-range
+// counts and starts (range-major over tiles).  One workgroup per range then
+// reads its segment of every tile and sets its bits in LDS.  The range path
+// above hashes every key twice (count, scatter) and scatters 4-byte updates
+// one by one across the whole update array.
+constexpr uint32_t kStageLdsWords = 16384 - 64;  // 64 KiB of dynamic LDS, less the scan's words
+constexpr int kApplyBlock = 1024;
+
+__device__ __forceinline__ uint32_t bloom_block_exclusive(uint32_t v, uint32_t* wsum, uint32_t* total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = uint32_t(__shfl_up(int(x), o));
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    uint32_t before = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < kBloomBlock / 64; ++w) {
+        if (w < wave) before += wsum[w];
+        tot += wsum[w];
+    }
+    __syncthreads();
+    *total = tot;
+    return before + x - v;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kBloomBlock) void k_bloom_stage(const uint8_t* __restrict__ base,
+                                                             const uint64_t* __restrict__ off,
+                                                             const uint64_t* __restrict__ len, uint64_t stream_len,
+                                                             uint64_t n, uint32_t m, uint64_t M, uint32_t k,
+                                                             uint32_t seed0, uint32_t nranges, uint32_t tiles,
+                                                             uint32_t kpt, uint32_t* __restrict__ stage,
+                                                             uint32_t* __restrict__ tcount,
+                                                             uint32_t* __restrict__ tstart, unsigned int* err) {
+    extern __shared__ uint32_t lds[];
+    __shared__ uint32_t wsum[kBloomBlock / 64];
+    const uint32_t per = kpt * k;  // update slots per thread
+    uint32_t* A = lds;                            // thread-major, per slots each
+    uint32_t* B = A + per * kBloomBlock;          // sorted by range
+    uint32_t* cnt = B + per * kBloomBlock;        // nranges counts, then cursors
+    for (uint32_t r = threadIdx.x; r < nranges; r += kBloomBlock) cnt[r] = 0u;
+    __syncthreads();
+    uint32_t* mine = A + threadIdx.x * per;
+    uint32_t na = 0;
+    const uint64_t t0 = uint64_t(blockIdx.x) * kBloomBlock * kpt;
+    for (uint32_t q = 0; q < kpt; ++q) {
+        const uint64_t i = t0 + uint64_t(q) * kBloomBlock + threadIdx.x;
+        if (i < n)
+            bloom_indices<MODE>(base, off, len, stream_len, i, m, M, k, seed0, err, [&](uint32_t idx) {
+                mine[na++] = idx;
+                atomicAdd(&cnt[idx >> kBloomRangeShift], 1u);
+            });
+    }
+    __syncthreads();
+    // exclusive scan of the counts: thread t owns a contiguous run of ranges
+    const uint32_t run = (nranges + kBloomBlock - 1) / kBloomBlock;
+    const uint32_t r0 = threadIdx.x * run, r1 = min(r0 + run, nranges);
+    uint32_t mysum = 0;
+    for (uint32_t r = r0; r < r1; ++r) mysum += cnt[r];
+    uint32_t total;
+    uint32_t at = bloom_block_exclusive(mysum, wsum, &total);
+    for (uint32_t r = r0; r < r1; ++r) {
+        const uint32_t c = cnt[r];
+        tcount[uint64_t(r) * tiles + blockIdx.x] = c;
+        tstart[uint64_t(r) * tiles + blockIdx.x] = at;
+        cnt[r] = at;  // becomes the range's cursor
+        at += c;
+    }
+    __syncthreads();
+    for (uint32_t j = 0; j < na; ++j) {
+        const uint32_t idx = mine[j];
+        B[atomicAdd(&cnt[idx >> kBloomRangeShift], 1u)] = idx;
+    }
+    __syncthreads();
+    uint32_t* dst = stage + uint64_t(blockIdx.x) * per * kBloomBlock;
+    for (uint32_t j = threadIdx.x; j < total; j += kBloomBlock) dst[j] = B[j];
+}
+
+// one workgroup per range: a thread per tile reads that tile's segment
+// (unrolled, so several loads are in flight) into the LDS bitmap
+__global__ __launch_bounds__(kApplyBlock) void k_bloom_apply_staged(const uint32_t* __restrict__ stage,
+                                                                    uint32_t tile_slots,
+                                                                    const uint32_t* __restrict__ tcount,
+                                                                    const uint32_t* __restrict__ tstart,
+                                                                    uint32_t tiles, uint32_t words,
+                                                                    uint32_t* __restrict__ bits) {
+    __shared__ uint32_t w[kBloomRangeWords];
+    const uint32_t r = blockIdx.x;
+    for (uint32_t t = threadIdx.x; t < kBloomRangeWords; t += kApplyBlock) w[t] = 0u;
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < tiles; t += kApplyBlock) {
+        const uint32_t c = tcount[uint64_t(r) * tiles + t];
+        const uint32_t* seg = stage + uint64_t(t) * tile_slots + tstart[uint64_t(r) * tiles + t];
+        uint32_t j = 0;
+        for (; j + 4 <= c; j += 4) {
+            const uint32_t a = seg[j], b = seg[j + 1], d = seg[j + 2], e = seg[j + 3];
+            atomicOr(&w[(a >> 5) & (kBloomRangeWords - 1)], 1u << (a & 31u));
+            atomicOr(&w[(b >> 5) & (kBloomRangeWords - 1)], 1u << (b & 31u));
+            atomicOr(&w[(d >> 5) & (kBloomRangeWords - 1)], 1u << (d & 31u));
+            atomicOr(&w[(e >> 5) & (kBloomRangeWords - 1)], 1u << (e & 31u));
+        }
+        for (; j < c; ++j) {
+            const uint32_t a = seg[j];
+            atomicOr(&w[(a >> 5) & (kBloomRangeWords - 1)], 1u << (a & 31u));
+        }
+    }
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < kBloomRangeWords; t += kApplyBlock) {
+        const uint64_t g = uint64_t(r) * kBloomRangeWords + t;
+        if (g < words && w[t]) bits[g] |= w[t];  // range r's words have no other writer
+    }
+}
+
+// keys per thread of a staged tile: two update lists (per slots each) and the
+// range counters fit the 64 KiB of dynamic LDS; 0 = not applicable
+static uint32_t bloom_stage_kpt(uint32_t k, uint32_t nranges) {
+    if (k == 0 || nranges >= kStageLdsWords) return 0u;
+    const uint32_t kpt = (kStageLdsWords - nranges) / 2 / (uint32_t(kBloomBlock) * k);
+    return kpt < 32u ? kpt : 32u;
+}
+
+uint64_t bloom_staged_scratch_words(uint64_t n, uint32_t m, uint32_t k) {
+    const uint64_t nranges = (uint64_t(m) + (1u << kBloomRangeShift) - 1) >> kBloomRangeShift;
+    if (nranges > kBloomMaxRanges) return 0;
+    const uint32_t kpt = bloom_stage_kpt(k, uint32_t(nranges));
+    if (kpt == 0) return 0;  // the range or atomic path serves these
+    const uint64_t tiles = (n + uint64_t(kBloomBlock) * kpt - 1) / (uint64_t(kBloomBlock) * kpt);
+    return tiles * kpt * k * kBloomBlock + 2 * tiles * nranges;
+}
+
+hipError_t launch_bloom_staged(int mode, const uint8_t* base, const uint64_t* off, const uint64_t* len,
+                               uint64_t stream_len, uint64_t n, uint32_t m, uint32_t k, uint32_t seed0,
+                               uint32_t* bits, unsigned int* err, uint32_t* scratch, hipStream_t s) {
+    if (n == 0 || k == 0) return hipSuccess;
+    const uint32_t nranges = (m + (1u << kBloomRangeShift) - 1) >> kBloomRangeShift;
+    const uint32_t kpt = bloom_stage_kpt(k, nranges);
+    const uint64_t tiles = (n + uint64_t(kBloomBlock) * kpt - 1) / (uint64_t(kBloomBlock) * kpt);
+    const uint32_t slots = kpt * k * kBloomBlock;
+    uint32_t* stage = scratch;
+    uint32_t* tcount = stage + tiles * slots;
+    uint32_t* tstart = tcount + tiles * nranges;
+    const uint64_t M = fastmod_magic(m);
+    const uint32_t words = (m + 31) / 32;
+    const uint32_t T = uint32_t(tiles);
+    const size_t lds = (size_t(2) * slots + nranges) * sizeof(uint32_t);
+    if (mode == 0)
+        hipLaunchKernelGGL(k_bloom_stage<0>, dim3(T), dim3(kBloomBlock), lds, s, base, off, len, stream_len, n, m, M,
+                           k, seed0, nranges, T, kpt, stage, tcount, tstart, err);
+    else
+        hipLaunchKernelGGL(k_bloom_stage<1>, dim3(T), dim3(kBloomBlock), lds, s, base, off, len, stream_len, n, m, M,
+                           k, seed0, nranges, T, kpt, stage, tcount, tstart, err);
+    hipLaunchKernelGGL(k_bloom_apply_staged, dim3(nranges), dim3(kApplyBlock), 0, s, stage, slots, tcount, tstart, T,
+                       words, bits);
+    return hipGetLastError();
+}
+
 hipError_t launch_bloom(int mode, bool query, const uint8_t* base, const uint64_t* off, const uint64_t* len,
                         uint64_t stream_len, uint64_t n, uint32_t m, uint32_t k, uint32_t seed0, uint32_t* bits,
                         uint8_t* out, unsigned int* err, hipStream_t s) {

@@ -104,7 +104,7 @@ struct nkv_ctx {
     int queue_split = 32;   // NKV_OPT_QUEUE_SPLIT
     int queue_waves = 4;    // NKV_OPT_QUEUE_WAVES
     int queue_ring = 13;    // NKV_OPT_QUEUE_RING
-    int bloom_path = 1;     // NKV_OPT_BLOOM_PATH
+    int bloom_path = 2;     // NKV_OPT_BLOOM_PATH
     int crc_load = 1;       // NKV_OPT_CRC_LOAD
     bool timing = false;
     bool timed = false;
@@ -467,7 +467,7 @@ int nkv_ctx_set_option(nkv_ctx* c, int key, int64_t value) {
             c->crc_load = int(value);
             return NKV_OK;
         case NKV_OPT_BLOOM_PATH:
-            if (value < 0 || value > 1) return NKV_ERR_INVALID;
+            if (value < 0 || value > 2) return NKV_ERR_INVALID;
             c->bloom_path = int(value);
             return NKV_OK;
         case NKV_OPT_QUEUE_RING:
@@ -1015,7 +1015,13 @@ int nkv_record_crc_dev(nkv_ctx* c, const void* d_stream, uint64_t stream_len, co
 static int bloom_insert(nkv_ctx* c, int mode, const uint8_t* base, const uint64_t* off, const uint64_t* len,
                         uint64_t stream_len, uint64_t n, uint32_t m, uint32_t k, uint32_t seed0, uint32_t* bits,
                         unsigned int* err) {
-    const uint64_t words = c->bloom_path == 1 && n >= 4096 ? bloom_ranges_scratch_words(n, m, k) : 0;
+    const uint64_t staged = c->bloom_path == 2 && n >= 4096 ? bloom_staged_scratch_words(n, m, k) : 0;
+    if (staged) {
+        TRY(grow(c->d_tmp, 4 * staged));
+        return st(launch_bloom_staged(mode, base, off, len, stream_len, n, m, k, seed0, bits, err,
+                                      static_cast<uint32_t*>(c->d_tmp.p), c->stream));
+    }
+    const uint64_t words = c->bloom_path >= 1 && n >= 4096 ? bloom_ranges_scratch_words(n, m, k) : 0;
     if (words) {
         TRY(grow(c->d_tmp, 4 * words));
         return st(launch_bloom_ranges(mode, base, off, len, stream_len, n, m, k, seed0, bits, err,

@@ -127,6 +127,13 @@ uint64_t bloom_ranges_scratch_words(uint64_t n, uint32_t m, uint32_t k);
 hipError_t launch_bloom_ranges(int mode, const uint8_t* base, const uint64_t* off, const uint64_t* len,
                                uint64_t stream_len, uint64_t n, uint32_t m, uint32_t k, uint32_t seed0,
                                uint32_t* bits, unsigned int* err, uint32_t* scratch, hipStream_t s);
+// Staged insert (one hash pass; mode as launch_bloom); scratch:
+// bloom_staged_scratch_words u32 (0 = not applicable: k > 32 or more than
+// 4096 ranges).
+uint64_t bloom_staged_scratch_words(uint64_t n, uint32_t m, uint32_t k);
+hipError_t launch_bloom_staged(int mode, const uint8_t* base, const uint64_t* off, const uint64_t* len,
+                               uint64_t stream_len, uint64_t n, uint32_t m, uint32_t k, uint32_t seed0,
+                               uint32_t* bits, unsigned int* err, uint32_t* scratch, hipStream_t s);
 hipError_t launch_fill(uint8_t* buf, uint64_t nbytes, uint64_t seed, hipStream_t s);
 // out[0] / out[1] = min / max of len[i] / 64 over the batch (2 u32 on the device)
 hipError_t launch_len_range(const uint64_t* len, uint64_t n, unsigned int* out, SyncSlot* sync, hipStream_t s);

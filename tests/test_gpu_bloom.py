@@ -136,14 +136,15 @@ def test_bloom_sstable_shape_1m_keys(nkv, oracle):
     assert np.array_equal(d_bits.cpu().numpy()[:want.size], want)
 
 
-@pytest.mark.parametrize("path", [0, 1])
+@pytest.mark.parametrize("path", [0, 1, 2])
 @pytest.mark.parametrize("n,m,k", [(5000, 47924, 7), (4096, 1, 1), (20000, 5000, 20), (70000, 1 << 22, 3),
-                                   (9000, 134217728, 2)])
+                                   (9000, 134217728, 2), (40000, 383416, 40)])
 def test_bloom_insert_paths_match_oracle(nkv, oracle, path, n, m, k):
-    """Both insert paths -- range-privatised (32768-bit ranges in LDS, counting
-    sort of the updates) and one atomicOr per bit -- on filters of 1 bit to
-    4096 ranges, k up to 20 (two register passes), ragged keys, bits OR-ed into
-    a non-empty filter."""
+    """Every insert path -- range-privatised (32768-bit ranges in LDS, counting
+    sort of the updates), the staged form of it (one hash pass, tiles sorted in
+    LDS; k = 40 falls back to the range path) and one atomicOr per bit -- on
+    filters of 1 bit to 4096 ranges, k up to 40 (several register passes),
+    ragged keys, bits OR-ed into a non-empty filter."""
     torch = _torch()
     _lib, _ = nkv
     ctx = _lib.Context(0)
@@ -173,10 +174,13 @@ def test_bloom_insert_paths_match_oracle(nkv, oracle, path, n, m, k):
     assert not got[want.size:].any()
 
 
-def test_bloom_from_records_range_path(nkv, oracle):
-    """The records form (keys at rec + 30) through the range-privatised path."""
+@pytest.mark.parametrize("path", [1, 2])
+def test_bloom_from_records_range_path(nkv, oracle, path):
+    """The records form (keys at rec + 30) through the range-privatised path
+    and its staged form."""
     from nakevaleng_amd import record, sstable
     _lib, ctx = nkv
+    ctx.set_option(_lib.NKV_OPT_BLOOM_PATH, path)
     rng = np.random.default_rng(44)
     recs = [record.New(rng.integers(0, 256, int(kk), dtype=np.uint8).tobytes(), b"v" * int(v), timestamp=1)
             for kk, v in zip(rng.integers(1, 40, 6000), rng.integers(0, 50, 6000))]
@@ -187,4 +191,5 @@ def test_bloom_from_records_range_path(nkv, oracle):
     kl = np.array([len(x) for x in keys], np.uint64)
     ko = np.zeros_like(kl)
     ko[1:] = np.cumsum(kl[:-1])
+    ctx.set_option(_lib.NKV_OPT_BLOOM_PATH, 1)
     assert bf.Contents == oracle.bloom_insert(kd, ko, kl, bf.M, bf.K, 99).tobytes()

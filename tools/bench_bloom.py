@@ -27,12 +27,15 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--verify", action="store_true")
+    ap.add_argument("--path", type=int, default=-1, help="NKV_OPT_BLOOM_PATH override")
     args = ap.parse_args()
     n, rb, ks = args.records, args.rec_bytes, args.key_bytes
     L = _lib.lib()
     ctx = _lib.Context(0)
     s = torch.cuda.current_stream()
     ctx.set_stream(s.cuda_stream)
+    if args.path >= 0:
+        ctx.set_option(_lib.NKV_OPT_BLOOM_PATH, args.path)
     m, k = bloomfilter.params(n, 0.01)
     seed0 = 0x6E616B65
     data = torch.empty(n * rb, dtype=torch.uint8, device="cuda")
