@@ -16,14 +16,20 @@ DST = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 KERNEL = "void nkv::k_leaf<0, 1>("
 
 vals = collections.defaultdict(list)
-for name in ("req", "fetch", "write"):
-    with open(os.path.join(SRC, f"{name}_counter_collection.csv")) as f:
+for name in ("req", "fetch", "write", "sizes"):
+    path = os.path.join(SRC, f"{name}_counter_collection.csv")
+    if not os.path.exists(path):
+        continue
+    with open(path) as f:
         for r in csv.DictReader(f):
             if r["Kernel_Name"].startswith(KERNEL):
                 vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
 mean = {k: sum(v) / len(v) for k, v in vals.items()}
 old = json.load(open(DST)) if os.path.exists(DST) else {}
 req = mean["TCC_EA0_RDREQ"]
+sized = all(c in mean for c in ("TCC_EA0_RDREQ_32B", "TCC_EA0_RDREQ_64B", "TCC_EA0_RDREQ_128B"))
+read_bytes = (32 * mean["TCC_EA0_RDREQ_32B"] + 64 * mean["TCC_EA0_RDREQ_64B"] + 128 * mean["TCC_EA0_RDREQ_128B"]
+              if sized else None)
 out = {
     "about": "rocprofv3 --pmc passes (separate runs, kernel trace only; tools/profile_r01.sh) on bench.py cfg2 "
              "(1 Mi x 4 KiB), k_leaf<0, 1> (leaf SHA-1, level 0 only); values are per-dispatch means over "
@@ -38,17 +44,20 @@ out = {
         "TCC_EA0_RDREQ_32B": mean["TCC_EA0_RDREQ_32B"],
         "FETCH_SIZE_KB": mean["FETCH_SIZE"],
         "WRITE_SIZE_KB": mean["WRITE_SIZE"],
+        "TCC_EA0_RDREQ_64B": mean.get("TCC_EA0_RDREQ_64B"),
+        "TCC_EA0_RDREQ_128B": mean.get("TCC_EA0_RDREQ_128B"),
     },
+    "read_bytes_per_launch": read_bytes,
     "fetch_calib_k_read": old.get("fetch_calib_k_read"),
     "hbm_read_bytes_bounds_per_launch": [req * 64, req * 128],
-    "hbm_bytes_per_launch": None,
-    "note": "gfx950 tallies 64-B and 128-B read requests alike in TCC_EA0_RDREQ and TCC_BUBBLE reads 0, so the "
-            "read bytes are bounded by RDREQ x 64 and RDREQ x 128; the algorithmic payload lies inside that "
-            "interval, i.e. the counters are consistent with each byte fetched once.  The guide's FETCH_SIZE x 2 "
-            "correction holds only for uniform 128-B streams: on tools/fetch_calib.bin, which reads exactly 4 GiB "
-            "with the same LDS-DMA pattern, FETCH_SIZE x 1024 is 0.82 of the true bytes, so no single factor "
-            "transfers and traffic stays null.  WRITE_SIZE is the 20 MiB of leaf digests (the tree levels are "
-            "built by k_reduce2 / k_reduce).",
+    "hbm_bytes_per_launch": (read_bytes + 1024 * mean["WRITE_SIZE"]) if sized else None,
+    "note": "Read bytes = 32 x TCC_EA0_RDREQ_32B + 64 x _64B + 128 x _128B (a separate pass, tools/pmc_sizes.sh): "
+            "the L2's memory-side requests, Infinity-Cache hits included (MI355X guide, HBM section), so an upper "
+            "bound on HBM reads.  Nearly every request is a 128-B line; the guide's FETCH_SIZE x 2 correction agrees "
+            "within 3 %.  The leaf kernel fetches 1.17 x its payload: each value's 64-B block is half of a 128-B "
+            "line, and part of the other halves are evicted before the next block uses them (tools/fetch_calib.hip, "
+            "the same pattern without the hashing and so 3x faster, re-fetches 1.63 x).  WRITE_SIZE is the 20 MiB "
+            "of leaf digests (the tree levels are built by k_reduce2 / k_reduce).",
 }
 with open(DST, "w") as f:
     json.dump(out, f, indent=1)
