@@ -24,4 +24,5 @@ pmc() {  # name, counters
 mkdir -p gpurun_out/pmc
 pmc req TCC_EA0_RDREQ TCC_EA0_RDREQ_DRAM TCC_BUBBLE TCC_EA0_RDREQ_32B &&
 pmc fetch FETCH_SIZE &&
-pmc write WRITE_SIZE
+pmc write WRITE_SIZE &&
+pmc sizes TCC_EA0_RDREQ TCC_EA0_RDREQ_32B TCC_EA0_RDREQ_64B TCC_EA0_RDREQ_128B
