@@ -691,22 +691,25 @@ __device__ __forceinline__ void sha1_blocks_ring_vc(uint8_t* wbuf, const uint8_t
     const int lane = threadIdx.x & 63;
     const uint32_t dq = (uint32_t(lane) & 3u) ^ ((uint32_t(lane) >> 4) & 3u);
     const uint8_t* src[4];
-    uint32_t lastc[4];
+    uint32_t lastoff[4];  // byte offset of the role value's last full block (< 4 GiB)
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int j = 16 * k + (lane >> 2);
         const uint64_t aj = uint64_t(__shfl(int64_t(reinterpret_cast<uintptr_t>(p)), j));
         const uint32_t nj = uint32_t(__shfl(int(my_nfull), j));
         src[k] = (nj ? reinterpret_cast<const uint8_t*>(aj) : g_ring_dummy) + 16 * dq;
-        lastc[k] = nj ? nj - 1 : 0u;
+        lastoff[k] = nj ? 64u * (nj - 1) : 0u;
     }
     const uint32_t nmax = wave_max_u32(my_nfull);
     if (nmax == 0) return;
+    // one v_min and one 64-bit add per DMA instruction: the chunk offset 64 c
+    // is wave-uniform
     auto issue = [&](uint32_t c) {
         uint8_t* dst = wbuf + 4096 * (c % R);
+        const uint32_t cb = 64u * c;
 #pragma unroll
         for (int k = 0; k < 4; ++k)
-            __builtin_amdgcn_global_load_lds(src[k] + 64ull * min(c, lastc[k]), dst + 1024 * k, 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(src[k] + min(cb, lastoff[k]), dst + 1024 * k, 16, 0, 0);
     };
     const uint32_t lds0 = uint32_t(reinterpret_cast<uintptr_t>(wbuf));
     const uint32_t row = lds0 + 64u * uint32_t(lane);
@@ -716,16 +719,11 @@ __device__ __forceinline__ void sha1_blocks_ring_vc(uint8_t* wbuf, const uint8_t
 #pragma unroll
         for (int q = 0; q < 4; ++q) v[q] = ds_read_b128_asm(s0 + 16u * (uint32_t(q) ^ swz));
     };
-#pragma unroll
-    for (uint32_t c = 0; c < uint32_t(R); ++c) issue(c);
-    wait_vmcnt<4 * (R - 1)>();
-    u32x4 cur[4];
-    read_window(0u, cur);
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(cur[0]), "+v"(cur[1]), "+v"(cur[2]), "+v"(cur[3]) : : "memory");
-    for (uint32_t b = 0; b < nmax; ++b) {
+    // block b from cur while window b+1 lands in nxt; the loop below runs it
+    // twice per iteration with the roles swapped, so no window is copied
+    auto step = [&](uint32_t b, u32x4 cur[4], u32x4 nxt[4]) {
         issue(b + R);
         wait_vmcnt<4 * (R - 1)>();
-        u32x4 nxt[4];
         read_window(b + 1, nxt);
         uint4 c4[4];
 #pragma unroll
@@ -734,9 +732,19 @@ __device__ __forceinline__ void sha1_blocks_ring_vc(uint8_t* wbuf, const uint8_t
         be16_from_raw(c4, w);
         if (b < my_nfull) sha1_compress(h, w);
         asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(nxt[0]), "+v"(nxt[1]), "+v"(nxt[2]), "+v"(nxt[3]) : : "memory");
+    };
 #pragma unroll
-        for (int q = 0; q < 4; ++q) cur[q] = nxt[q];
+    for (uint32_t c = 0; c < uint32_t(R); ++c) issue(c);
+    wait_vmcnt<4 * (R - 1)>();
+    u32x4 wa[4], wb[4];
+    read_window(0u, wa);
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(wa[0]), "+v"(wa[1]), "+v"(wa[2]), "+v"(wa[3]) : : "memory");
+    uint32_t b = 0;
+    for (; b + 2 <= nmax; b += 2) {
+        step(b, wa, wb);
+        step(b + 1, wb, wa);
     }
+    if (b < nmax) step(b, wa, wb);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
