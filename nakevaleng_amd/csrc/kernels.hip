@@ -296,6 +296,20 @@ __device__ __forceinline__ void sha1_tail(const uint8_t* p, uint64_t len, uint32
     uint32_t w[16];
     const uint64_t nfull = len >> 6;
     const uint32_t rem = uint32_t(len & 63);
+    const uint64_t bits = len << 3;
+    // A wave-level step issues every instruction whatever the exec mask, so the
+    // branches below are taken on wave votes: a wave whose values are all
+    // whole blocks (every 4 KiB SSTable value) pays neither the byte loads and
+    // masking nor a second compression that no lane needs.
+    if (__all(rem == 0u)) {
+        w[0] = 0x80000000u;
+#pragma unroll
+        for (int j = 1; j < 14; ++j) w[j] = 0u;
+        w[14] = uint32_t(bits >> 32);
+        w[15] = uint32_t(bits);
+        sha1_compress(h, w);
+        return;
+    }
     const uint8_t* pt = p + 64 * nfull;
     if (ALIGNED) {
         const uint4* q = reinterpret_cast<const uint4*>(pt);
@@ -316,19 +330,23 @@ __device__ __forceinline__ void sha1_tail(const uint8_t* p, uint64_t len, uint32
         if (v >= 0 && v < 4) x |= 0x80u << (24 - 8 * v);
         w[j] = x;
     }
-    const uint64_t bits = len << 3;
     const bool two = rem >= 56;
     if (!two) {
         w[14] = uint32_t(bits >> 32);
         w[15] = uint32_t(bits);
     }
     sha1_compress(h, w);
-    if (two) {
+    if (__any(two)) {
+        uint32_t h2[5];
 #pragma unroll
         for (int j = 0; j < 14; ++j) w[j] = 0u;
         w[14] = uint32_t(bits >> 32);
         w[15] = uint32_t(bits);
-        sha1_compress(h, w);
+#pragma unroll
+        for (int i = 0; i < 5; ++i) h2[i] = h[i];
+        sha1_compress(h2, w);
+#pragma unroll
+        for (int i = 0; i < 5; ++i) h[i] = two ? h2[i] : h[i];
     }
 }
 
