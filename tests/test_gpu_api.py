@@ -215,3 +215,39 @@ def test_tree_from_records_dev_async_and_bad_header(nkv, oracle):
     assert int(d_err.item()) == 1
     assert L.nkv_tree_from_records_dev(ctx.h, d_bad.data_ptr(), len(stream), d_roff.data_ptr(), n,
                                        d_nodes.data_ptr(), None) == _lib.NKV_ERR_INVALID
+    # the grid-fold slots restore themselves: a good stream after a bad one
+    # reports no error
+    d_err.fill_(7)
+    _lib.check(L.nkv_tree_from_records_dev(ctx.h, d_stream.data_ptr(), len(stream), d_roff.data_ptr(), n,
+                                           d_nodes.data_ptr(), d_err.data_ptr()))
+    torch.cuda.synchronize()
+    assert int(d_err.item()) == 0
+    assert np.array_equal(d_nodes.cpu().numpy().reshape(-1, 20), want)
+
+
+@pytest.mark.parametrize("n", [4096, 5000, 300000])
+def test_tree_from_records_dev_uniform_gated(nkv, oracle, n):
+    """Uniform records (the SSTable case) through the device-range plan: k_locate
+    measures the range in its grid fold, the input-order kernel runs, twice in a
+    row (the fold slots must be back at their identities between calls)."""
+    import torch
+    _lib, ctx = nkv
+    L = _lib.lib()
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    rb, ks = 512, 16
+    body = oracle.splitmix64_bytes(n * rb, n).reshape(n, rb)
+    body[:, 14:22] = np.frombuffer(np.uint64(ks).tobytes(), np.uint8)
+    body[:, 22:30] = np.frombuffer(np.uint64(rb - 30 - ks).tobytes(), np.uint8)
+    roff = np.arange(n, dtype=np.uint64) * rb
+    want = oracle.tree_from_digests(oracle.leaf_hashes(body.reshape(-1), roff + 30 + ks,
+                                                       np.full(n, rb - 30 - ks, np.uint64), threads=8))
+    d_stream = torch.from_numpy(body.reshape(-1).copy()).cuda()
+    d_roff = torch.from_numpy(roff.view(np.int64)).cuda()
+    d_err = torch.full((1,), 7, dtype=torch.int32, device="cuda")
+    for _ in range(2):
+        d_nodes = torch.zeros(L.nkv_total_nodes(n) * 20, dtype=torch.uint8, device="cuda")
+        _lib.check(L.nkv_tree_from_records_dev(ctx.h, d_stream.data_ptr(), n * rb, d_roff.data_ptr(), n,
+                                               d_nodes.data_ptr(), d_err.data_ptr()))
+        torch.cuda.synchronize()
+        assert int(d_err.item()) == 0
+        assert np.array_equal(d_nodes.cpu().numpy().reshape(-1, 20), want)
