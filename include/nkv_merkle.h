@@ -93,10 +93,10 @@ int nkv_ctx_sync(nkv_ctx *ctx);
                                4 / 5 = direct loads in 128 / 256-byte runs per lane */
 #define NKV_OPT_BUCKET 2    /* ragged values (nkv_tree_from_values*, nkv_tree_from_records*):
                                1 = hash in length-sorted order (work queue); 0 = in input
-                               order, fused with the first tree levels; 2 (default) = auto:
-                               input order when the full-block counts of a batch of >= 4096
-                               values lie within max(1, min/16) of each other (one 8-byte
-                               read-back), else sorted */
+                               order; 2 (default) = auto: input order when the full-block
+                               counts of a batch of >= 4096 values lie within max(1, min/16)
+                               of each other, else sorted (decided on the device, no
+                               read-back) */
 #define NKV_OPT_DEEP_PREFETCH 3 /* length-sorted ragged batches: 0 = one block of
                                    lookahead; 1 = several blocks; 2 = several blocks in a
                                    work-queue kernel that spreads the longest chains one
@@ -225,7 +225,7 @@ int nkv_leaf_hash_strided_dev(nkv_ctx *ctx, const void *d_base, uint64_t stride,
                               uint64_t n, void *d_nodes);
 /* levels 1..top of d_nodes from its level 0 */
 int nkv_tree_reduce_dev(nkv_ctx *ctx, void *d_nodes, uint64_t n);
-/* leaf hash fused with the first tree levels, then the rest of the reduce */
+/* leaf hash (order per NKV_OPT_BUCKET), then the tree levels */
 int nkv_tree_from_values_dev(nkv_ctx *ctx, const void *d_base, const uint64_t *d_off,
                              const uint64_t *d_len, uint64_t n, void *d_nodes);
 int nkv_tree_from_strided_dev(nkv_ctx *ctx, const void *d_base, uint64_t stride, uint64_t len,

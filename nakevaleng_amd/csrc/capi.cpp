@@ -260,7 +260,7 @@ int mark(nkv_ctx* c, int which) {
 }
 
 // Order of a ragged batch for the leaf kernel (NKV_OPT_BUCKET): input order
-// (fused tree levels, no sort), length-sorted (work queue), or both kernels
+// (no sort), length-sorted (work queue), or both kernels
 // launched behind a device-side Gate.  Auto mode (2) sorts batches of fewer than
 // 4096 values; for larger ones a narrow range of full-block counts
 // (max <= min + max(1, min / 16), e.g. SSTable records of one size) gains

@@ -1,10 +1,13 @@
 // kernels.hip -- gfx950 kernels of the Merkle step of SSTable build.
 //
 //   K1  k_leaf        NewLeaf over many values (merklenode.go:27-34), one lane
-//                     per leaf, 64 leaves per wavefront; optionally fused with
-//                     the first 8 tree levels of its 256-leaf block (K2a).
-//   K2  k_reduce      build() levels (merkletree.go:31-64): a 256-node slab of
-//                     one level reduced up to 8 levels in LDS per launch.
+//                     per leaf, 64 leaves per wavefront (level 0 only).
+//   K1q k_leaf_queue  the same for ragged, length-sorted batches (work queue).
+//   K1v k_leaf_verify the compaction read: record checksum check + NewLeaf.
+//   K2w k_reduce2     build() levels (merkletree.go:31-64) two at a time at
+//                     full lane use, while a level holds >= 64 Ki nodes.
+//   K2  k_reduce      the rest: a 256-node slab of one level reduced up to 8
+//                     levels in LDS per launch.
 //   K3  k_bfs_image   Serialize() byte image (merkletree.go:67-92,
 //                     merklenode.go:37-63) at closed-form offsets.
 //   K0  k_locate      value offset/length of each serialized core/record
