@@ -28,6 +28,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.
 # Measured compute ceiling of the per-lane SHA-1 (no memory traffic, 8 waves/SIMD,
 # 2.37-2.39 GHz): tools/sha1_rate.hip -> profiles/r01_sha1_compute_rate.txt.
 SHA1_VALU_CEILING_GBS = 4100.0
+# The same ceiling at the shader clock this workload sustains while streaming
+# random bytes from HBM (2.04 GHz against 2.37 GHz from L2/registers, board power
+# limit; tools/pattern_power.hip -> profiles/r01_clock_power.txt).
+STREAMING_CLOCK_RATIO = 2.04 / 2.37
 SEED = 0x6E616B65
 SEED_MIXED = 0x6E616B66
 
@@ -332,6 +336,8 @@ def main():
                 "traffic_bounds": traffic_bounds,  # RDREQ x 64 .. x 128 B (profiles/pmc_traffic.json)
                 "valu_ceiling": SHA1_VALU_CEILING_GBS,
                 "valu_frac": round(achieved / SHA1_VALU_CEILING_GBS, 4),
+                "valu_ceiling_at_streaming_clock": round(SHA1_VALU_CEILING_GBS * STREAMING_CLOCK_RATIO, 1),
+                "valu_frac_at_streaming_clock": round(achieved / (SHA1_VALU_CEILING_GBS * STREAMING_CLOCK_RATIO), 4),
             },
             "kernel_ms": {"leaf_fused": round(leaf_ms, 4), "tree_reduce_rest": round(reduce_ms, 4),
                           "bfs_image": round(bfs_ms, 4)},
