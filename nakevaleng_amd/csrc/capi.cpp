@@ -113,7 +113,7 @@ struct nkv_ctx {
     std::vector<hipEvent_t> ring;
     size_t ring_used = 0;
     DevBuf d_data, d_off, d_len, d_nodes, d_img, d_tmp, d_err, d_aux, d_keys, d_perm, d_stmp, d_queue, d_stats,
-        d_range, d_sync;
+        d_range, d_sync, d_part;
     void* h_stage = nullptr;  // small pinned staging (offsets, lengths, stats)
     unsigned int* h_small = nullptr;  // 64 pinned bytes for device-to-host decisions
     size_t h_cap = 0;
@@ -162,6 +162,13 @@ int grow(DevBuf& b, size_t bytes) {
 }
 
 SyncSlot* sync_slot(nkv_ctx* c, SyncUse u) { return static_cast<SyncSlot*>(c->d_sync.p) + u; }
+
+// scratch for k_locate's per-workgroup partials
+int locate_parts(nkv_ctx* c, uint64_t n, uint32_t** part) {
+    TRY(grow(c->d_part, 4 * locate_part_words(n)));
+    *part = static_cast<uint32_t*>(c->d_part.p);
+    return NKV_OK;
+}
 
 int grow_host(nkv_ctx* c, size_t bytes) {
     if (bytes == 0) bytes = 16;
@@ -420,7 +427,7 @@ void nkv_ctx_destroy(nkv_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (DevBuf* b : {&c->d_data, &c->d_off, &c->d_len, &c->d_nodes, &c->d_img, &c->d_tmp,
                       &c->d_err, &c->d_aux, &c->d_keys, &c->d_perm, &c->d_stmp, &c->d_queue, &c->d_stats,
-                      &c->d_range, &c->d_sync})
+                      &c->d_range, &c->d_sync, &c->d_part})
         if (b->p) (void)hipFree(b->p);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
     if (c->h_small) (void)hipHostFree(c->h_small);
@@ -892,8 +899,10 @@ int nkv_locate_values_dev(nkv_ctx* c, const void* d_stream, uint64_t stream_len,
     if (!d_stream || !d_rec_off || !d_voff || !d_vlen) return NKV_ERR_INVALID;
     TRY(grow(c->d_err, 4));
     unsigned int* err = static_cast<unsigned int*>(c->d_err.p);
+    uint32_t* part = nullptr;
+    TRY(locate_parts(c, n, &part));
     HIPTRY(launch_locate(static_cast<const uint8_t*>(d_stream), stream_len, d_rec_off, n, d_voff,
-                         d_vlen, err, nullptr, sync_slot(c, kSyncLocate), c->stream));
+                         d_vlen, err, nullptr, part, c->stream));
     unsigned int h = 0;
     HIPTRY(hipMemcpyAsync(&h, err, 4, hipMemcpyDeviceToHost, c->stream));
     HIPTRY(hipStreamSynchronize(c->stream));
@@ -918,8 +927,10 @@ int nkv_tree_from_records_dev(nkv_ctx* c, const void* d_stream, uint64_t stream_
     const bool gated = c->bucket == 2 && n >= 4096;
     if (gated) TRY(grow(c->d_range, 8));
     unsigned int* range = gated ? static_cast<unsigned int*>(c->d_range.p) : nullptr;
+    uint32_t* part = nullptr;
+    TRY(locate_parts(c, n, &part));
     HIPTRY(launch_locate(static_cast<const uint8_t*>(d_stream), stream_len, d_rec_off, n, voff, vlen, err, range,
-                         sync_slot(c, kSyncLocate), c->stream));
+                         part, c->stream));
     TRY(tree_from_device_values(c, static_cast<const uint8_t*>(d_stream), voff, vlen, n, false,
                                 static_cast<uint8_t*>(d_nodes), nullptr, range));
     if (d_err) return NKV_OK;
@@ -963,8 +974,9 @@ int nkv_tree_verify_records_dev(nkv_ctx* c, const void* d_stream, uint64_t strea
         const bool gated = c->bucket == 2 && n >= 4096;
         if (gated) TRY(grow(c->d_range, 8));
         unsigned int* range = gated ? static_cast<unsigned int*>(c->d_range.p) : nullptr;
-        HIPTRY(launch_locate(stream, stream_len, d_rec_off, n, voff, vlen, err, range, sync_slot(c, kSyncLocate),
-                             c->stream));
+        uint32_t* part = nullptr;
+        TRY(locate_parts(c, n, &part));
+        HIPTRY(launch_locate(stream, stream_len, d_rec_off, n, voff, vlen, err, range, part, c->stream));
         TRY(plan_of(c, vlen, nullptr, n, &plan, &g, range));
     }
     if (plan != kSorted)

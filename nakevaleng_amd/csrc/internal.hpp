@@ -48,7 +48,7 @@ struct SyncSlot {
     unsigned long long pad;
 };
 constexpr SyncSlot kSyncInit{0u, 0xFFFFFFFFu, 0u, 0u, 0ull, 0ull};
-enum SyncUse { kSyncRange = 0, kSyncLocate = 1, kSyncSplit = 2, kSyncSlots = 4 };
+enum SyncUse { kSyncRange = 0, kSyncSplit = 2, kSyncSlots = 4 };
 
 // BFS image layout in image order (index 0 = top level).
 struct BfsLayout {
@@ -85,10 +85,12 @@ hipError_t launch_bfs_image(const uint8_t* nodes, const BfsLayout& lay, uint8_t*
                             hipStream_t s);
 // err (u32): 1 if any header points outside the stream, else 0; range
 // (nullable, 2 u32): min / max full-block count of the values, as
-// launch_len_range writes it.  Neither needs initialising.
+// launch_len_range writes it.  Neither needs initialising; part: scratch of
+// locate_part_words(n) u32.
+uint64_t locate_part_words(uint64_t n);
 hipError_t launch_locate(const uint8_t* stream, uint64_t stream_len, const uint64_t* rec_off,
                          uint64_t n, uint64_t* voff, uint64_t* vlen, unsigned int* err, unsigned int* range,
-                         SyncSlot* sync, hipStream_t s);
+                         uint32_t* part, hipStream_t s);
 hipError_t scan_exclusive_u64(const uint64_t* in, uint64_t* out, uint64_t n, void* tmp,
                               size_t* tmp_bytes, hipStream_t s);
 // In-place exclusive scan of n u32 (gated); sums: scan_sums_words(n) u32.

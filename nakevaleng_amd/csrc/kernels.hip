@@ -1254,23 +1254,18 @@ __global__ __launch_bounds__(kBlock) void k_bfs_image(const uint8_t* __restrict_
 // @4, Status u8 @12, TypeInfo u8 @13, KeySize u64 @14, ValueSize u64 @22,
 // Key @30, Value @30+KeySize.  rec_off[i] = start of record i.
 
-// Grid-stride over at most kLocateBlocks workgroups: each block folds its
-// range once (same-address atomics serialise, so a block per 256 records would
-// cost more than the locate itself).
-constexpr uint32_t kLocateBlocks = 1024;
-
+// One record per thread; each workgroup leaves its range and error flag in
+// part[3 b .. 3 b + 2] (plain stores: no same-address atomics across 4096
+// blocks), and k_locate_fold combines them in a one-workgroup launch.
 __global__ __launch_bounds__(kBlock) void k_locate(const uint8_t* __restrict__ stream,
                                                     uint64_t stream_len,
                                                     const uint64_t* __restrict__ rec_off, uint64_t n,
                                                     uint64_t* __restrict__ voff,
-                                                    uint64_t* __restrict__ vlen,
-                                                    unsigned int* __restrict__ err, unsigned int* __restrict__ range,
-                                                    SyncSlot* __restrict__ sync) {
+                                                    uint64_t* __restrict__ vlen, uint32_t* __restrict__ part) {
+    const uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
     uint32_t lo = 0xFFFFFFFFu, hi = 0u, bad = 0u;
     unsigned long long none = 0;
-    const uint64_t stride = uint64_t(gridDim.x) * kBlock;
-#pragma unroll 4
-    for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride) {
+    if (i < n) {
         const uint64_t r = rec_off[i];
         uint64_t o = 0, l = 0;
         if (r + 30 <= stream_len) {
@@ -1289,18 +1284,32 @@ __global__ __launch_bounds__(kBlock) void k_locate(const uint8_t* __restrict__ s
         voff[i] = o;
         vlen[i] = l;
         const uint64_t b = l >> 6;
-        const uint32_t bb = b > 0xFFFFFFFFull ? 0xFFFFFFFFu : uint32_t(b);
-        lo = min(lo, bb);
-        hi = max(hi, bb);
+        lo = hi = b > 0xFFFFFFFFull ? 0xFFFFFFFFu : uint32_t(b);
     }
     block_fold(lo, hi, bad, none);
-    uint32_t tot[3];
-    unsigned long long tsum;
-    if (grid_fold(sync, lo, hi, bad, 0ull, tot, &tsum) && threadIdx.x == 0) {
-        *err = tot[2];
+    if (threadIdx.x == 0) {
+        part[3 * blockIdx.x] = lo;
+        part[3 * blockIdx.x + 1] = hi;
+        part[3 * blockIdx.x + 2] = bad;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_locate_fold(const uint32_t* __restrict__ part, uint32_t nb,
+                                                         unsigned int* __restrict__ err,
+                                                         unsigned int* __restrict__ range) {
+    uint32_t lo = 0xFFFFFFFFu, hi = 0u, bad = 0u;
+    unsigned long long none = 0;
+    for (uint32_t b = threadIdx.x; b < nb; b += kBlock) {
+        lo = min(lo, part[3 * b]);
+        hi = max(hi, part[3 * b + 1]);
+        bad |= part[3 * b + 2];
+    }
+    block_fold(lo, hi, bad, none);
+    if (threadIdx.x == 0) {
+        *err = bad;
         if (range) {
-            range[0] = tot[0];
-            range[1] = tot[1];
+            range[0] = lo;
+            range[1] = hi;
         }
     }
 }
@@ -1507,11 +1516,14 @@ hipError_t launch_bfs_image(const uint8_t* nodes, const BfsLayout& lay, uint8_t*
     return hipGetLastError();
 }
 
+uint64_t locate_part_words(uint64_t n) { return 3 * uint64_t(grid_for(n)); }
+
 hipError_t launch_locate(const uint8_t* stream, uint64_t stream_len, const uint64_t* rec_off,
                          uint64_t n, uint64_t* voff, uint64_t* vlen, unsigned int* err, unsigned int* range,
-                         SyncSlot* sync, hipStream_t s) {
-    hipLaunchKernelGGL(k_locate, dim3(std::min(grid_for(n), kLocateBlocks)), dim3(kBlock), 0, s, stream,
-                       stream_len, rec_off, n, voff, vlen, err, range, sync);
+                         uint32_t* part, hipStream_t s) {
+    const unsigned nb = grid_for(n);
+    hipLaunchKernelGGL(k_locate, dim3(nb), dim3(kBlock), 0, s, stream, stream_len, rec_off, n, voff, vlen, part);
+    hipLaunchKernelGGL(k_locate_fold, dim3(1), dim3(kBlock), 0, s, part, nb, err, range);
     return hipGetLastError();
 }
 
