@@ -108,8 +108,9 @@ struct nkv_ctx {
     int crc_load = 1;       // NKV_OPT_CRC_LOAD
     bool timing = false;
     bool timed = false;
-    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
-    // per-call event triples (leaf start, leaf end / reduce start, reduce end)
+    // per-call event triples (leaf start, leaf end / reduce start, reduce end),
+    // the latest kTimingRing / 3 calls
+    static constexpr size_t kTimingRing = 3 * 65536;
     std::vector<hipEvent_t> ring;
     size_t ring_used = 0;
     DevBuf d_data, d_off, d_len, d_nodes, d_img, d_tmp, d_err, d_aux, d_keys, d_perm, d_stmp, d_queue, d_stats,
@@ -250,18 +251,19 @@ int finish_tree(nkv_ctx* c, uint8_t* nodes, uint64_t n, uint8_t* root20, uint8_t
 int mark(nkv_ctx* c, int which) {
     if (!c->timing) return NKV_OK;
     if (which == 0) {
+        if (c->ring_used + 3 > nkv_ctx::kTimingRing) c->ring_used = 0;  // restart the window
         if (c->ring_used + 3 > c->ring.size()) {
             for (int i = 0; i < 3; ++i) {
                 hipEvent_t e;
-                HIPTRY(hipEventCreate(&e));
+                HIPTRY(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));  // timing only: no cache writeback per record
                 c->ring.push_back(e);
             }
         }
         c->ring_used += 3;
     }
-    hipEvent_t e = c->ring[c->ring_used - 3 + which];
-    HIPTRY(hipEventRecord(e, c->stream));
-    HIPTRY(hipEventRecord(c->ev[which], c->stream));
+    // one event per mark: each record is a timestamp packet on the stream
+    // (a few us of GPU time), so the timed loop carries three per tree
+    HIPTRY(hipEventRecord(c->ring[c->ring_used - 3 + which], c->stream));
     if (which == 2) c->timed = true;
     return NKV_OK;
 }
@@ -402,7 +404,6 @@ int nkv_ctx_create(int device, nkv_ctx** out) {
     int rc = st(hipSetDevice(device));
     if (rc == NKV_OK) rc = st(hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking));
     if (rc == NKV_OK) rc = st(hipHostMalloc(reinterpret_cast<void**>(&c->h_small), 64, hipHostMallocDefault));
-    for (int i = 0; i < 3 && rc == NKV_OK; ++i) rc = st(hipEventCreate(&c->ev[i]));
     if (rc == NKV_OK) rc = grow(c->d_sync, sizeof(SyncSlot) * kSyncSlots);
     if (rc == NKV_OK) {  // the grid-fold accumulators start (and every launch leaves them) at kSyncInit
         SyncSlot init[kSyncSlots];
@@ -431,8 +432,6 @@ void nkv_ctx_destroy(nkv_ctx* c) {
         if (b->p) (void)hipFree(b->p);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
     if (c->h_small) (void)hipHostFree(c->h_small);
-    for (hipEvent_t e : c->ev)
-        if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->ring) (void)hipEventDestroy(e);
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;
@@ -534,10 +533,11 @@ int nkv_ctx_timing_summary(nkv_ctx* c, int* calls, float* leaf_ms_total, float* 
 int nkv_ctx_last_timing(nkv_ctx* c, float* leaf_ms, float* reduce_ms) {
     TRY(bind(c));
     if (!c->timed) return NKV_ERR_INVALID;
-    HIPTRY(hipEventSynchronize(c->ev[2]));
+    hipEvent_t* ev = &c->ring[c->ring_used - 3];
+    HIPTRY(hipEventSynchronize(ev[2]));
     float a = 0.f, b = 0.f;
-    HIPTRY(hipEventElapsedTime(&a, c->ev[0], c->ev[1]));
-    HIPTRY(hipEventElapsedTime(&b, c->ev[1], c->ev[2]));
+    HIPTRY(hipEventElapsedTime(&a, ev[0], ev[1]));
+    HIPTRY(hipEventElapsedTime(&b, ev[1], ev[2]));
     if (leaf_ms) *leaf_ms = a;
     if (reduce_ms) *reduce_ms = b;
     return NKV_OK;
