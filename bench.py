@@ -60,7 +60,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", choices=["sstable4k", "mixed", "records", "records_verify"], default="sstable4k",
+    ap.add_argument("--config", choices=["sstable4k", "mixed", "records", "records_verify", "one_tree"],
+                    default="sstable4k",
                     help="sstable4k = BASELINE configs[1] (the metric); mixed = configs[2]; records = the "
                          "compaction form: 1 Mi serialized 4 KiB records in a Data table, values located "
                          "from the record headers and hashed in place; records_verify = the same plus every "
@@ -167,6 +168,7 @@ def main():
         ctx.set_option(_lib.NKV_OPT_BUCKET, args.bucket)
     roots = torch.empty(world * 20, dtype=torch.uint8, device="cuda")
     mixed = args.config == "mixed"
+    one_tree = args.config == "one_tree"
     records = args.config in ("records", "records_verify")
     verify_crc = args.config == "records_verify"
     if records:
@@ -207,6 +209,15 @@ def main():
 
         def tree():
             _lib.check(L.nkv_tree_from_strided_dev(ctx.h, data.data_ptr(), vlen, vlen, n, nodes.data_ptr()))
+
+        if one_tree:  # one tree over every rank's leaves (rank r holds leaves [r n, (r+1) n))
+            from nakevaleng_amd import sharded_tree
+            if n & (n - 1):
+                raise SystemExit("--config one_tree needs a power-of-two --leaves (ranges aligned to 2^k)")
+            ops = sharded_tree.DeviceOps(dev, ctx=ctx)
+
+            def tree():
+                nodes[-20:] = sharded_tree.sharded_root((data, vlen, vlen), n * world, ops=ops, host_root=False)
     else:
         import numpy as np
         lens_h, off_h = mixed_lengths(args.mixed_bytes, SEED_MIXED + rank)
@@ -224,7 +235,7 @@ def main():
 
     def step():
         tree()
-        if world > 1:  # C1: gather the per-table roots
+        if world > 1 and not one_tree:  # C1: gather the per-table roots
             dist.all_gather_into_tensor(roots, nodes[-20:])
 
     for _ in range(args.warmup):
@@ -272,6 +283,7 @@ def main():
 
     verified = None
     if args.verify and rank == 0:
+        import numpy as np
         from oracle import oracle_c as oc
         if mixed:
             host = oc.splitmix64_bytes(nbytes, SEED_MIXED)
@@ -284,8 +296,8 @@ def main():
             if verify_crc:
                 assert d_stats.cpu().tolist() == [0, -1, 0], d_stats.cpu().tolist()
         else:
-            host = oc.splitmix64_bytes(nbytes, SEED)
-            want = oc.tree_from_digests(oc.leaf_hashes_strided(host, vlen, vlen, n, threads=16))
+            host = np.concatenate([oc.splitmix64_bytes(nbytes, SEED + r) for r in range(world if one_tree else 1)])
+            want = oc.tree_from_digests(oc.leaf_hashes_strided(host, vlen, vlen, len(host) // vlen, threads=16))
         verified = want[-1].tobytes().hex() == root
         del host
 
@@ -325,11 +337,16 @@ def main():
                              "Data table in HBM; values located from the headers and hashed in place, full tree"
                              + ("; every record's Crc (Key ++ Value) checked in the same pass" if verify_crc else ""))
                             if records else
+                            (f"one tree over {world} GPU(s): {n} x {vlen} B values per rank, each rank builds the "
+                             "levels of its aligned leaf range, sub-roots all-gathered, top levels on every rank")
+                            if one_tree else
                             "BASELINE configs[1]: single SSTable flush, 1 Mi x 4 KiB values, "
                             "leaf SHA-1 + full tree reduce (one table per GPU; roots all-gathered over RCCL when N>1)",
                 "leaves_per_gpu": n,
                 "value_bytes": vlen if not mixed else "64..65536 (mean %.0f)" % (nbytes / n),
-                "parallelism": f"{world} independent tables" + (" + RCCL all_gather of roots" if world > 1 else ""),
+                "parallelism": (f"1 tree split over {world} ranks" + (" + RCCL all_gather of sub-roots" if world > 1 else ""))
+                               if one_tree else
+                               f"{world} independent tables" + (" + RCCL all_gather of roots" if world > 1 else ""),
             },
             "roofline": {
                 "bound": "hbm",

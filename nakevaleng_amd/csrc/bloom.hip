@@ -103,7 +103,7 @@ __global__ __launch_bounds__(kBloomBlock) void k_bloom(const uint8_t* __restrict
         L = len[i];
     } else {
         const uint64_t r = off[i];
-        if (r + 30 > stream_len) {
+        if (!header_in(r, stream_len)) {
             atomicOr(err, 1u);
             return;
         }
@@ -156,7 +156,7 @@ __device__ __forceinline__ bool bloom_key(const uint8_t* base, const uint64_t* o
         return true;
     }
     const uint64_t r = off[i];
-    if (r + 30 > stream_len) return false;
+    if (!header_in(r, stream_len)) return false;
     const uint64_t l = bl_ld_le64(base + r + 14);
     if (l > stream_len - r - 30) return false;
     *key = base + r + 30;

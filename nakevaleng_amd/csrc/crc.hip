@@ -181,7 +181,7 @@ __global__ __launch_bounds__(B) void k_crc(const uint8_t* __restrict__ base, con
     if (live) {
         if (RECORDS) {
             const uint64_t r = off[i];
-            if (r + 30 <= stream_len) {
+            if (header_in(r, stream_len)) {
                 const uint64_t ks = crc_ld_le64(base + r + 14);
                 const uint64_t vs = crc_ld_le64(base + r + 22);
                 if (ks <= stream_len && vs <= stream_len && r + 30 + ks + vs <= stream_len) {
@@ -361,7 +361,7 @@ __global__ __launch_bounds__(WG) void k_crc_group(const uint8_t* __restrict__ ba
         if (live) {
             if (RECORDS) {
                 const uint64_t r = off[i];
-                if (r + 30 <= stream_len) {
+                if (header_in(r, stream_len)) {
                     const uint64_t ks = crc_ld_le64(base + r + 14);
                     const uint64_t vs = crc_ld_le64(base + r + 22);
                     if (ks <= stream_len && vs <= stream_len && r + 30 + ks + vs <= stream_len) {

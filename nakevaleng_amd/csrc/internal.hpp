@@ -23,6 +23,10 @@ constexpr int kLeafWavesPerSimd = NKV_LEAF_WAVES;  // 8 waves/SIMD <=> <= 64 VGP
 // read-back): range = the batch's (min, max) full-block counts from
 // launch_len_range; pol 1 runs the kernel only for a narrow range (input
 // order), pol 2 only for a wide one (length-sorted work queue), 0 always.
+// A record header [r, r + 30) (record.go:191-199) lies inside a stream of len
+// bytes; written so that a wild offset near 2^64 cannot wrap past the check.
+__host__ __device__ inline bool header_in(uint64_t r, uint64_t len) { return r <= len && len - r >= 30; }
+
 struct Gate {
     const unsigned int* range = nullptr;
     int pol = 0;

@@ -919,7 +919,7 @@ __global__ __launch_bounds__(kBlock, kLeafWavesPerSimd) void k_leaf_verify(
     bool hdr_bad = false;
     if (live) {
         const uint64_t r = rec_off[t];
-        if (r + 30 <= stream_len) {
+        if (header_in(r, stream_len)) {
             const uint64_t k = ld_le64(stream + r + 14), v = ld_le64(stream + r + 22);
             if (k <= stream_len && v <= stream_len && r + 30 + k + v <= stream_len) {
                 key = stream + r + 30;
@@ -1268,7 +1268,7 @@ __global__ __launch_bounds__(kBlock) void k_locate(const uint8_t* __restrict__ s
     if (i < n) {
         const uint64_t r = rec_off[i];
         uint64_t o = 0, l = 0;
-        if (r + 30 <= stream_len) {
+        if (header_in(r, stream_len)) {
             const uint64_t ks = ld_le64(stream + r + 14);
             const uint64_t vs = ld_le64(stream + r + 22);
             o = r + 30 + ks;

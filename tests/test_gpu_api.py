@@ -251,3 +251,48 @@ def test_tree_from_records_dev_uniform_gated(nkv, oracle, n):
         torch.cuda.synchronize()
         assert int(d_err.item()) == 0
         assert np.array_equal(d_nodes.cpu().numpy().reshape(-1, 20), want)
+
+
+@pytest.mark.parametrize("n", [300, 5000])
+def test_record_paths_wild_offsets(nkv, n):
+    """Record offsets far outside the stream (near 2^64, where offset + 30
+    wraps) are reported as bad headers by every device record path, and no
+    kernel reads through them."""
+    import torch
+    _lib, ctx = nkv
+    L = _lib.lib()
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    rb, ks = 256, 16
+    n_ = n
+    body = np.zeros((n_, rb), np.uint8)
+    body[:, 14:22] = np.frombuffer(np.uint64(ks).tobytes(), np.uint8)
+    body[:, 22:30] = np.frombuffer(np.uint64(rb - 30 - ks).tobytes(), np.uint8)
+    slen = n_ * rb
+    roff = np.arange(n_, dtype=np.uint64) * rb
+    for i, w in ((1, 2**64 - 8), (n_ // 2, 2**64 - 29), (n_ - 2, slen - 29), (n_ - 1, slen)):
+        roff[i] = w
+    d_stream = torch.from_numpy(body.reshape(-1)).cuda()
+    d_roff = torch.from_numpy(roff.view(np.int64)).cuda()
+    d_nodes = torch.zeros(L.nkv_total_nodes(n_) * 20, dtype=torch.uint8, device="cuda")
+    d_err = torch.zeros(1, dtype=torch.int32, device="cuda")
+    _lib.check(L.nkv_tree_from_records_dev(ctx.h, d_stream.data_ptr(), slen, d_roff.data_ptr(), n_,
+                                           d_nodes.data_ptr(), d_err.data_ptr()))
+    d_stats = torch.zeros(3, dtype=torch.int64, device="cuda")
+    _lib.check(L.nkv_record_crc_dev(ctx.h, d_stream.data_ptr(), slen, d_roff.data_ptr(), n_, None,
+                                    d_stats.data_ptr()))
+    torch.cuda.synchronize()
+    assert int(d_err.item()) == 1
+    assert int(d_stats[2].item()) == 1
+    d_stats.zero_()
+    _lib.check(L.nkv_tree_verify_records_dev(ctx.h, d_stream.data_ptr(), slen, d_roff.data_ptr(), n_,
+                                             d_nodes.data_ptr(), None, d_stats.data_ptr()))
+    torch.cuda.synchronize()
+    assert int(d_stats[2].item()) == 1
+    d_bits = torch.zeros(4 * 1024, dtype=torch.uint8, device="cuda")
+    assert L.nkv_bloom_insert_records_dev(ctx.h, d_stream.data_ptr(), slen, d_roff.data_ptr(), n_, 32768, 3, 1,
+                                          d_bits.data_ptr()) == _lib.NKV_ERR_INVALID
+    d_voff = torch.empty(n_, dtype=torch.int64, device="cuda")
+    d_vlen = torch.empty(n_, dtype=torch.int64, device="cuda")
+    assert L.nkv_locate_values_dev(ctx.h, d_stream.data_ptr(), slen, d_roff.data_ptr(), n_, d_voff.data_ptr(),
+                                   d_vlen.data_ptr()) == _lib.NKV_ERR_INVALID
+    torch.cuda.synchronize()
