@@ -340,8 +340,12 @@ def main():
                             (f"one tree over {world} GPU(s): {n} x {vlen} B values per rank, each rank builds the "
                              "levels of its aligned leaf range, sub-roots all-gathered, top levels on every rank")
                             if one_tree else
-                            "BASELINE configs[1]: single SSTable flush, 1 Mi x 4 KiB values, "
-                            "leaf SHA-1 + full tree reduce (one table per GPU; roots all-gathered over RCCL when N>1)",
+                            ("BASELINE configs[1]: single SSTable flush, 1 Mi x 4 KiB values, "
+                             if (n, vlen) == (1 << 20, 4096) else
+                             "BASELINE configs[4] per-GPU table (8 Mi x 4 KiB values), "
+                             if (n, vlen) == (8 << 20, 4096) else
+                             f"single SSTable flush, {n} x {vlen} B values, ")
+                            + "leaf SHA-1 + full tree reduce (one table per GPU; roots all-gathered over RCCL when N>1)",
                 "leaves_per_gpu": n,
                 "value_bytes": vlen if not mixed else "64..65536 (mean %.0f)" % (nbytes / n),
                 "parallelism": (f"1 tree split over {world} ranks" + (" + RCCL all_gather of sub-roots" if world > 1 else ""))
