@@ -90,7 +90,10 @@ int nkv_ctx_sync(nkv_ctx *ctx);
 /* Tuning knobs (defaults are the measured-best settings). */
 #define NKV_OPT_LEAF_LOAD 1 /* leaf-kernel load path for 16-byte aligned values:
                                1 = LDS-DMA stage, 2 = direct loads, 3 = direct non-temporal,
-                               4 / 5 = direct loads in 128 / 256-byte runs per lane */
+                               4 / 5 = direct loads in 128 / 256-byte runs per lane,
+                               9 / 10 = line-pair / 80-byte-window LDS-DMA stage for values
+                               that are not 64-byte aligned (waves of equal full-block
+                               counts; other waves as 1) */
 #define NKV_OPT_BUCKET 2    /* ragged values (nkv_tree_from_values*, nkv_tree_from_records*):
                                1 = hash in length-sorted order (work queue); 0 = in input
                                order; 2 (default) = auto: input order when the full-block

@@ -769,6 +769,93 @@ __device__ __forceinline__ void sha1_blocks_ring_vc(uint8_t* wbuf, const uint8_t
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// LOAD 9: line-pair stage for values that are not 64-byte aligned (records in a
+// Data table: the Value starts 30 + KeySize bytes into its record).  Block b of
+// a value is bytes [o + 64 b, o + 64 b + 64) of its aligned line pair
+// [A + 64 b, A + 64 b + 128), A = p & ~63, o = p & 63.  Eight LDS-DMA
+// instructions per block move the pairs of all 64 values: instruction k
+// serves values 8k .. 8k+7, lane l quad (l & 7) of value 8k + (l >> 3), so
+// value j's pair lands contiguously at wbuf + 128 j and the lane reads its
+// window with four byte-unaligned ds_read_b128 (no register funnel).  Every
+// DMA source is 16-byte aligned and inside a line that holds bytes of the
+// value's block (quads past o + 63 are clamped to the last needed one), so no
+// request straddles two lines.  The addresses are one 32-bit offset per role
+// from a wave-uniform base plus the uniform 64 b; this needs every live value
+// of the wave to have the same full-block count and the wave's pairs to lie
+// within 4 GiB of the base.  Otherwise it returns false and does nothing (the
+// caller runs the LOAD 8 stream).  Stage: 8 KiB per wave.
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t u = uint64_t(__shfl_xor(static_cast<long long>(v), o));
+        v = u < v ? u : v;
+    }
+    const uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(v));
+    const uint32_t hi = __builtin_amdgcn_readfirstlane(uint32_t(v >> 32));
+    return (uint64_t(hi) << 32) | lo;
+}
+
+// kWindow (LOAD 10): the same stream with only each value's 80-byte window row
+// (five aligned quads from (o & ~15), clamped like the pair's), so a wave's
+// stage is 5 KiB, five DMA instructions move a block (quad g = 64 k + l of
+// instruction k is quad g % 5 of value g / 5), and eight waves per SIMD fit
+// the 160 KiB LDS (eight 20 KiB workgroups per CU).
+// kWindow is a literal at every call site (the function is inlined and folded).
+__device__ __forceinline__ bool sha1_blocks_pair(const bool kWindow, uint8_t* wbuf, const uint8_t* p, bool live, uint32_t my_nfull,
+                                                 uint32_t h[5]) {
+    const int kDma = kWindow ? 5 : 8;          // DMA instructions per block
+    const uint32_t kRow = kWindow ? 80u : 128u;
+    const int lane = threadIdx.x & 63;
+    const uint32_t nmax = wave_max_u32(live ? my_nfull : 0u);
+    if (nmax == 0) return true;  // no live value has a full block
+    if (!__all(!live || my_nfull == nmax)) return false;
+    const uint64_t a = reinterpret_cast<uintptr_t>(p) & ~uint64_t(63);
+    const uint64_t wb = wave_min_u64(live ? a : ~uint64_t(0));
+    const uint64_t rel = live ? a - wb : 0u;
+    if (!__all(rel + 64ull * (uint64_t(nmax) + 1ull) <= 0xFFFFFFFFull)) return false;
+    const uint32_t o = live ? uint32_t(reinterpret_cast<uintptr_t>(p) & 63u) : 0u;
+    const uint8_t* base = reinterpret_cast<const uint8_t*>(wb);
+    // lane 0 is live whenever any lane is (dead lanes are the grid's tail), so
+    // dead values' roles re-read lane 0's quads into their unused rows
+    uint32_t voff[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        if (k >= kDma) break;
+        const uint32_t g = 64u * uint32_t(k) + uint32_t(lane);
+        const int j = kWindow ? int(g / 5u) : 8 * k + (lane >> 3);
+        const uint32_t qi = kWindow ? g - 5u * uint32_t(j) : uint32_t(lane) & 7u;
+        const bool lj = __shfl(int(live), j) != 0;
+        const uint32_t src = lj ? uint32_t(j) : 0u;
+        const uint32_t rj = uint32_t(__shfl(int(uint32_t(rel)), int(src)));
+        const uint32_t oj = uint32_t(__shfl(int(o), int(src)));
+        const uint32_t qlast = (oj + 63u) >> 4;
+        voff[k] = rj + 16u * min((kWindow ? (oj >> 4) : 0u) + qi, qlast);
+    }
+    auto issue = [&](uint32_t b) {
+        const uint32_t cb = 64u * b;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if (k < kDma) __builtin_amdgcn_global_load_lds(base + (voff[k] + cb), wbuf + 1024 * k, 16, 0, 0);
+    };
+    const uint32_t rd = uint32_t(reinterpret_cast<uintptr_t>(wbuf)) + kRow * uint32_t(lane) + (kWindow ? (o & 15u) : o);
+    issue(0u);
+    for (uint32_t b = 0; b < nmax; ++b) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        u32x4 v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = ds_read_b128_asm(rd + 16u * uint32_t(q));
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]) : : "memory");
+        if (b + 1 < nmax) issue(b + 1);
+        uint4 c4[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) c4[q] = make_uint4(v[q].x, v[q].y, v[q].z, v[q].w);
+        uint32_t w[16];
+        be16_from_raw(c4, w);
+        if (live) sha1_compress(h, w);
+    }
+    return true;
+}
+
 // MODE 0: value i at base + i*stride, length L.  MODE 1: base + off[i], len[i].
 // perm (MODE 1 only, nullable): lane i hashes leaf perm[i] (length bucketing).
 // No tree level is fused here: a wave-level step costs a whole SHA-1
@@ -779,13 +866,13 @@ __device__ __forceinline__ void sha1_blocks_ring_vc(uint8_t* wbuf, const uint8_t
 // LOAD: 0 = any alignment (register funnel); 1 = 16-byte aligned, LDS-DMA
 // stage; 2 = aligned, direct loads; 3 = aligned, direct non-temporal loads.
 template <int MODE, int LOAD>
-__global__ __launch_bounds__(kBlock, (LOAD == 6 || LOAD == 7) ? 2 : ((LOAD == 4 || LOAD == 5) ? 4 : kLeafWavesPerSimd)) void k_leaf(const uint8_t* __restrict__ base,
+__global__ __launch_bounds__(kBlock, (LOAD == 6 || LOAD == 7) ? 2 : ((LOAD == 4 || LOAD == 5) ? 4 : (LOAD == 9 ? 5 : kLeafWavesPerSimd))) void k_leaf(const uint8_t* __restrict__ base,
                                                   const uint64_t* __restrict__ off,
                                                   const uint64_t* __restrict__ len, uint64_t stride,
                                                   uint64_t L, const uint32_t* __restrict__ perm,
                                                   uint64_t n, uint8_t* __restrict__ nodes, Gate gate) {
-    // 16 KiB: four wave-private 4 KiB LDS-DMA stages (LOAD == 1)
-    __shared__ __attribute__((aligned(16))) uint8_t smem[kBlock * 64];
+    // 16 KiB: four wave-private 4 KiB LDS-DMA stages (LOAD 1, 8); 8 KiB each for LOAD 9, 5 KiB for LOAD 10
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kBlock * (LOAD == 9 ? 128 : (LOAD == 10 ? 80 : 64))];
     if (!gate.open()) return;
     NKV_STAMP(0);
     const uint64_t g = blockIdx.x;
@@ -818,18 +905,22 @@ __global__ __launch_bounds__(kBlock, (LOAD == 6 || LOAD == 7) ? 2 : ((LOAD == 4 
             else sha1_tail<true>(p, ln, h);
             store_digest(nodes, leaf, h);
         }
-    } else if (LOAD == 1 || LOAD == 8) {
+    } else if (LOAD == 1 || LOAD == 8 || LOAD == 9 || LOAD == 10) {
         // wave-cooperative LDS-DMA stream of the full blocks, then the tail.
         // The DMA reads each value's own blocks at the value's address, so it
         // serves any alignment (LOAD 8: unaligned values, unaligned tail); only
         // full blocks are fetched, so every byte read belongs to the value.
         const int lane = threadIdx.x & 63;
         const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-        uint8_t* wbuf = smem + 4096 * wave;
+        uint8_t* wbuf = smem + (LOAD == 9 ? 8192 : (LOAD == 10 ? 5120 : 4096)) * wave;
         const uint32_t q = (uint32_t(lane) & 3u) ^ ((uint32_t(lane) >> 4) & 3u);
         const uint32_t my_nfull = live ? uint32_t(ln >> 6) : 0u;
         sha1_init(h);
-        if (MODE == 0) {
+        bool staged = false;
+        if constexpr (LOAD == 9 || LOAD == 10) staged = sha1_blocks_pair(LOAD == 10, wbuf, p, live, my_nfull, h);
+        if (staged) {
+            // line-pair stage done (wave-uniform)
+        } else if (MODE == 0) {
             // value j of this wave at wave_base + j * stride (32-bit offsets:
             // saddr-form DMA, one VGPR of addressing)
             const uint64_t first = g * kBlock + 64 * uint64_t(wave);
@@ -1393,6 +1484,8 @@ static void leaf_dispatch(int load, const uint8_t* base, const uint64_t* off, co
         case 6: leaf_kernel<MODE, 6>(base, off, len, stride, L, perm, n, nodes, s, g); break;
         case 7: leaf_kernel<MODE, 7>(base, off, len, stride, L, perm, n, nodes, s, g); break;
         case 8: leaf_kernel<MODE, 8>(base, off, len, stride, L, perm, n, nodes, s, g); break;
+        case 9: leaf_kernel<MODE, 9>(base, off, len, stride, L, perm, n, nodes, s, g); break;
+        case 10: leaf_kernel<MODE, 10>(base, off, len, stride, L, perm, n, nodes, s, g); break;
         default: leaf_kernel<MODE, 0>(base, off, len, stride, L, perm, n, nodes, s, g); break;
     }
 }
@@ -1400,7 +1493,9 @@ static void leaf_dispatch(int load, const uint8_t* base, const uint64_t* off, co
 hipError_t launch_leaf_strided(const uint8_t* base, uint64_t stride, uint64_t L, uint64_t n, int load,
                                uint8_t* nodes, hipStream_t s) {
     const bool al = ((reinterpret_cast<uintptr_t>(base) | stride) & 15) == 0;
-    if (!al) load = load == 1 ? 8 : 0;  // LDS-DMA serves any alignment; direct loads need 16 B
+    // LDS-DMA serves any alignment (direct loads need 16 B); the 80-byte window
+    // stage (LOAD 10) by default, the value-relative stream in its ragged waves
+    if (!al && load != 9 && load != 10) load = load == 1 ? 10 : 0;
     leaf_dispatch<0>(load, base, nullptr, nullptr, stride, L, nullptr, n, nodes, s, Gate{});
     return hipGetLastError();
 }
@@ -1409,7 +1504,7 @@ hipError_t launch_leaf_offsets(const uint8_t* base, const uint64_t* off, const u
                                const uint32_t* perm, uint64_t n, bool aligned, int load, uint8_t* nodes,
                                hipStream_t s, bool deep, Gate gate) {
     if (perm && deep) load = aligned ? 6 : 7;  // ragged, length-sorted: deep prefetch
-    else if (!aligned) load = load == 1 ? 8 : 0;  // LDS-DMA serves any alignment
+    else if (!aligned && load != 9 && load != 10) load = load == 1 ? 10 : 0;  // as launch_leaf_strided
     leaf_dispatch<1>(load, base, off, len, 0, 0, perm, n, nodes, s, gate);
     return hipGetLastError();
 }

@@ -391,3 +391,67 @@ def test_bucket_modes_narrow_and_wide(nkv, oracle, bucket, spread):
         ctx.close()
     want = oracle.tree_from_digests(oracle.leaf_hashes(data, off, lens, threads=8))
     assert np.array_equal(d_nodes.cpu().numpy().reshape(-1, 20), want)
+
+
+@pytest.mark.parametrize("load", [9, 10])
+@pytest.mark.parametrize("shift", [0, 1, 2, 15, 16, 17, 46, 48, 63])
+@pytest.mark.parametrize("n,vlen,rec", [(1, 4050, 4096), (63, 4050, 4096), (3001, 4050, 4096), (777, 327, 400),
+                                        (300, 63, 128), (257, 64, 130), (130, 1024, 1100)])
+def test_line_pair_stage_uniform(nkv, oracle, load, shift, n, vlen, rec):
+    """NKV_OPT_LEAF_LOAD 9 / 10 (line-pair / 80-byte-window LDS-DMA stage, byte-unaligned LDS reads): records-like values at
+    every sub-line offset, through the offsets path and the strided path, dead lanes in the last wave."""
+    torch = _torch()
+    _lib, ctx = nkv
+    _bind(torch, ctx)
+    L = _lib.lib()
+    nbytes = shift + rec * n + 64
+    data = oracle.splitmix64_bytes(nbytes, SEED + shift)
+    off = (np.arange(n, dtype=np.uint64) * rec + shift).astype(np.uint64)
+    lens = np.full(n, vlen, np.uint64)
+    want = oracle.tree_from_digests(oracle.leaf_hashes(data, off, lens, threads=8))
+    d_data, d_off, d_len = _dev(torch, data), _dev(torch, off), _dev(torch, lens)
+    d_nodes = torch.zeros(L.nkv_total_nodes(n) * 20, dtype=torch.uint8, device="cuda")
+    d_nodes2 = torch.zeros_like(d_nodes)
+    ctx.set_option(_lib.NKV_OPT_LEAF_LOAD, load)
+    try:
+        _lib.check(L.nkv_tree_from_values_dev(ctx.h, d_data.data_ptr(), d_off.data_ptr(), d_len.data_ptr(),
+                                              n, d_nodes.data_ptr()))
+        _lib.check(L.nkv_tree_from_strided_dev(ctx.h, d_data.data_ptr() + shift, rec, vlen, n,
+                                               d_nodes2.data_ptr()))
+        torch.cuda.synchronize()
+    finally:
+        ctx.set_option(_lib.NKV_OPT_LEAF_LOAD, 1)
+    assert np.array_equal(d_nodes.cpu().numpy().reshape(-1, 20), want)
+    assert np.array_equal(d_nodes2.cpu().numpy().reshape(-1, 20), want)
+
+
+@pytest.mark.parametrize("load", [9, 10])
+@pytest.mark.parametrize("spread", [1, 64, 3000])
+def test_line_pair_stage_ragged_falls_back(nkv, oracle, load, spread):
+    """LOAD 9 in input order over values whose full-block counts differ inside a wave: those waves take
+    the value-relative stream, equal-count waves the line-pair stage; every digest matches."""
+    torch = _torch()
+    _lib, ctx = nkv
+    _bind(torch, ctx)
+    L = _lib.lib()
+    rng = np.random.default_rng(spread)
+    n = 4500
+    lens = (4000 + rng.integers(0, spread, n)).astype(np.uint64)
+    lens[:640] = 4050  # the first ten waves have equal counts
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum(lens[:-1] + 46)
+    off += 46
+    data = oracle.splitmix64_bytes(int(off[-1] + lens[-1]) + 64, SEED)
+    want = oracle.tree_from_digests(oracle.leaf_hashes(data, off, lens, threads=8))
+    d_data, d_off, d_len = _dev(torch, data), _dev(torch, off), _dev(torch, lens)
+    d_nodes = torch.zeros(L.nkv_total_nodes(n) * 20, dtype=torch.uint8, device="cuda")
+    ctx.set_option(_lib.NKV_OPT_LEAF_LOAD, load)
+    ctx.set_option(_lib.NKV_OPT_BUCKET, 0)
+    try:
+        _lib.check(L.nkv_tree_from_values_dev(ctx.h, d_data.data_ptr(), d_off.data_ptr(), d_len.data_ptr(),
+                                              n, d_nodes.data_ptr()))
+        torch.cuda.synchronize()
+    finally:
+        ctx.set_option(_lib.NKV_OPT_LEAF_LOAD, 1)
+        ctx.set_option(_lib.NKV_OPT_BUCKET, 2)
+    assert np.array_equal(d_nodes.cpu().numpy().reshape(-1, 20), want)
