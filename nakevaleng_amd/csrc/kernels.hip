@@ -53,6 +53,22 @@ __device__ __forceinline__ uint64_t ld_le64(const uint8_t* p) {
     return v;
 }
 
+// KeySize and ValueSize (header bytes 14..29, record.go:191-199) of the
+// record at p, from two or three aligned 8-byte loads and a funnel shift
+// instead of sixteen byte loads (one line request per lane per load rather
+// than one per byte).  The third load is issued only when the fields are
+// not 8-byte aligned; it then holds byte 29, so every load stays inside an
+// aligned word that holds a header byte (no page can be crossed).
+__device__ __forceinline__ void ld_header_sizes(const uint8_t* p, uint64_t& ks, uint64_t& vs) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p + 14);
+    const uint64_t* q = reinterpret_cast<const uint64_t*>(a & ~uintptr_t(7));
+    const uint32_t sh = uint32_t(a & 7u) * 8u;
+    const uint64_t q0 = q[0], q1 = q[1];
+    const uint64_t q2 = sh ? q[2] : 0ull;
+    ks = sh ? (q0 >> sh) | (q1 << (64u - sh)) : q0;
+    vs = sh ? (q1 >> sh) | (q2 << (64u - sh)) : q1;
+}
+
 // ---------------------------------------------------------------------------
 // Block and grid folds (SyncSlot, internal.hpp).  block_fold leaves the
 // workgroup's min / max / or / sum in thread 0.  grid_fold then folds them
@@ -1360,8 +1376,8 @@ __global__ __launch_bounds__(kBlock) void k_locate(const uint8_t* __restrict__ s
         const uint64_t r = rec_off[i];
         uint64_t o = 0, l = 0;
         if (header_in(r, stream_len)) {
-            const uint64_t ks = ld_le64(stream + r + 14);
-            const uint64_t vs = ld_le64(stream + r + 22);
+            uint64_t ks, vs;
+            ld_header_sizes(stream + r, ks, vs);
             o = r + 30 + ks;
             l = vs;
             if (ks > stream_len || vs > stream_len || o + l > stream_len) {
