@@ -78,6 +78,8 @@ def parse():
     ap.add_argument("--leaves", type=int, default=1 << 20)
     ap.add_argument("--key-bytes", type=int, default=16, help="records configs: KeySize (the Value starts at +30+key)")
     ap.add_argument("--value-bytes", type=int, default=4096)
+    ap.add_argument("--preroll-s", type=float, default=0.3,
+                    help="untimed steps for at least this long before the warmup (clock settling)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-leaves", type=int, default=1 << 20)
     ap.add_argument("--verify", action="store_true", help="check the root against the C oracle")
@@ -125,8 +127,41 @@ def cpu_baseline(n_leaves: int, vlen: int) -> dict:
     }
 
 
+def launcher_cmd(argv, n: int, port: int):
+    """The one-node launch of N rank processes (one per GPU) for this bench."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def ensure_ranks(args, argv, run=None) -> "int | None":
+    """`--gpus N` must match the process group.  Under a launcher WORLD_SIZE is
+    set and must equal N; without one, N > 1 starts the N ranks as a child
+    torch.distributed.run (before this process touches a GPU) and returns its
+    exit code; None means: run the bench in this process."""
+    world = os.environ.get("WORLD_SIZE")
+    if world is not None:
+        if int(world) != args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+            return 2
+        return None
+    if args.gpus <= 1:
+        return None
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return (run or subprocess.call)(launcher_cmd(argv, args.gpus, port))
+
+
 def main():
     args = parse()
+    if args.config in ("records", "records_verify") and args.value_bytes <= 30 + args.key_bytes:
+        raise SystemExit("bench.py: --value-bytes (the record size) must exceed the 30-B header + --key-bytes")
+    rc = ensure_ranks(args, sys.argv[1:])
+    if rc is not None:
+        sys.exit(rc)
     import torch
     import torch.distributed as dist
 
@@ -238,6 +273,20 @@ def main():
         if world > 1 and not one_tree:  # C1: gather the per-table roots
             dist.all_gather_into_tensor(roots, nodes[-20:])
 
+    # Untimed pre-roll, independent of --warmup: the shader clock settles only
+    # after ~30 ms of back-to-back launches ("The clock"),
+    # so run steps for at least PREROLL_S before the caller's warmup steps.
+    torch.cuda.synchronize()
+    preroll_steps, t_pre = 0, time.perf_counter()
+    while time.perf_counter() - t_pre < args.preroll_s or preroll_steps < 1:
+        step()
+        preroll_steps += 1
+        if preroll_steps % 8 == 0:
+            torch.cuda.synchronize()
+    torch.cuda.synchronize()
+    if records and (int(d_err.item()) != 0 or (verify_crc and int(d_stats[2].item()) != 0)):
+        # a malformed synthetic stream would time empty hashes
+        raise SystemExit("bench.py: the record stream failed the header checks")
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -325,6 +374,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "preroll_steps": preroll_steps,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -363,6 +413,9 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
+                # the whole step (leaf + tree + launches, N ranks): payload per
+                # GPU / ms_per_step / peak
+                "step_frac": round(nbytes / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
                 "traffic_bounds": traffic_bounds,  # RDREQ x 64 .. x 128 B (profiles/pmc_traffic.json)
                 "valu_ceiling": SHA1_VALU_CEILING_GBS,

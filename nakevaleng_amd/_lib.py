@@ -94,6 +94,7 @@ SIGNATURES = {
 }
 
 _lib = None
+_OWN = object()  # Context.stream sentinel: the context's own stream
 
 
 class NkvError(RuntimeError):
@@ -159,6 +160,7 @@ class Context:
         check(lib().nkv_ctx_create(device, ctypes.byref(h)), f"nkv_ctx_create(device={device})")
         self.h = h
         self.device = device
+        self.stream = _OWN  # the context's own stream until set_stream
 
     def close(self) -> None:
         if getattr(self, "h", None):
@@ -177,8 +179,29 @@ class Context:
     def __exit__(self, *exc):
         self.close()
 
-    def set_stream(self, stream_handle: Optional[int]) -> None:
-        check(lib().nkv_ctx_set_stream(self.h, stream_handle))
+    def set_stream(self, stream_handle) -> None:
+        """Launch on `stream_handle` (a hipStream_t as int, None = the null stream,
+        _OWN = the context's own stream)."""
+        if stream_handle is _OWN:
+            check(lib().nkv_ctx_use_own_stream(self.h))
+        else:
+            check(lib().nkv_ctx_set_stream(self.h, stream_handle))
+        self.stream = stream_handle
+
+    def on_stream(self, stream_handle):
+        """Context manager: launch on `stream_handle` inside the block, then restore."""
+        ctx = self
+
+        class _On:
+            def __enter__(self_):
+                self_.prev = ctx.stream
+                ctx.set_stream(stream_handle)
+                return ctx
+
+            def __exit__(self_, *exc):
+                ctx.set_stream(self_.prev)
+
+        return _On()
 
     def set_option(self, key: int, value: int) -> None:
         check(lib().nkv_ctx_set_option(self.h, key, value), f"nkv_ctx_set_option({key}, {value})")
@@ -204,7 +227,23 @@ class Context:
 _default: dict = {}
 
 
-def default_context(device: int = 0) -> Context:
+def current_device() -> int:
+    """The device this process works on: torch's current device when a GPU is
+    visible (one process per GPU binds it with torch.cuda.set_device), else the
+    launcher's LOCAL_RANK (0 without a launcher)."""
+    try:
+        import torch
+        if torch.cuda.is_available():
+            return int(torch.cuda.current_device())
+    except ImportError:
+        pass
+    return int(os.environ.get("LOCAL_RANK", "0"))
+
+
+def default_context(device: Optional[int] = None) -> Context:
+    """One shared context per device; device None = current_device()."""
+    if device is None:
+        device = current_device()
     ctx = _default.get(device)
     if ctx is None:
         ctx = _default[device] = Context(device)

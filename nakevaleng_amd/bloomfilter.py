@@ -78,22 +78,27 @@ class BloomFilter:
         return bytes(self._contents)
 
     def QueryMany(self, elements: Sequence[bytes]) -> np.ndarray:
-        """Query (bloomfilter.go:93-111) for a batch, on the device."""
+        """Query (bloomfilter.go:93-111) for a batch, on the context's device.
+
+        The inputs go to that device and the launch uses its current torch
+        stream; the context's previous stream is restored afterwards."""
         import torch
         self._flush()
         if not elements:
             return np.zeros(0, bool)
         ctx = self._ctx or _lib.default_context()
+        dev = torch.device("cuda", ctx.device)
         data, off, lens = _pack(elements)
         words = np.zeros(((self.M + 31) // 32) * 4, np.uint8)
         words[:len(self._contents)] = np.frombuffer(self._contents, np.uint8)
-        d = [torch.from_numpy(a.view(np.uint8).copy()).cuda() for a in (data, off, lens, words)]
-        out = torch.zeros(len(elements), dtype=torch.uint8, device="cuda")
-        ctx.set_stream(torch.cuda.current_stream().cuda_stream)
-        _lib.check(_lib.lib().nkv_bloom_query_dev(ctx.h, d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(),
-                                                  len(elements), self.M, self.K, self._seed0, d[3].data_ptr(),
-                                                  out.data_ptr()))
-        torch.cuda.synchronize()
+        d = [torch.from_numpy(a.view(np.uint8).copy()).to(dev) for a in (data, off, lens, words)]
+        out = torch.zeros(len(elements), dtype=torch.uint8, device=dev)
+        stream = torch.cuda.current_stream(dev)
+        with ctx.on_stream(stream.cuda_stream):
+            _lib.check(_lib.lib().nkv_bloom_query_dev(ctx.h, d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(),
+                                                      len(elements), self.M, self.K, self._seed0,
+                                                      d[3].data_ptr(), out.data_ptr()))
+        stream.synchronize()
         return out.cpu().numpy().astype(bool)
 
     def Query(self, element: bytes) -> bool:

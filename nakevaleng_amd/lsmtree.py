@@ -22,13 +22,33 @@ def shard(num_tables: int, world: int, rank: int) -> List[int]:
     return list(range(rank, num_tables, world))
 
 
-def gpu_table_root(table: Table, device: int = 0) -> bytes:
-    """Root of one table's Merkle tree, values hashed in place on the device."""
+def rank_device(device=None) -> int:
+    """The GPU this rank hashes on: `device` when given (an int or torch.device),
+    else the launcher's LOCAL_RANK (one process per GPU, modulo the visible
+    devices), else the process's current device."""
+    import os
+    if device is not None:
+        return device.index if hasattr(device, "index") else int(device)
+    local = os.environ.get("LOCAL_RANK")
+    if local is not None:
+        try:
+            import torch
+            cnt = torch.cuda.device_count()
+        except ImportError:
+            cnt = 0
+        return int(local) % cnt if cnt else int(local)
+    from . import _lib
+    return _lib.current_device()
+
+
+def gpu_table_root(table: Table, device: Optional[int] = None) -> bytes:
+    """Root of one table's Merkle tree, values hashed in place on `device`
+    (None: rank_device())."""
     from . import _lib
     stream, rec_sizes = table
     n = len(rec_sizes)
     L = _lib.lib()
-    ctx = _lib.default_context(device)
+    ctx = _lib.default_context(rank_device(device))
     buf = np.frombuffer(bytes(stream) + b"\0", dtype=np.uint8)
     rs = np.ascontiguousarray(rec_sizes, dtype=np.uint64)
     root = np.zeros(20, np.uint8)
@@ -66,19 +86,23 @@ def gather_roots(local: Dict[int, bytes], num_tables: int, device=None) -> List[
     return roots  # type: ignore[return-value]
 
 
-def compact_roots(tables: Sequence[Table], build: Callable[[Table], bytes] = None, device=None) -> List[bytes]:
+def compact_roots(tables: Sequence[Table], build: Callable[[Table, int], bytes] = None,
+                  device=None) -> List[bytes]:
     """Build the Merkle tree of every table this rank owns and all-gather the roots.
 
-    `build` maps one table to its root; the default hashes on this rank's GPU.
+    `build(table, device)` maps one table to its root; the default hashes on
+    this rank's GPU (rank_device(device): LOCAL_RANK under one process per GPU),
+    and the roots are gathered from that same device over RCCL.
     """
     import torch.distributed as dist
 
     world = dist.get_world_size() if dist.is_initialized() else 1
     rank = dist.get_rank() if dist.is_initialized() else 0
+    dev = rank_device(device)
     if build is None:
-        dev = 0 if device is None else (device.index if hasattr(device, "index") else int(device))
-        build = lambda tb: gpu_table_root(tb, dev)  # noqa: E731
-    local = {i: build(tables[i]) for i in shard(len(tables), world, rank)}
+        build = gpu_table_root
+    local = {i: build(tables[i], dev) for i in shard(len(tables), world, rank)}
     if world == 1:
         return [local[i] for i in range(len(tables))]
-    return gather_roots(local, len(tables), device)
+    import torch
+    return gather_roots(local, len(tables), torch.device("cuda", dev))

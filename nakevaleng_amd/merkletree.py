@@ -39,7 +39,7 @@ class _LeafBatch:
     def __init__(self):
         self.values: List[bytes] = []
         self.digests: Optional[np.ndarray] = None
-        self.device = 0
+        self.device = None  # None: the process's device (_lib.current_device)
 
     def add(self, data: bytes) -> int:
         self.values.append(bytes(data))

@@ -13,7 +13,7 @@ gob encoding) is outside this path and unchanged.
 """
 from __future__ import annotations
 
-from typing import Iterable, List
+from typing import Iterable, List, Optional
 
 import numpy as np
 
@@ -51,10 +51,11 @@ def make_table_secondaries(path: str, dbname: str, level: int, run: int,
 
 
 def make_metadata_from_records(path: str, dbname: str, level: int, run: int, stream: bytes,
-                               rec_sizes: np.ndarray, device: int = 0) -> bytes:
+                               rec_sizes: np.ndarray, device: Optional[int] = None) -> bytes:
     """Same output file as make_metadata, straight from the Data-table bytes and
     KeyContext.RecSize list: values are located and hashed on the device
-    (nkv_tree_from_records).  Returns the root digest."""
+    (nkv_tree_from_records) on `device` (None: the process's device).  Returns the
+    root digest."""
     n = len(rec_sizes)
     if n == 0:
         raise MerkleTreeError("cannot build Merkle Tree from 0 nodes")

@@ -41,16 +41,17 @@ def oracle_root(table):
 def _worker(rank, world, port, k, q):
     import torch.distributed as dist
     from nakevaleng_amd import lsmtree
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    # what torch.distributed.run sets for each rank of one node
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LOCAL_RANK=str(rank))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    built = []
+    devices = []
 
-    def build(tb):
-        built.append(1)
+    def build(tb, device):
+        devices.append(device)
         return oracle_root(tb)
 
     roots = lsmtree.compact_roots(make_tables(k), build=build)
-    q.put((rank, len(built), [r.hex() for r in roots]))
+    q.put((rank, devices, [r.hex() for r in roots]))
     dist.destroy_process_group()
 
 
@@ -67,5 +68,22 @@ def test_compact_roots_world2(oracle, k):
         p.join(timeout=60)
     want = [oracle_root(t).hex() for t in make_tables(k)]
     assert res[0][2] == want and res[1][2] == want  # every rank holds every root
-    assert res[0][1] + res[1][1] == k  # each table built exactly once
-    assert res[0][1] == (k + 1) // 2
+    assert len(res[0][1]) + len(res[1][1]) == k  # each table built exactly once
+    assert len(res[0][1]) == (k + 1) // 2
+    # each rank hashes on its own device (LOCAL_RANK), never all on device 0
+    assert set(res[0][1]) == {0} and set(res[1][1]) == {1}
+
+
+def test_rank_device_resolution(monkeypatch):
+    from nakevaleng_amd import lsmtree
+    import torch
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 0)
+    assert lsmtree.rank_device(3) == 3
+    assert lsmtree.rank_device(torch.device("cuda", 5)) == 5
+    monkeypatch.setenv("LOCAL_RANK", "6")
+    assert lsmtree.rank_device() == 6
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 4)
+    assert lsmtree.rank_device() == 2  # LOCAL_RANK modulo the visible devices
+    monkeypatch.delenv("LOCAL_RANK")
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: False)
+    assert lsmtree.rank_device() == 0
