@@ -78,6 +78,9 @@ typedef struct nkv_ctx nkv_ctx;
 
 /* ---- errors, devices, contexts ---- */
 const char *nkv_strerror(int status);
+/* "nkv-src-sha256:<64 hex>": SHA-256 of the sources and build flags this
+ * library was compiled from (nakevaleng_amd/build.py checks it before use). */
+const char *nkv_build_id(void);
 int nkv_device_count(int *count);
 int nkv_ctx_create(int device, nkv_ctx **out);
 void nkv_ctx_destroy(nkv_ctx *ctx);
@@ -178,6 +181,15 @@ int nkv_tree_from_values(nkv_ctx *ctx, const uint8_t *base, const uint64_t *off,
 uint64_t nkv_generic_bfs_size(const uint64_t *len, uint64_t n);
 int nkv_tree_generic(nkv_ctx *ctx, const uint8_t *data, const uint64_t *off, const uint64_t *len,
                      uint64_t n, uint8_t *root20, uint8_t *upper_out, uint8_t *img_out);
+
+/* (*MerkleTree).Validate (merkletree.go:162-171) of a tree New built from n
+ * leaves: rehash (merklenode.go:99-108) recomputes every internal node from
+ * the leaves' Data -- leaf i = leaf_data[off[i] .. off[i]+len[i]), a NewLeaf
+ * leaf is its 20-byte digest, any other length is a generic leaf (README
+ * example); pads contribute no bytes -- on the device, and compares the 20
+ * bytes with root20 (the tree's Root.Data).  *ok = 1 if they match, else 0. */
+int nkv_tree_validate(nkv_ctx *ctx, const uint8_t *leaf_data, const uint64_t *off, const uint64_t *len,
+                      uint64_t n, const uint8_t *root20, int *ok);
 
 /* Merkle step straight from a serialized Data-table stream (the records
  * written by record.Serialize, record.go:191-199) and the RecSize of each

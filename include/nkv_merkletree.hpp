@@ -87,6 +87,9 @@ class Session {
     }
 
     const uint8_t* arena() const { return static_cast<const uint8_t*>(arena_); }
+    // nkv_host_alloc calls so far: a sealed batch's arena is reused by the next
+    // batch (flush after flush), so this grows only when a batch outgrows it
+    uint64_t arena_allocs() const { return allocs_; }
 
     void ResolveBatch(Batch& b) {
         if (b.resolved) return;
@@ -103,6 +106,7 @@ class Session {
         while (want < bytes) want *= 2;
         void* p = nullptr;
         check(nkv_host_alloc(ctx_, want, &p), "nkv_host_alloc");
+        ++allocs_;
         if (arena_) {
             std::memcpy(p, arena_, used_);
             nkv_host_free(ctx_, arena_);
@@ -113,7 +117,7 @@ class Session {
 
     nkv_ctx* ctx_ = nullptr;
     void* arena_ = nullptr;
-    uint64_t cap_ = 0, used_ = 0, epoch_ = 0;
+    uint64_t cap_ = 0, used_ = 0, epoch_ = 0, allocs_ = 0;
     std::shared_ptr<Batch> batch_;
 };
 
@@ -235,9 +239,32 @@ class MerkleTree {  // merkletree.go:13-15
         Root = nodes_.empty() ? nullptr : &nodes_.front();
     }
 
-    // merkletree.go:162-171: recompute the root from the leaves' Data
+    // merkletree.go:162-171: recompute the root from the leaves' Data.  A tree
+    // New built (Root unchanged) is rehashed in one device call over its
+    // leaves' current Data (nkv_tree_validate); any other tree per depth.
     bool Validate() {
         if (!Root) throw std::runtime_error("Validate: nil root");
+        if (Root == built_root_ && !leaves_.empty()) {
+            bool childless = true;
+            for (MerkleNode* x : leaves_) childless = childless && !x->Left && !x->Right;
+            if (childless) {
+                if (Root->Resolve().size() < 20) throw std::runtime_error("Validate: index out of range");
+                std::vector<uint8_t> flat;
+                std::vector<uint64_t> off, len;
+                for (MerkleNode* x : leaves_) {
+                    const auto& d = x->Resolve();
+                    off.push_back(flat.size());
+                    len.push_back(d.size());
+                    flat.insert(flat.end(), d.begin(), d.end());
+                }
+                flat.push_back(0);
+                int ok = 0;
+                check(nkv_tree_validate(Session::Default().ctx(), flat.data(), off.data(), len.data(), leaves_.size(),
+                                        Root->Data.data(), &ok),
+                      "Validate");
+                return ok != 0;
+            }
+        }
         std::vector<uint8_t> h = Rehash(Root);
         if (Root->Resolve().size() < 20 || h.size() < 20)
             throw std::runtime_error("Validate: index out of range");
@@ -293,6 +320,8 @@ class MerkleTree {  // merkletree.go:13-15
 
     std::deque<MerkleNode> nodes_;  // owns every node of the tree (stable addresses)
     std::vector<uint8_t> levels_;
+    std::vector<MerkleNode*> leaves_;  // level 0 as New built it
+    MerkleNode* built_root_ = nullptr;
 };
 
 inline std::vector<std::vector<uint8_t>> Sha1Many(const std::vector<std::vector<uint8_t>>& msgs) {
@@ -368,6 +397,7 @@ inline std::unique_ptr<MerkleTree> New(std::vector<MerkleNode> level, std::strin
         pool.push_back(x);
         below.push_back(&pool.back());
     }
+    t->leaves_ = below;
     const int lv = nkv_num_levels(n);
     for (int L = 1; L < lv; ++L) {
         if (below.size() % 2) {
@@ -385,7 +415,7 @@ inline std::unique_ptr<MerkleTree> New(std::vector<MerkleNode> level, std::strin
         }
         below.swap(cur);
     }
-    t->Root = below[0];
+    t->Root = t->built_root_ = below[0];
     return t;
 }
 

@@ -40,6 +40,7 @@ _int = ctypes.c_int
 # name -> (restype, argtypes); every symbol include/nkv_merkle.h declares
 SIGNATURES = {
     "nkv_strerror": (ctypes.c_char_p, [_int]),
+    "nkv_build_id": (ctypes.c_char_p, []),
     "nkv_device_count": (_int, [ctypes.POINTER(_int)]),
     "nkv_ctx_create": (_int, [_int, ctypes.POINTER(_vp)]),
     "nkv_ctx_destroy": (None, [_vp]),
@@ -63,6 +64,7 @@ SIGNATURES = {
     "nkv_tree_from_values": (_int, [_vp, _u8p, _u64p, _u64p, _u64, _u8p, _u8p, _u8p]),
     "nkv_generic_bfs_size": (_u64, [_u64p, _u64]),
     "nkv_tree_generic": (_int, [_vp, _u8p, _u64p, _u64p, _u64, _u8p, _u8p, _u8p]),
+    "nkv_tree_validate": (_int, [_vp, _u8p, _u64p, _u64p, _u64, _u8p, ctypes.POINTER(_int)]),
     "nkv_tree_from_records": (_int, [_vp, _u8p, _u64, _u64p, _u64, _u8p, _u8p, _u8p]),
     "nkv_record_crc": (_int, [_vp, _u8p, _u64, _u64p, _u64, ctypes.POINTER(ctypes.c_uint32), _u64p, _u64p]),
     "nkv_bloom_params": (_int, [_u64, ctypes.c_double, ctypes.POINTER(ctypes.c_uint32),

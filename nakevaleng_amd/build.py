@@ -1,7 +1,16 @@
-"""Build libnkvmerkle.so in-tree (hipcc, gfx950).  Used by __graft_entry__.build()."""
+"""Build libnkvmerkle.so in-tree (hipcc, gfx950).  Used by __graft_entry__.build().
+
+The library embeds the SHA-256 of its sources, headers and compile flags
+(nkv_build_id(), a string in .rodata).  build() compares it with the tree's
+sources and recompiles on any mismatch, so a library that did not come from
+these sources is never used -- on the GPU box as here (file times say nothing
+once the tree has been copied).
+"""
 from __future__ import annotations
 
+import hashlib
 import os
+import re
 import subprocess
 import sys
 
@@ -10,30 +19,52 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 SO = os.path.join(PKG, "libnkvmerkle.so")
 SOURCES = ["kernels.hip", "crc.hip", "bloom.hip", "capi.cpp", "host_stage.cpp"]
-HEADERS = ["internal.hpp", "sha1_dev.hpp", "host_stage.hpp"]
+HEADERS = ["internal.hpp", "sha1_dev.hpp", "host_stage.hpp", "crc_dev.hpp"]
 ARCH = os.environ.get("NKV_OFFLOAD_ARCH", "gfx950")
+FLAGS = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread",
+         "-Wall", "-Wno-unused-result"]
+_ID = re.compile(rb"nkv-src-sha256:([0-9a-f]{64})")
 
 
-def _stale() -> bool:
-    if not os.path.exists(SO):
-        return True
-    t = os.path.getmtime(SO)
-    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(ROOT, "include", "nkv_merkle.h")]
-    return any(os.path.getmtime(d) > t for d in deps)
+def source_hash(diag: bool = False) -> str:
+    """SHA-256 over the compile flags and every source/header the library is built from."""
+    h = hashlib.sha256()
+    h.update(" ".join(FLAGS + (["-DNKV_DIAG"] if diag else [])).encode())
+    for path in [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(ROOT, "include", "nkv_merkle.h")]:
+        h.update(os.path.basename(path).encode() + b"\0")
+        with open(path, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
+def embedded_hash(so: str = SO):
+    """The source hash compiled into `so` (None if absent or unreadable); no loading."""
+    try:
+        with open(so, "rb") as f:
+            m = _ID.search(f.read())
+    except OSError:
+        return None
+    return m.group(1).decode() if m else None
 
 
 DIAG_SO = os.path.join(PKG, "libnkvmerkle_diag.so")
+last_status = ""  # what the latest build() did (printed by it, reported by the GPU tests)
 
 
-def build(force: bool = False, verbose: bool = False, diag: bool = False) -> str:
+def build(force: bool = False, verbose: bool = False, diag: bool = False, quiet: bool = False) -> str:
     """diag=True builds the stamp-instrumented library (tools/diag_timeline.py only)."""
+    global last_status
     so = DIAG_SO if diag else SO
-    if not force and not diag and not _stale():
-        return SO
+    want = source_hash(diag)
+    have = embedded_hash(so)
+    if not force and have == want:
+        last_status = f"{os.path.basename(so)}: embedded source hash {want[:16]} matches the sources (no rebuild)"
+        if not quiet:
+            print(last_status, file=sys.stderr)
+        return so
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     tmp = so + ".tmp"
-    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread",
-           "-Wall", "-Wno-unused-result", "-I", os.path.join(ROOT, "include"), "-I", CSRC]
+    cmd = [hipcc] + FLAGS + ["-I", os.path.join(ROOT, "include"), "-I", CSRC, f'-DNKV_SRC_HASH="{want}"']
     if diag:
         cmd.append("-DNKV_DIAG")
     cmd += [os.path.join(CSRC, f) for f in SOURCES] + ["-o", tmp]
@@ -41,6 +72,12 @@ def build(force: bool = False, verbose: bool = False, diag: bool = False) -> str
         print(" ".join(cmd), file=sys.stderr)
     subprocess.check_call(cmd)
     os.replace(tmp, so)
+    if embedded_hash(so) != want:
+        raise RuntimeError(f"{so}: the build did not embed source hash {want}")
+    last_status = (f"{os.path.basename(so)}: rebuilt with hipcc --offload-arch={ARCH} "
+                   f"(embedded hash was {have[:16] if have else 'none'}, sources {want[:16]})")
+    if not quiet:
+        print(last_status, file=sys.stderr)
     return so
 
 

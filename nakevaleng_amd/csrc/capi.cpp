@@ -188,6 +188,16 @@ int grow_host(nkv_ctx* c, size_t bytes) {
 
 uint64_t align16(uint64_t x) { return (x + 15) & ~uint64_t(15); }
 
+// sum(rec_size) <= stream_len, checked term by term so a wrapped sum cannot pass
+bool records_fit(const uint64_t* rec_size, uint64_t n, uint64_t stream_len) {
+    uint64_t left = stream_len;
+    for (uint64_t i = 0; i < n; ++i) {
+        if (rec_size[i] > left) return false;
+        left -= rec_size[i];
+    }
+    return true;
+}
+
 // Pack n host values into d_data at 16-byte aligned offsets and upload their
 // packed offsets/lengths to d_off / d_len.  The bytes go through the pipelined
 // pinned stager (a pool of host threads gathers chunk k+1 while chunk k is in
@@ -367,7 +377,13 @@ int tree_from_device_values(nkv_ctx* c, const uint8_t* base, const uint64_t* off
 
 }  // namespace
 
+#ifndef NKV_SRC_HASH
+#define NKV_SRC_HASH "unknown"
+#endif
+
 extern "C" {
+
+const char* nkv_build_id(void) { return "nkv-src-sha256:" NKV_SRC_HASH; }
 
 const char* nkv_strerror(int s) {
     switch (s) {
@@ -688,15 +704,44 @@ int nkv_tree_generic(nkv_ctx* c, const uint8_t* data, const uint64_t* off, const
     return NKV_OK;
 }
 
+int nkv_tree_validate(nkv_ctx* c, const uint8_t* leaf_data, const uint64_t* off, const uint64_t* len,
+                      uint64_t n, const uint8_t* root20, int* ok) {
+    TRY(bind(c));
+    if (!ok) return NKV_ERR_INVALID;
+    *ok = 0;
+    if (n == 0) return NKV_ERR_EMPTY;  // New never builds an empty tree (merkletree.go:19-21)
+    if (!leaf_data || !off || !len || !root20) return NKV_ERR_INVALID;
+    bool all20 = true;
+    for (uint64_t i = 0; i < n && all20; ++i) all20 = len[i] == NKV_DIGEST_SIZE;
+    uint8_t got[NKV_DIGEST_SIZE];
+    if (all20) {
+        // NewLeaf leaves: gather the digests into level 0 and reduce to the root
+        TRY(grow_host(c, 8 * n));
+        uint64_t* dst = static_cast<uint64_t*>(c->h_stage);
+        for (uint64_t i = 0; i < n; ++i) dst[i] = NKV_DIGEST_SIZE * i;
+        TRY(grow(c->d_nodes, NKV_DIGEST_SIZE * total_of(n)));
+        uint8_t* nodes = static_cast<uint8_t*>(c->d_nodes.p);
+        const Segments seg{leaf_data, off, len, dst, n};
+        HIPTRY(c->stage.upload(seg, NKV_DIGEST_SIZE * n, nodes, c->stream));
+        HIPTRY(launch_reduce(nodes, n, 0, levels_of(n) - 1, c->stream));
+        HIPTRY(hipMemcpyAsync(c->h_small, nodes + NKV_DIGEST_SIZE * (total_of(n) - 1), NKV_DIGEST_SIZE,
+                              hipMemcpyDeviceToHost, c->stream));
+        HIPTRY(hipStreamSynchronize(c->stream));
+        memcpy(got, c->h_small, NKV_DIGEST_SIZE);
+    } else {
+        TRY(nkv_tree_generic(c, leaf_data, off, len, n, got, nullptr, nullptr));
+    }
+    *ok = memcmp(got, root20, NKV_DIGEST_SIZE) == 0;
+    return NKV_OK;
+}
+
 int nkv_tree_from_records(nkv_ctx* c, const uint8_t* stream, uint64_t stream_len,
                           const uint64_t* rec_size, uint64_t n, uint8_t* root20,
                           uint8_t* nodes_out, uint8_t* img_out) {
     TRY(bind(c));
     if (n == 0) return NKV_ERR_EMPTY;
     if (!stream || !rec_size) return NKV_ERR_INVALID;
-    uint64_t sum = 0;
-    for (uint64_t i = 0; i < n; ++i) sum += rec_size[i];
-    if (sum > stream_len) return NKV_ERR_INVALID;
+    if (!records_fit(rec_size, n, stream_len)) return NKV_ERR_INVALID;
     TRY(stage_stream(c, stream, stream_len, c->d_data, rec_size, n, c->d_aux));
     TRY(grow(c->d_off, 8 * n));
     TRY(grow(c->d_len, 8 * n));
@@ -721,9 +766,7 @@ int nkv_record_crc(nkv_ctx* c, const uint8_t* stream, uint64_t stream_len, const
     if (first_bad) *first_bad = ~0ull;
     if (n == 0) return NKV_OK;
     if (!stream || !rec_size) return NKV_ERR_INVALID;
-    uint64_t sum = 0;
-    for (uint64_t i = 0; i < n; ++i) sum += rec_size[i];
-    if (sum > stream_len) return NKV_ERR_INVALID;
+    if (!records_fit(rec_size, n, stream_len)) return NKV_ERR_INVALID;
     TRY(stage_stream(c, stream, stream_len, c->d_data, rec_size, n, c->d_aux));
     TRY(grow(c->d_len, 8 * n));
     TRY(grow(c->d_off, 4 * n));
@@ -792,9 +835,7 @@ int nkv_bloom_from_records(nkv_ctx* c, const uint8_t* stream, uint64_t stream_le
     TRY(grow(c->d_img, wbytes));
     HIPTRY(hipMemsetAsync(c->d_img.p, 0, wbytes, c->stream));
     if (n) {
-        uint64_t sum = 0;
-        for (uint64_t i = 0; i < n; ++i) sum += rec_size[i];
-        if (sum > stream_len) return NKV_ERR_INVALID;
+        if (!records_fit(rec_size, n, stream_len)) return NKV_ERR_INVALID;
         TRY(stage_stream(c, stream, stream_len, c->d_data, rec_size, n, c->d_aux));
         TRY(grow(c->d_len, 8 * n));
         uint64_t* rec_off = static_cast<uint64_t*>(c->d_len.p);

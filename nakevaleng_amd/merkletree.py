@@ -19,6 +19,7 @@ deferred-leaf design as the Go cgo shim in INTEGRATION.md).
 """
 from __future__ import annotations
 
+import ctypes
 import io
 from typing import List, Optional
 
@@ -151,6 +152,7 @@ class MerkleTree:  # merkletree.go:13-15
         self._leaves: Optional[List[MerkleNode]] = None  # copies of the level given to New
         self._image: Optional[bytes] = None
         self._materialized = False
+        self._built_root: Optional[MerkleNode] = None  # the root New materialized
 
     # ---- Root (pointer tree) ----
     @property
@@ -179,7 +181,7 @@ class MerkleTree:  # merkletree.go:13-15
             for i in range(counts[L]):
                 cur.append(MerkleNode(self.nodes[s + i].tobytes(), prev[2 * i], prev[2 * i + 1]))
             below = cur
-        self._root = below[0]
+        self._root = self._built_root = below[0]
         self._materialized = True
 
     # ---- Serialize ----
@@ -222,12 +224,41 @@ class MerkleTree:  # merkletree.go:13-15
 
     # ---- Validate ----
     def Validate(self) -> bool:  # merkletree.go:162-171
+        if self._leaves is not None and (not self._materialized or self._root is self._built_root):
+            # a tree New built, links unchanged: rehash is the tree over the
+            # leaves' current Data -- one device call (nkv_tree_validate)
+            return _validate_leaves(self._leaves, root_of(self))
         root = self.Root
         h = _rehash(root)
         for i in range(20):
             if root.Data[i] != h[i]:
                 return False
         return True
+
+
+def _validate_leaves(leaves: List[MerkleNode], root: bytes) -> bool:
+    """Validate of a tree New built from `leaves` (C-ABI nkv_tree_validate)."""
+    if any(x.Left is not None or x.Right is not None for x in leaves):
+        return _rehash_root_matches(leaves, root)
+    datas = [x.Data for x in leaves]
+    n = len(datas)
+    lens = np.fromiter((len(d) for d in datas), dtype=np.uint64, count=n)
+    off = np.zeros(n, np.uint64)
+    if n > 1:
+        off[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    base = np.frombuffer(b"".join(datas) + b"\0", dtype=np.uint8)
+    if len(root) < 20:
+        raise MerkleTreeError("Validate: index out of range")  # Go: Root.Data[i], i < 20
+    r = np.frombuffer(bytes(root[:20]), np.uint8).copy()
+    ok = ctypes.c_int(0)
+    _lib.check(_lib.lib().nkv_tree_validate(_lib.default_context().h, _lib.p8(base), _lib.p64(off),
+                                            _lib.p64(lens), n, _lib.p8(r), ctypes.byref(ok)), "Validate")
+    return bool(ok.value)
+
+
+def _rehash_root_matches(leaves: List[MerkleNode], root: bytes) -> bool:
+    """Leaves that are themselves subtrees: rehash them first, then the tree above."""
+    return _validate_leaves([MerkleNode(_rehash(x)) for x in leaves], root)
 
 
 def _rehash(node: MerkleNode) -> bytes:

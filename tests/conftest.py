@@ -30,3 +30,13 @@ def nkv():
     ctx = _lib.Context(0)
     yield _lib, ctx
     ctx.close()
+
+
+def pytest_terminal_summary(terminalreporter):
+    """Say which library the run used and whether it was built from these sources."""
+    try:
+        from nakevaleng_amd import build as b
+    except Exception:  # pragma: no cover
+        return
+    if b.last_status:
+        terminalreporter.write_line("nakevaleng_amd: " + b.last_status)

@@ -87,5 +87,25 @@ int main(int argc, char** argv) {
         auto t = New(lv);
         std::printf("early_root %s\n", t->Root->String().c_str());
     }
+    // three flush cycles of one memtable size: the pinned arena is allocated by
+    // the first and reused by the next two (no nkv_host_alloc after the first)
+    {
+        auto& S = nkv::merkletree::Session::Default();
+        for (int k = 0; k < 3; ++k) {
+            const uint64_t n = 4096;
+            const size_t vlen = 512;
+            auto data = splitmix64_bytes(n * vlen, 0xF1u + uint64_t(k));
+            std::vector<MerkleNode> leaves;
+            for (uint64_t i = 0; i < n; ++i) leaves.push_back(NewLeaf(data.data() + i * vlen, vlen));
+            const uint64_t before = S.arena_allocs();
+            auto t = New(leaves);
+            std::printf("flush%d_allocs_during %llu\n", k, (unsigned long long)(S.arena_allocs() - before));
+            std::printf("flush%d_allocs_total %llu\n", k, (unsigned long long)S.arena_allocs());
+            std::printf("flush%d_root %s\n", k, t->Root->String().c_str());
+            std::printf("flush%d_validate %d\n", k, int(t->Validate()));
+            t->Root->Data[0] ^= 1;  // the stored root no longer matches the leaves
+            std::printf("flush%d_bad_root_validate %d\n", k, int(t->Validate()));
+        }
+    }
     return 0;
 }

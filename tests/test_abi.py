@@ -118,3 +118,18 @@ def test_bloom_params_host_function_matches_oracle(oracle):
     m, k = ctypes.c_uint32(0), ctypes.c_uint32(0)
     assert L.nkv_bloom_params(0, 0.01, ctypes.byref(m), ctypes.byref(k)) == _lib.NKV_ERR_INVALID
     assert L.nkv_bloom_params(10, 1.5, ctypes.byref(m), ctypes.byref(k)) == _lib.NKV_ERR_INVALID
+
+
+def test_build_id_is_the_source_hash(lib):
+    """The library in the tree was compiled from these sources (nakevaleng_amd/build.py)."""
+    from nakevaleng_amd import build as b
+    want = b.source_hash()
+    assert b.embedded_hash() == want
+    assert lib.lib().nkv_build_id().decode() == "nkv-src-sha256:" + want
+
+
+def test_validate_argument_checks_without_device(lib):
+    import ctypes
+    L = lib.lib()
+    ok = ctypes.c_int(7)
+    assert L.nkv_tree_validate(None, None, None, None, 0, None, ctypes.byref(ok)) == lib.NKV_ERR_INVALID

@@ -52,3 +52,11 @@ def test_cpp_mirror_on_gpu(tmp_path, oracle):
     assert kv["early_leaf3"] == hashlib.sha1(vals[3]).hexdigest()
     want = oracle.tree_from_digests(np.frombuffer(b"".join(hashlib.sha1(v).digest() for v in vals), np.uint8))
     assert kv["early_root"] == want[-1].tobytes().hex()
+    # flush after flush: one pinned arena, allocated by the first cycle only
+    assert int(kv["flush0_allocs_total"]) >= 1
+    assert kv["flush1_allocs_total"] == kv["flush0_allocs_total"] == kv["flush2_allocs_total"]
+    for k in range(3):
+        data = oracle.splitmix64_bytes(4096 * 512, 0xF1 + k)
+        want = oracle.tree_from_digests(oracle.leaf_hashes_strided(data, 512, 512, 4096))
+        assert kv[f"flush{k}_root"] == want[-1].tobytes().hex()
+        assert kv[f"flush{k}_validate"] == "1" and kv[f"flush{k}_bad_root_validate"] == "0"

@@ -1,0 +1,183 @@
+"""GPU: device Validate through the C-ABI, compaction over several tables on the
+rank's device, the configs[4] per-GPU table, and record-header edge cases.
+
+Reference: Validate / rehash (ds/merkletree/merkletree.go:162-171,
+merklenode.go:99-108); compaction's per-table Merkle step
+(core/lsmtree/lsmtree.go:71-128,211, core/sstable/sstable.go:35-47); the
+record layout (core/record/record.go:191-199).
+"""
+import ctypes
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+GOLDEN = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "merkle_golden.json")))
+
+
+def _validate(L, ctx, datas, root):
+    lens = np.fromiter((len(d) for d in datas), dtype=np.uint64, count=len(datas))
+    off = np.zeros(len(datas), np.uint64)
+    off[1:] = np.cumsum(lens[:-1])
+    base = np.frombuffer(b"".join(datas) + b"\0", np.uint8)
+    ok = ctypes.c_int(-1)
+    from nakevaleng_amd import _lib
+    r = np.frombuffer(bytes(root), np.uint8).copy()
+    _lib.check(L.nkv_tree_validate(ctx.h, _lib.p8(base), _lib.p64(off), _lib.p64(lens), len(datas), _lib.p8(r),
+                                   ctypes.byref(ok)))
+    return ok.value
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 7, 1000, 4097, 70001])
+def test_validate_abi_digest_leaves(nkv, oracle, n):
+    _lib, ctx = nkv
+    L = _lib.lib()
+    rng = np.random.default_rng(n)
+    leaf20 = rng.integers(0, 256, (n, 20), dtype=np.uint8)
+    root = oracle.tree_from_digests(leaf20.reshape(-1))[-1].tobytes()
+    datas = [leaf20[i].tobytes() for i in range(n)]
+    assert _validate(L, ctx, datas, root) == 1
+    bad = bytearray(root)
+    bad[19] ^= 1
+    assert _validate(L, ctx, datas, bytes(bad)) == 0
+    j = int(rng.integers(0, n))
+    datas[j] = bytes(20)
+    assert _validate(L, ctx, datas, root) == 0
+
+
+def test_validate_abi_generic_leaves(nkv):
+    """README example (raw leaves "1".."7"): rehash returns the raw Data at the leaves."""
+    _lib, ctx = nkv
+    g = GOLDEN["readme"]
+    datas = [x.encode() for x in g["leaves"]]
+    assert _validate(_lib.lib(), ctx, datas, bytes.fromhex(g["root"])) == 1
+    assert _validate(_lib.lib(), ctx, datas[::-1], bytes.fromhex(g["root"])) == 0
+
+
+def test_validate_abi_empty_and_args(nkv):
+    _lib, ctx = nkv
+    ok = ctypes.c_int(5)
+    assert _lib.lib().nkv_tree_validate(ctx.h, None, None, None, 0, None, ctypes.byref(ok)) == _lib.NKV_ERR_EMPTY
+    assert ok.value == 0
+
+
+def test_mirror_validate_fast_path_matches_rehash(nkv):
+    """The mirror's one-call Validate (New-built trees) agrees with the
+    reference-shaped per-depth rehash on good and corrupted trees."""
+    from nakevaleng_amd import merkletree as mt
+    vals = [bytes([i % 251]) * (i * 7 % 300) for i in range(333)]
+    t = mt.New([mt.NewLeaf(v) for v in vals])
+    assert t.Validate()
+    root = t.Root
+    assert mt._rehash(root) == root.Data
+    # corrupt an interior node: rehash ignores interior Data, only the root is compared
+    root.Left.Right.Data = bytes(20)
+    assert t.Validate() and mt._rehash(root) == root.Data
+    leaf = root
+    while leaf.Left is not None:
+        leaf = leaf.Left
+    leaf.Data = bytes(20)
+    assert not t.Validate()
+    assert mt._rehash(root) != root.Data
+    # a new Root (hand-built tree): the per-depth rehash path
+    t.Root = mt.MerkleNode(hashlib.sha1(b"a" + b"b").digest(), mt.MerkleNode(b"a"), mt.MerkleNode(b"b"))
+    assert t.Validate()
+
+
+def test_cpp_style_repeated_flush_validate(nkv, oracle):
+    """Three flush cycles (NewLeaf x n, New, Validate) in a row, checked each time."""
+    from nakevaleng_amd import merkletree as mt
+    for cycle in range(3):
+        vals = [bytes([cycle, i % 256]) * 50 for i in range(500 + cycle)]
+        t = mt.New([mt.NewLeaf(v) for v in vals])
+        want = oracle.tree_from_digests(np.frombuffer(b"".join(hashlib.sha1(v).digest() for v in vals), np.uint8))
+        assert mt.root_of(t) == want[-1].tobytes()
+        assert t.Validate()
+
+
+def _records_table(rng, n, value_bytes, key_bytes=16):
+    from nakevaleng_amd import record
+    recs = [record.New(rng.bytes(key_bytes), rng.bytes(value_bytes), timestamp=1700000000 + i) for i in range(n)]
+    return record.data_table(recs)
+
+
+def test_compact_roots_four_tables_default_build(nkv, oracle):
+    """configs[3] per-table shape (4 runs, lsm_run_max = 4), reduced record count:
+    compact_roots with its default builder hashes every table on this rank's
+    device and returns the roots by table index."""
+    from nakevaleng_amd import lsmtree, record
+    rng = np.random.default_rng(4)
+    tables = [_records_table(rng, 2048 + 17 * t, 4096 - 30 - 16) for t in range(4)]
+    roots = lsmtree.compact_roots(tables)
+    for (stream, sizes), got in zip(tables, roots):
+        off, ln = record.value_spans(stream, sizes)
+        want = oracle.tree_from_digests(oracle.leaf_hashes(np.frombuffer(stream, np.uint8), off, ln, threads=8))
+        assert got == want[-1].tobytes()
+
+
+def test_config4_per_gpu_table_8Mi_x_4KiB(nkv, oracle):
+    """BASELINE configs[4]'s per-GPU table: 8 Mi x 4 KiB values (32 GiB) in HBM,
+    leaf hash + the 24-level tree on the device; root against the oracle."""
+    import torch
+    _lib, ctx = nkv
+    L = _lib.lib()
+    n, vlen, seed = 8 << 20, 4096, 0x6E616B65
+    stream = torch.cuda.current_stream()
+    ctx.set_stream(stream.cuda_stream)
+    try:
+        data = torch.empty(n * vlen, dtype=torch.uint8, device="cuda")
+        nodes = torch.empty(L.nkv_total_nodes(n) * 20, dtype=torch.uint8, device="cuda")
+        _lib.check(L.nkv_fill_splitmix64_dev(ctx.h, data.data_ptr(), n * vlen, seed))
+        _lib.check(L.nkv_tree_from_strided_dev(ctx.h, data.data_ptr(), vlen, vlen, n, nodes.data_ptr()))
+        torch.cuda.synchronize()
+        got_leaves = nodes[:n * 20].cpu().numpy()
+        got_root = nodes[-20:].cpu().numpy().tobytes()
+        host = data.cpu().numpy()
+        del data
+        leaves = oracle.leaf_hashes_strided(host, vlen, vlen, n, threads=16)
+        del host
+        assert np.array_equal(got_leaves, leaves.reshape(-1))
+        want = oracle.tree_from_digests(leaves)
+        assert got_root == want[-1].tobytes()
+        assert L.nkv_num_levels(n) == 24
+    finally:
+        ctx.set_stream(_lib._OWN)
+        torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("r8", range(8))
+def test_locate_header_only_record_at_stream_end(nkv, r8):
+    """A 30-byte header-only record (KeySize = ValueSize = 0) ending exactly at
+    stream_len, starting at every offset mod 8 (the aligned 8-byte header loads)."""
+    import torch
+    from nakevaleng_amd import record
+    _lib, ctx = nkv
+    L = _lib.lib()
+    first = record.New(b"k" * 3, b"v" * (8 + (r8 - 1) % 8), timestamp=1)  # 33 + len = r8 (mod 8)
+    last = record.New(b"", b"", timestamp=2)
+    stream, sizes = record.data_table([first, last])
+    r = int(sizes[0])
+    assert r % 8 == r8 and len(stream) == r + 30
+    n = 2
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    try:
+        d_stream = torch.from_numpy(np.frombuffer(stream, np.uint8).copy()).cuda()
+        d_roff = torch.tensor([0, r], dtype=torch.int64, device="cuda")
+        d_voff = torch.empty(n, dtype=torch.int64, device="cuda")
+        d_vlen = torch.empty(n, dtype=torch.int64, device="cuda")
+        rc = L.nkv_locate_values_dev(ctx.h, d_stream.data_ptr(), len(stream), d_roff.data_ptr(), n,
+                                     d_voff.data_ptr(), d_vlen.data_ptr())
+        assert rc == _lib.NKV_OK
+        off, ln = record.value_spans(stream, sizes)
+        assert np.array_equal(d_voff.cpu().numpy().astype(np.uint64), off)
+        assert np.array_equal(d_vlen.cpu().numpy().astype(np.uint64), ln)
+        assert int(ln[1]) == 0 and int(off[1]) == len(stream)
+        # one byte short: the header no longer fits and the call reports it
+        rc = L.nkv_locate_values_dev(ctx.h, d_stream.data_ptr(), len(stream) - 1, d_roff.data_ptr(), n,
+                                     d_voff.data_ptr(), d_vlen.data_ptr())
+        assert rc == _lib.NKV_ERR_INVALID
+    finally:
+        ctx.set_stream(_lib._OWN)
