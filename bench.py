@@ -407,7 +407,7 @@ def main():
                 "kernel": ("leaf phase: length sort + ragged leaf SHA-1 (%s)" % LEAF_KERNEL.get(args.deep, "default"))
                           if mixed else
                           ("leaf phase: k_leaf_verify (record CRC + leaf SHA-1, input order)" if verify_crc else
-                           "leaf phase: k_leaf<offsets, 80-B window LDS-DMA stage> (input order)") if records else
+                           "leaf phase: k_leaf<offsets, aligned-segment stage + register shift> (input order)") if records else
                           "k_leaf<strided, LDS-DMA> (leaf SHA-1, level 0)",
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,

@@ -96,7 +96,11 @@ int nkv_ctx_sync(nkv_ctx *ctx);
                                4 / 5 = direct loads in 128 / 256-byte runs per lane,
                                9 / 10 = line-pair / 80-byte-window LDS-DMA stage for values
                                that are not 64-byte aligned (waves of equal full-block
-                               counts; other waves as 1) */
+                               counts; other waves as 1); 11 (the default for values that
+                               are not 16-byte aligned) = waves whose values share one
+                               offset mod 64 stream aligned 64-byte segments (LDS-DMA,
+                               or register loads when block counts differ) and shift
+                               them in registers, other waves as 10 */
 #define NKV_OPT_BUCKET 2    /* ragged values (nkv_tree_from_values*, nkv_tree_from_records*):
                                1 = hash in length-sorted order (work queue); 0 = in input
                                order; 2 (default) = auto: input order when the full-block

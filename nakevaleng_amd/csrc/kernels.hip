@@ -872,6 +872,173 @@ __device__ __forceinline__ bool sha1_blocks_pair(const bool kWindow, uint8_t* wb
     return true;
 }
 
+// LOAD 11: values that share one misalignment o = (address mod 64) != 0
+// across the wave (Data-table records of one size: Value at rec + 30 + KeySize,
+// record.go:191-199).  Each lane streams its value's 64-byte ALIGNED segments
+// straight into registers, in order, once: block b's window is bytes
+// [o, o + 64) of segments b, b + 1, so segment b + 1 is loaded for block b and
+// kept for block b + 1 (two register sets swap roles; the loop is unrolled by
+// two).  The L2 then sees every 128-byte line requested by one lane in two
+// consecutive blocks, as for 64-byte aligned values, where the window stages
+// (LOAD 8/9/10) request each line in three consecutive blocks and the line
+// falls out of the 4 MiB L2 in between (records form).
+// The funnel is the 16 v_perm_b32 byte swaps the aligned path runs anyway: o is
+// wave-uniform, so the dword offset o >> 2 selects one of 16 straight-line
+// register patterns (scalar branch) and the byte offset o & 3 is the v_perm
+// selector (an SGPR).  Every segment loaded holds a byte of the value's full
+// blocks, so no load steps past the value's last full block (no page beyond
+// the buffer is touched).  No LDS.  Returns false (and does nothing) when the
+// wave's live values do not share o, or o == 0.
+template <int Q>
+__device__ __forceinline__ void funnel_q(const uint32_t a[16], const uint32_t b[16], uint32_t sel, uint32_t w[16]) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int j = Q + i;  // dword j of the 32-dword pair (a, b): the window's dword i
+        const uint32_t lo = j < 16 ? a[j] : b[j - 16];
+        const uint32_t hi = j + 1 < 16 ? a[j + 1] : b[j - 15];
+        w[i] = be_word(hi, lo, sel);
+    }
+}
+
+__device__ __forceinline__ void funnel_u(uint32_t q, const uint32_t a[16], const uint32_t b[16], uint32_t sel,
+                                         uint32_t w[16]) {
+    switch (q) {
+        case 0: funnel_q<0>(a, b, sel, w); break;
+        case 1: funnel_q<1>(a, b, sel, w); break;
+        case 2: funnel_q<2>(a, b, sel, w); break;
+        case 3: funnel_q<3>(a, b, sel, w); break;
+        case 4: funnel_q<4>(a, b, sel, w); break;
+        case 5: funnel_q<5>(a, b, sel, w); break;
+        case 6: funnel_q<6>(a, b, sel, w); break;
+        case 7: funnel_q<7>(a, b, sel, w); break;
+        case 8: funnel_q<8>(a, b, sel, w); break;
+        case 9: funnel_q<9>(a, b, sel, w); break;
+        case 10: funnel_q<10>(a, b, sel, w); break;
+        case 11: funnel_q<11>(a, b, sel, w); break;
+        case 12: funnel_q<12>(a, b, sel, w); break;
+        case 13: funnel_q<13>(a, b, sel, w); break;
+        case 14: funnel_q<14>(a, b, sel, w); break;
+        default: funnel_q<15>(a, b, sel, w); break;
+    }
+}
+
+__device__ __forceinline__ void load_seg(const uint4* s, uint32_t r[16]) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint4 v = s[q];
+        r[4 * q + 0] = v.x;
+        r[4 * q + 1] = v.y;
+        r[4 * q + 2] = v.z;
+        r[4 * q + 3] = v.w;
+    }
+}
+
+__device__ __forceinline__ bool sha1_blocks_shift(uint8_t* wbuf, const uint8_t* p, bool live, uint32_t my_nfull,
+                                                  uint32_t h[5]) {
+    const uint32_t o = live ? uint32_t(reinterpret_cast<uintptr_t>(p) & 63u) : 0u;
+    // lane 0 is live whenever any lane is (dead lanes are the grid's tail)
+    const uint32_t o0 = __builtin_amdgcn_readfirstlane(o);
+    if (o0 == 0u || !__all(!live || o == o0)) return false;
+    const uint32_t nmax = wave_max_u32(live ? my_nfull : 0u);
+    if (nmax == 0) return true;
+    const uint32_t q = o0 >> 2;
+    const uint32_t sel = be_sel(o0 & 3u);
+    uint32_t a[16], b[16], w[16];
+    if (wbuf && __all(!live || my_nfull == nmax)) {
+        // Equal block counts: the segments go HBM -> LDS by LDS-DMA, one segment
+        // of lookahead, in k_leaf's aligned stage layout (value j's segment at
+        // wbuf + 64 j, chunks XOR-swizzled; sha1_blocks_lds), then into the
+        // register pair.  32-bit offsets from a wave-uniform base (one VGPR per
+        // DMA role) keep the register pair and the schedule within 64 VGPRs.
+        const uint64_t sa = reinterpret_cast<uintptr_t>(p) - o;
+        const uint64_t wb = wave_min_u64(live ? sa : ~uint64_t(0));
+        const uint64_t rel = live ? sa - wb : 0u;
+        if (__all(rel + 64ull * (uint64_t(nmax) + 1ull) <= 0xFFFFFFFFull)) {
+            const int lane = threadIdx.x & 63;
+            const uint8_t* base = reinterpret_cast<const uint8_t*>(wb);
+            const uint32_t cq = (uint32_t(lane) & 3u) ^ ((uint32_t(lane) >> 4) & 3u);
+            uint32_t voff[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                // dead values' roles re-read lane 0's segments into unused rows
+                const int j = 16 * k + (lane >> 2);
+                const bool lj = __shfl(int(live), j) != 0;
+                voff[k] = uint32_t(__shfl(int(uint32_t(rel)), lj ? j : 0)) + 16u * cq;
+            }
+            auto issue = [&](uint32_t sg) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    __builtin_amdgcn_global_load_lds(base + (voff[k] + 64u * sg), wbuf + 1024 * k, 16, 0, 0);
+            };
+            // chunk c of this lane's segment sits at (wbuf + 64 lane) + 16 (c ^ swz)
+            // = rd0 ^ 16 c with rd0 = wbuf + 64 lane + 16 swz (64-B aligned rows).
+            // One address VGPR, the other three are recomputed per read (the
+            // asm hides rd0 from hoisting: four live addresses spill at 64 VGPRs)
+            const uint32_t rd0 = uint32_t(reinterpret_cast<uintptr_t>(wbuf)) + 64u * uint32_t(lane) +
+                                 16u * ((uint32_t(lane) >> 2) & 3u);
+            auto take = [&](uint32_t r[16]) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                uint32_t ra = rd0;
+                asm volatile("" : "+v"(ra));
+                u32x4 v[4];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) v[c] = ds_read_b128_asm(ra ^ (16u * uint32_t(c)));
+                // stage read before its refill; the in/out operands keep the
+                // registers from being used before the wait
+                asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]) : : "memory");
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    r[4 * c + 0] = v[c].x;
+                    r[4 * c + 1] = v[c].y;
+                    r[4 * c + 2] = v[c].z;
+                    r[4 * c + 3] = v[c].w;
+                }
+            };
+            // segments 0 .. nmax (block k's window spans segments k and k + 1)
+            issue(0u);
+            take(a);
+            issue(1u);
+            for (uint32_t k = 0; k < nmax; k += 2) {
+                take(b);  // segment k + 1
+                if (k + 2 <= nmax) issue(k + 2);
+                funnel_u(q, a, b, sel, w);
+                if (live) sha1_compress(h, w);
+                if (k + 1 >= nmax) break;
+                take(a);  // segment k + 2
+                if (k + 3 <= nmax) issue(k + 3);
+                funnel_u(q, b, a, sel, w);
+                if (live) sha1_compress(h, w);
+            }
+            return true;
+        }
+    }
+    // p - o, not an integer-to-pointer cast: stays in the global address space
+    const uint4* seg = reinterpret_cast<const uint4*>(live ? p - o : p);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        a[i] = 0u;
+        b[i] = 0u;
+    }
+    if (my_nfull) load_seg(seg, a);
+    for (uint32_t k = 0; k < nmax; k += 2) {
+        // block k: segments k (a) and k + 1 (b)
+        if (k < my_nfull) load_seg(seg + 4 * (k + 1), b);
+        funnel_u(q, a, b, sel, w);
+        if (k < my_nfull) sha1_compress(h, w);
+        // keep each load after the previous compress: hoisted above it, a
+        // segment set would be live through the compress and spill at 64 VGPRs
+        // (the other resident waves cover the load latency)
+        asm volatile("" ::: "memory");
+        if (k + 1 >= nmax) break;
+        // block k + 1: segments k + 1 (b) and k + 2 (a)
+        if (k + 1 < my_nfull) load_seg(seg + 4 * (k + 2), a);
+        funnel_u(q, b, a, sel, w);
+        if (k + 1 < my_nfull) sha1_compress(h, w);
+        asm volatile("" ::: "memory");
+    }
+    return true;
+}
+
 // MODE 0: value i at base + i*stride, length L.  MODE 1: base + off[i], len[i].
 // perm (MODE 1 only, nullable): lane i hashes leaf perm[i] (length bucketing).
 // No tree level is fused here: a wave-level step costs a whole SHA-1
@@ -888,7 +1055,7 @@ __global__ __launch_bounds__(kBlock, (LOAD == 6 || LOAD == 7) ? 2 : ((LOAD == 4 
                                                   uint64_t L, const uint32_t* __restrict__ perm,
                                                   uint64_t n, uint8_t* __restrict__ nodes, Gate gate) {
     // 16 KiB: four wave-private 4 KiB LDS-DMA stages (LOAD 1, 8); 8 KiB each for LOAD 9, 5 KiB for LOAD 10
-    __shared__ __attribute__((aligned(16))) uint8_t smem[kBlock * (LOAD == 9 ? 128 : (LOAD == 10 ? 80 : 64))];
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kBlock * (LOAD == 9 ? 128 : (LOAD == 10 || LOAD == 11 ? 80 : 64))];
     if (!gate.open()) return;
     NKV_STAMP(0);
     const uint64_t g = blockIdx.x;
@@ -921,19 +1088,21 @@ __global__ __launch_bounds__(kBlock, (LOAD == 6 || LOAD == 7) ? 2 : ((LOAD == 4 
             else sha1_tail<true>(p, ln, h);
             store_digest(nodes, leaf, h);
         }
-    } else if (LOAD == 1 || LOAD == 8 || LOAD == 9 || LOAD == 10) {
+    } else if (LOAD == 1 || LOAD == 8 || LOAD == 9 || LOAD == 10 || LOAD == 11) {
         // wave-cooperative LDS-DMA stream of the full blocks, then the tail.
         // The DMA reads each value's own blocks at the value's address, so it
         // serves any alignment (LOAD 8: unaligned values, unaligned tail); only
         // full blocks are fetched, so every byte read belongs to the value.
         const int lane = threadIdx.x & 63;
         const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-        uint8_t* wbuf = smem + (LOAD == 9 ? 8192 : (LOAD == 10 ? 5120 : 4096)) * wave;
+        uint8_t* wbuf = smem + (LOAD == 9 ? 8192 : (LOAD == 10 || LOAD == 11 ? 5120 : 4096)) * wave;
         const uint32_t q = (uint32_t(lane) & 3u) ^ ((uint32_t(lane) >> 4) & 3u);
         const uint32_t my_nfull = live ? uint32_t(ln >> 6) : 0u;
         sha1_init(h);
         bool staged = false;
-        if constexpr (LOAD == 9 || LOAD == 10) staged = sha1_blocks_pair(LOAD == 10, wbuf, p, live, my_nfull, h);
+        if constexpr (LOAD == 11) staged = sha1_blocks_shift(wbuf, p, live, my_nfull, h);
+        if constexpr (LOAD == 9 || LOAD == 10 || LOAD == 11)
+            if (!staged) staged = sha1_blocks_pair(LOAD != 9, wbuf, p, live, my_nfull, h);
         if (staged) {
             // line-pair stage done (wave-uniform)
         } else if (MODE == 0) {
@@ -970,6 +1139,16 @@ __global__ __launch_bounds__(kBlock, (LOAD == 6 || LOAD == 7) ? 2 : ((LOAD == 4 
                         __builtin_amdgcn_global_load_lds(src[k] + 64ull * b, wbuf + 1024 * k, 16, 0, 0);
             };
             sha1_blocks_lds(wbuf, wave_max_u32(my_nfull), my_nfull, issue, h);
+        }
+        if constexpr (LOAD == 11 && MODE == 1) {
+            // reload the value's place instead of keeping it live through the
+            // register stage (its two 16-dword segment sets need the VGPRs)
+            asm volatile("" ::: "memory");
+            if (live) {
+                leaf = perm ? uint64_t(perm[t]) : t;
+                p = base + off[leaf];
+                ln = len[leaf];
+            }
         }
         if (live) {
             sha1_tail<LOAD == 1>(p, ln, h);
@@ -1502,6 +1681,7 @@ static void leaf_dispatch(int load, const uint8_t* base, const uint64_t* off, co
         case 8: leaf_kernel<MODE, 8>(base, off, len, stride, L, perm, n, nodes, s, g); break;
         case 9: leaf_kernel<MODE, 9>(base, off, len, stride, L, perm, n, nodes, s, g); break;
         case 10: leaf_kernel<MODE, 10>(base, off, len, stride, L, perm, n, nodes, s, g); break;
+        case 11: leaf_kernel<MODE, 11>(base, off, len, stride, L, perm, n, nodes, s, g); break;
         default: leaf_kernel<MODE, 0>(base, off, len, stride, L, perm, n, nodes, s, g); break;
     }
 }
@@ -1509,9 +1689,10 @@ static void leaf_dispatch(int load, const uint8_t* base, const uint64_t* off, co
 hipError_t launch_leaf_strided(const uint8_t* base, uint64_t stride, uint64_t L, uint64_t n, int load,
                                uint8_t* nodes, hipStream_t s) {
     const bool al = ((reinterpret_cast<uintptr_t>(base) | stride) & 15) == 0;
-    // LDS-DMA serves any alignment (direct loads need 16 B); the 80-byte window
-    // stage (LOAD 10) by default, the value-relative stream in its ragged waves
-    if (!al && load != 9 && load != 10) load = load == 1 ? 10 : 0;
+    // LDS-DMA serves any alignment (direct loads need 16 B).  Default: the
+    // segment stage (LOAD 11) for waves whose values share their offset mod 64,
+    // else the 80-byte window stage (LOAD 10), else the value-relative stream
+    if (!al && load != 9 && load != 10 && load != 11) load = load == 1 ? 11 : 0;
     leaf_dispatch<0>(load, base, nullptr, nullptr, stride, L, nullptr, n, nodes, s, Gate{});
     return hipGetLastError();
 }
@@ -1520,7 +1701,7 @@ hipError_t launch_leaf_offsets(const uint8_t* base, const uint64_t* off, const u
                                const uint32_t* perm, uint64_t n, bool aligned, int load, uint8_t* nodes,
                                hipStream_t s, bool deep, Gate gate) {
     if (perm && deep) load = aligned ? 6 : 7;  // ragged, length-sorted: deep prefetch
-    else if (!aligned && load != 9 && load != 10) load = load == 1 ? 10 : 0;  // as launch_leaf_strided
+    else if (!aligned && load != 9 && load != 10 && load != 11) load = load == 1 ? 11 : 0;  // as launch_leaf_strided
     leaf_dispatch<1>(load, base, off, len, 0, 0, perm, n, nodes, s, gate);
     return hipGetLastError();
 }

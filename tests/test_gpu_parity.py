@@ -393,7 +393,7 @@ def test_bucket_modes_narrow_and_wide(nkv, oracle, bucket, spread):
     assert np.array_equal(d_nodes.cpu().numpy().reshape(-1, 20), want)
 
 
-@pytest.mark.parametrize("load", [9, 10])
+@pytest.mark.parametrize("load", [9, 10, 11])
 @pytest.mark.parametrize("shift", [0, 1, 2, 15, 16, 17, 46, 48, 63])
 @pytest.mark.parametrize("n,vlen,rec", [(1, 4050, 4096), (63, 4050, 4096), (3001, 4050, 4096), (777, 327, 400),
                                         (300, 63, 128), (257, 64, 130), (130, 1024, 1100)])
@@ -425,7 +425,7 @@ def test_line_pair_stage_uniform(nkv, oracle, load, shift, n, vlen, rec):
     assert np.array_equal(d_nodes2.cpu().numpy().reshape(-1, 20), want)
 
 
-@pytest.mark.parametrize("load", [9, 10])
+@pytest.mark.parametrize("load", [9, 10, 11])
 @pytest.mark.parametrize("spread", [1, 64, 3000])
 def test_line_pair_stage_ragged_falls_back(nkv, oracle, load, spread):
     """LOAD 9 in input order over values whose full-block counts differ inside a wave: those waves take
@@ -446,6 +446,39 @@ def test_line_pair_stage_ragged_falls_back(nkv, oracle, load, spread):
     d_data, d_off, d_len = _dev(torch, data), _dev(torch, off), _dev(torch, lens)
     d_nodes = torch.zeros(L.nkv_total_nodes(n) * 20, dtype=torch.uint8, device="cuda")
     ctx.set_option(_lib.NKV_OPT_LEAF_LOAD, load)
+    ctx.set_option(_lib.NKV_OPT_BUCKET, 0)
+    try:
+        _lib.check(L.nkv_tree_from_values_dev(ctx.h, d_data.data_ptr(), d_off.data_ptr(), d_len.data_ptr(),
+                                              n, d_nodes.data_ptr()))
+        torch.cuda.synchronize()
+    finally:
+        ctx.set_option(_lib.NKV_OPT_LEAF_LOAD, 1)
+        ctx.set_option(_lib.NKV_OPT_BUCKET, 2)
+    assert np.array_equal(d_nodes.cpu().numpy().reshape(-1, 20), want)
+
+
+@pytest.mark.parametrize("shift", [1, 3, 4, 17, 46, 60, 63])
+@pytest.mark.parametrize("maxlen", [64, 130, 4050])
+def test_shift_stage_uniform_offset_ragged_lengths(nkv, oracle, shift, maxlen):
+    """NKV_OPT_LEAF_LOAD 11 (register stage of aligned 64-B segments, wave-uniform
+    misalignment): one record size, so every value sits at the same offset mod 64,
+    but the lengths differ (0 .. maxlen), so lanes of a wave stop at different
+    blocks; the last value ends exactly at the end of the buffer."""
+    torch = _torch()
+    _lib, ctx = nkv
+    _bind(torch, ctx)
+    L = _lib.lib()
+    rng = np.random.default_rng(shift * 1000 + maxlen)
+    n, rec = 2000, 64 * ((maxlen + 63) // 64 + 1)
+    off = (np.arange(n, dtype=np.uint64) * rec + shift).astype(np.uint64)
+    lens = rng.integers(0, maxlen + 1, n).astype(np.uint64)
+    lens[:64] = maxlen  # one wave of equal lengths
+    lens[-1] = maxlen
+    data = oracle.splitmix64_bytes(int(off[-1] + lens[-1]), SEED + shift)
+    want = oracle.tree_from_digests(oracle.leaf_hashes(data, off, lens, threads=8))
+    d_data, d_off, d_len = _dev(torch, data), _dev(torch, off), _dev(torch, lens)
+    d_nodes = torch.zeros(L.nkv_total_nodes(n) * 20, dtype=torch.uint8, device="cuda")
+    ctx.set_option(_lib.NKV_OPT_LEAF_LOAD, 11)
     ctx.set_option(_lib.NKV_OPT_BUCKET, 0)
     try:
         _lib.check(L.nkv_tree_from_values_dev(ctx.h, d_data.data_ptr(), d_off.data_ptr(), d_len.data_ptr(),
