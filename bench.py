@@ -75,6 +75,7 @@ def parse():
     ap.add_argument("--queue-split", type=int, default=-1, help="NKV_OPT_QUEUE_SPLIT override")
     ap.add_argument("--queue-waves", type=int, default=0, help="NKV_OPT_QUEUE_WAVES override")
     ap.add_argument("--queue-ring", type=int, default=0, help="NKV_OPT_QUEUE_RING override (2, 3, 4)")
+    ap.add_argument("--records-fused", type=int, default=-1, help="NKV_OPT_RECORDS_FUSED override (0, 1)")
     ap.add_argument("--leaves", type=int, default=1 << 20)
     ap.add_argument("--key-bytes", type=int, default=16, help="records configs: KeySize (the Value starts at +30+key)")
     ap.add_argument("--value-bytes", type=int, default=4096)
@@ -197,6 +198,8 @@ def main():
         ctx.set_option(_lib.NKV_OPT_QUEUE_WAVES, args.queue_waves)
     if args.queue_ring:
         ctx.set_option(_lib.NKV_OPT_QUEUE_RING, args.queue_ring)
+    if args.records_fused >= 0:
+        ctx.set_option(_lib.NKV_OPT_RECORDS_FUSED, args.records_fused)
     if args.no_bucket:
         ctx.set_option(_lib.NKV_OPT_BUCKET, 0)
     elif args.bucket >= 0:

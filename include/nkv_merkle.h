@@ -139,6 +139,9 @@ int nkv_ctx_sync(nkv_ctx *ctx);
                                   ring of value-relative chunks (no funnel) with 2 / 3 / 4
                                   slots (default 13).  3 and 13 allow 3 waves per SIMD, 4
                                   and 14 two */
+#define NKV_OPT_RECORDS_FUSED 11 /* records form (nkv_tree_from_records*): 1 (default) = one
+                                    launch locates each value from its header and hashes it
+                                    (k_leaf_records); 0 = a separate locate pass first */
 int nkv_ctx_set_option(nkv_ctx *ctx, int key, int64_t value);
 /* When enabled, the device-resident tree calls record HIP events around the
  * leaf kernel and the tree reduce on the context's stream. */

@@ -30,6 +30,7 @@ NKV_OPT_HOST_THREADS = 7
 NKV_OPT_STAGE_CHUNK = 8
 NKV_OPT_QUEUE_RING = 9
 NKV_OPT_BLOOM_PATH = 10
+NKV_OPT_RECORDS_FUSED = 11
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)
 _u64p = ctypes.POINTER(ctypes.c_uint64)

@@ -106,6 +106,7 @@ struct nkv_ctx {
     int queue_ring = 13;    // NKV_OPT_QUEUE_RING
     int bloom_path = 2;     // NKV_OPT_BLOOM_PATH
     int crc_load = 1;       // NKV_OPT_CRC_LOAD
+    int records_fused = 1;  // NKV_OPT_RECORDS_FUSED
     bool timing = false;
     bool timed = false;
     // per-call event triples (leaf start, leaf end / reduce start, reduce end),
@@ -114,7 +115,7 @@ struct nkv_ctx {
     std::vector<hipEvent_t> ring;
     size_t ring_used = 0;
     DevBuf d_data, d_off, d_len, d_nodes, d_img, d_tmp, d_err, d_aux, d_keys, d_perm, d_stmp, d_queue, d_stats,
-        d_range, d_sync, d_part;
+        d_range, d_sync, d_part, d_tmp2;
     void* h_stage = nullptr;  // small pinned staging (offsets, lengths, stats)
     unsigned int* h_small = nullptr;  // 64 pinned bytes for device-to-host decisions
     size_t h_cap = 0;
@@ -375,6 +376,42 @@ int tree_from_device_values(nkv_ctx* c, const uint8_t* base, const uint64_t* off
     return mark(c, 2);
 }
 
+// The Merkle step of a device-resident Data table: one k_leaf_records launch
+// locates every record's value and hashes it in input order -- all of them
+// (NKV_OPT_BUCKET 0), or (auto) the waves whose block counts are narrow, the
+// others deferred -- then the length-sorted work queue takes what was deferred
+// (behind a device Gate: on a table of one record size it is never opened),
+// then the levels.  err (device u32) = 1 if a header points outside the stream.
+int records_tree(nkv_ctx* c, const uint8_t* stream, uint64_t stream_len, const uint64_t* rec_off, uint64_t n,
+                 uint8_t* nodes, unsigned int* err) {
+    TRY(grow(c->d_off, 8 * n));
+    TRY(grow(c->d_len, 8 * n));
+    TRY(grow(c->d_range, 8));
+    uint64_t* voff = static_cast<uint64_t*>(c->d_off.p);
+    uint64_t* vlen = static_cast<uint64_t*>(c->d_len.p);
+    unsigned int* range = static_cast<unsigned int*>(c->d_range.p);
+    uint32_t* part = nullptr;
+    TRY(locate_parts(c, n, &part));
+    if (!c->records_fused) {  // NKV_OPT_RECORDS_FUSED 0: separate locate pass, then the leaf plan
+        const bool gated = c->bucket == 2 && n >= 4096;
+        HIPTRY(launch_locate(stream, stream_len, rec_off, n, voff, vlen, err, gated ? range : nullptr, part,
+                             c->stream));
+        return tree_from_device_values(c, stream, voff, vlen, n, false, nodes, nullptr, gated ? range : nullptr);
+    }
+    // plan_of's rule: input order without bucketing or for tiny batches; auto
+    // for >= 4096 values; else everything sorted
+    const int policy = (c->bucket == 0 || n <= 64) ? 0 : ((c->bucket == 2 && n >= 4096) ? 1 : 2);
+    TRY(mark(c, 0));
+    HIPTRY(launch_leaf_records(stream, stream_len, rec_off, n, policy, voff, vlen, nodes, err, range, part,
+                               c->stream));
+    if (policy != 0)
+        TRY(leaf_level(c, stream, voff, vlen, n, false, nodes, policy == 2 ? kSorted : kGated, Gate{range, 0},
+                       false));
+    TRY(mark(c, 1));
+    HIPTRY(launch_reduce(nodes, n, 0, levels_of(n) - 1, c->stream));
+    return mark(c, 2);
+}
+
 }  // namespace
 
 #ifndef NKV_SRC_HASH
@@ -444,7 +481,7 @@ void nkv_ctx_destroy(nkv_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (DevBuf* b : {&c->d_data, &c->d_off, &c->d_len, &c->d_nodes, &c->d_img, &c->d_tmp,
                       &c->d_err, &c->d_aux, &c->d_keys, &c->d_perm, &c->d_stmp, &c->d_queue, &c->d_stats,
-                      &c->d_range, &c->d_sync, &c->d_part})
+                      &c->d_range, &c->d_sync, &c->d_part, &c->d_tmp2})
         if (b->p) (void)hipFree(b->p);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
     if (c->h_small) (void)hipHostFree(c->h_small);
@@ -504,6 +541,10 @@ int nkv_ctx_set_option(nkv_ctx* c, int key, int64_t value) {
             if (value < 4096 || value > (int64_t(1) << 32) || (value & 4095)) return NKV_ERR_INVALID;
             if (c->stage.drain() != hipSuccess) return NKV_ERR_DEVICE;
             c->stage.chunk = size_t(value);
+            return NKV_OK;
+        case NKV_OPT_RECORDS_FUSED:
+            if (value < 0 || value > 1) return NKV_ERR_INVALID;
+            c->records_fused = int(value);
             return NKV_OK;
         case NKV_OPT_QUEUE_WAVES:
             if (value < 1 || value > 5) return NKV_ERR_INVALID;  // 8 KiB LDS per wave: <= 20 per CU
@@ -743,19 +784,19 @@ int nkv_tree_from_records(nkv_ctx* c, const uint8_t* stream, uint64_t stream_len
     if (!stream || !rec_size) return NKV_ERR_INVALID;
     if (!records_fit(rec_size, n, stream_len)) return NKV_ERR_INVALID;
     TRY(stage_stream(c, stream, stream_len, c->d_data, rec_size, n, c->d_aux));
-    TRY(grow(c->d_off, 8 * n));
-    TRY(grow(c->d_len, 8 * n));
-    // d_len doubles as the record-offset scratch before it receives lengths
-    uint64_t* rec_off = static_cast<uint64_t*>(c->d_len.p);
+    // record offsets in their own scratch (records_tree uses d_off / d_len)
+    TRY(grow(c->d_tmp2, 8 * n));
+    uint64_t* rec_off = static_cast<uint64_t*>(c->d_tmp2.p);
     TRY(nkv_record_offsets_dev(c, static_cast<const uint64_t*>(c->d_aux.p), n, rec_off));
-    // values land in d_off (offsets) and d_aux (lengths; RecSize no longer needed)
-    uint64_t* voff = static_cast<uint64_t*>(c->d_off.p);
-    uint64_t* vlen = static_cast<uint64_t*>(c->d_aux.p);
-    TRY(nkv_locate_values_dev(c, c->d_data.p, stream_len, rec_off, n, voff, vlen));
     TRY(grow(c->d_nodes, 20 * total_of(n)));
     uint8_t* nodes = static_cast<uint8_t*>(c->d_nodes.p);
-    TRY(tree_from_device_values(c, static_cast<const uint8_t*>(c->d_data.p), voff, vlen, n, false,
-                                nodes));
+    TRY(grow(c->d_err, 4));
+    unsigned int* err = static_cast<unsigned int*>(c->d_err.p);
+    TRY(records_tree(c, static_cast<const uint8_t*>(c->d_data.p), stream_len, rec_off, n, nodes, err));
+    unsigned int h = 0;
+    HIPTRY(hipMemcpyAsync(&h, err, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPTRY(hipStreamSynchronize(c->stream));
+    if (h) return NKV_ERR_INVALID;
     return finish_tree(c, nodes, n, root20, nodes_out, img_out);
 }
 
@@ -955,25 +996,13 @@ int nkv_tree_from_records_dev(nkv_ctx* c, const void* d_stream, uint64_t stream_
     TRY(bind(c));
     if (n == 0) return NKV_ERR_EMPTY;
     if (!d_stream || !d_rec_off || !d_nodes) return NKV_ERR_INVALID;
-    TRY(grow(c->d_off, 8 * n));
-    TRY(grow(c->d_len, 8 * n));
     unsigned int* err = reinterpret_cast<unsigned int*>(d_err);
     if (!err) {
         TRY(grow(c->d_err, 4));
         err = static_cast<unsigned int*>(c->d_err.p);
     }
-    uint64_t* voff = static_cast<uint64_t*>(c->d_off.p);
-    uint64_t* vlen = static_cast<uint64_t*>(c->d_len.p);
-    // the locate pass also measures the range the order choice needs
-    const bool gated = c->bucket == 2 && n >= 4096;
-    if (gated) TRY(grow(c->d_range, 8));
-    unsigned int* range = gated ? static_cast<unsigned int*>(c->d_range.p) : nullptr;
-    uint32_t* part = nullptr;
-    TRY(locate_parts(c, n, &part));
-    HIPTRY(launch_locate(static_cast<const uint8_t*>(d_stream), stream_len, d_rec_off, n, voff, vlen, err, range,
-                         part, c->stream));
-    TRY(tree_from_device_values(c, static_cast<const uint8_t*>(d_stream), voff, vlen, n, false,
-                                static_cast<uint8_t*>(d_nodes), nullptr, range));
+    TRY(records_tree(c, static_cast<const uint8_t*>(d_stream), stream_len, d_rec_off, n,
+                     static_cast<uint8_t*>(d_nodes), err));
     if (d_err) return NKV_OK;
     unsigned int h = 0;
     HIPTRY(hipMemcpyAsync(&h, err, 4, hipMemcpyDeviceToHost, c->stream));

@@ -95,6 +95,14 @@ uint64_t locate_part_words(uint64_t n);
 hipError_t launch_locate(const uint8_t* stream, uint64_t stream_len, const uint64_t* rec_off,
                          uint64_t n, uint64_t* voff, uint64_t* vlen, unsigned int* err, unsigned int* range,
                          uint32_t* part, hipStream_t s);
+// The records form's leaf pass (k_leaf_records): locate each record's value and
+// hash it in input order (policy 0), only in waves of narrow block counts (1,
+// the rest deferred to the length-sorted pass), or never (2); voff / vlen
+// receive the deferred values' places (kDone for hashed ones); err / range /
+// part as launch_locate, range opening the wide Gate iff something was deferred.
+hipError_t launch_leaf_records(const uint8_t* stream, uint64_t stream_len, const uint64_t* rec_off, uint64_t n,
+                               int policy, uint64_t* voff, uint64_t* vlen, uint8_t* nodes, unsigned int* err,
+                               unsigned int* range, uint32_t* part, hipStream_t s);
 hipError_t scan_exclusive_u64(const uint64_t* in, uint64_t* out, uint64_t n, void* tmp,
                               size_t* tmp_bytes, hipStream_t s);
 // In-place exclusive scan of n u32 (gated); sums: scan_sums_words(n) u32.

@@ -60,9 +60,12 @@ __device__ __forceinline__ uint64_t ld_le64(const uint8_t* p) {
 // not 8-byte aligned; it then holds byte 29, so every load stays inside an
 // aligned word that holds a header byte (no page can be crossed).
 __device__ __forceinline__ void ld_header_sizes(const uint8_t* p, uint64_t& ks, uint64_t& vs) {
-    const uintptr_t a = reinterpret_cast<uintptr_t>(p + 14);
-    const uint64_t* q = reinterpret_cast<const uint64_t*>(a & ~uintptr_t(7));
-    const uint32_t sh = uint32_t(a & 7u) * 8u;
+    // pointer arithmetic on p (not an integer-to-pointer cast) keeps the global
+    // address space: global_load, not flat_load
+    const uint8_t* f = p + 14;
+    const uint32_t mis = uint32_t(reinterpret_cast<uintptr_t>(f) & 7u);
+    const uint64_t* q = reinterpret_cast<const uint64_t*>(f - mis);
+    const uint32_t sh = mis * 8u;
     const uint64_t q0 = q[0], q1 = q[1];
     const uint64_t q2 = sh ? q[2] : 0ull;
     ks = sh ? (q0 >> sh) | (q1 << (64u - sh)) : q0;
@@ -131,6 +134,10 @@ __device__ __forceinline__ bool grid_fold(SyncSlot* slot, uint32_t lo, uint32_t 
 
 // SHA-1 compressions of a len-byte message (FIPS 180-4 padding: + 0x80 + 8 B)
 __device__ __forceinline__ uint64_t compressions(uint64_t len) { return (len + 8) / 64 + 1; }
+
+// Value offset of a record k_leaf_records already hashed (the length-sorted
+// pass that follows it skips the value).
+constexpr uint64_t kDone = ~uint64_t(0);
 
 // CRC tables for k_leaf_verify (crc.hip keeps its own copy: no relocatable
 // device code, so each translation unit defines its constants)
@@ -382,10 +389,20 @@ __device__ __forceinline__ void sha1_tail(const uint8_t* p, uint64_t len, uint32
 //
 // src[k] = chunk address of block 0 for this lane's DMA role k; nf[k] = full
 // blocks of that value (0 for a dead lane).  my_nfull: this lane's own value.
+// Wave reductions by ds_swizzle (xor pattern in the instruction, within each
+// 32-lane half) and two readlanes: no lane-index VGPRs, which __shfl_xor
+// computes once and the compiler then keeps live through a whole kernel.
+template <int X>
+__device__ __forceinline__ uint32_t swz_xor(uint32_t v) {
+    return uint32_t(__builtin_amdgcn_ds_swizzle(int(v), (X << 10) | 0x1F));
+}
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = max(v, uint32_t(__shfl_xor(int(v), o)));
-    return __builtin_amdgcn_readfirstlane(v);
+    v = max(v, swz_xor<1>(v));
+    v = max(v, swz_xor<2>(v));
+    v = max(v, swz_xor<4>(v));
+    v = max(v, swz_xor<8>(v));
+    v = max(v, swz_xor<16>(v));
+    return max(uint32_t(__builtin_amdgcn_readlane(int(v), 0)), uint32_t(__builtin_amdgcn_readlane(int(v), 32)));
 }
 
 // issue(b) starts the four DMA instructions of block b (each lane for its DMA
@@ -800,15 +817,22 @@ __device__ __forceinline__ void sha1_blocks_ring_vc(uint8_t* wbuf, const uint8_t
 // of the wave to have the same full-block count and the wave's pairs to lie
 // within 4 GiB of the base.  Otherwise it returns false and does nothing (the
 // caller runs the LOAD 8 stream).  Stage: 8 KiB per wave.
+template <int X>
+__device__ __forceinline__ uint64_t min_swz64(uint64_t v) {
+    const uint64_t u = (uint64_t(swz_xor<X>(uint32_t(v >> 32))) << 32) | swz_xor<X>(uint32_t(v));
+    return u < v ? u : v;
+}
 __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const uint64_t u = uint64_t(__shfl_xor(static_cast<long long>(v), o));
-        v = u < v ? u : v;
-    }
-    const uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(v));
-    const uint32_t hi = __builtin_amdgcn_readfirstlane(uint32_t(v >> 32));
-    return (uint64_t(hi) << 32) | lo;
+    v = min_swz64<1>(v);
+    v = min_swz64<2>(v);
+    v = min_swz64<4>(v);
+    v = min_swz64<8>(v);
+    v = min_swz64<16>(v);
+    const uint64_t a = (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(uint32_t(v >> 32)), 0))) << 32) |
+                       uint32_t(__builtin_amdgcn_readlane(int(uint32_t(v)), 0));
+    const uint64_t b = (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(uint32_t(v >> 32)), 32))) << 32) |
+                       uint32_t(__builtin_amdgcn_readlane(int(uint32_t(v)), 32));
+    return a < b ? a : b;
 }
 
 // kWindow (LOAD 10): the same stream with only each value's 80-byte window row
@@ -998,16 +1022,23 @@ __device__ __forceinline__ bool sha1_blocks_shift(uint8_t* wbuf, const uint8_t* 
             issue(0u);
             take(a);
             issue(1u);
+            // sched_barrier: no instruction crosses a phase boundary, so the
+            // scheduler cannot overlap one block's compression with the next
+            // block's reads and funnel (two windows live at 64 VGPRs spill)
             for (uint32_t k = 0; k < nmax; k += 2) {
                 take(b);  // segment k + 1
                 if (k + 2 <= nmax) issue(k + 2);
                 funnel_u(q, a, b, sel, w);
+                __builtin_amdgcn_sched_barrier(0);
                 if (live) sha1_compress(h, w);
+                __builtin_amdgcn_sched_barrier(0);
                 if (k + 1 >= nmax) break;
                 take(a);  // segment k + 2
                 if (k + 3 <= nmax) issue(k + 3);
                 funnel_u(q, b, a, sel, w);
+                __builtin_amdgcn_sched_barrier(0);
                 if (live) sha1_compress(h, w);
+                __builtin_amdgcn_sched_barrier(0);
             }
             return true;
         }
@@ -1039,6 +1070,42 @@ __device__ __forceinline__ bool sha1_blocks_shift(uint8_t* wbuf, const uint8_t* 
     return true;
 }
 
+// The full blocks of a wave's 64 values at any addresses (wbuf: the wave's
+// 5 KiB of LDS): the segment stage when the values share their offset mod 64,
+// else the 80-byte window stage when their full-block counts are equal, else
+// the value-relative stream.  k_leaf's LOAD 11 for MODE 1 and k_leaf_records.
+__device__ __forceinline__ void sha1_blocks_any(uint8_t* wbuf, const uint8_t* p, bool live, uint32_t my_nfull,
+                                                uint32_t h[5]) {
+    if (sha1_blocks_shift(wbuf, p, live, my_nfull, h)) return;
+    if (sha1_blocks_pair(true, wbuf, p, live, my_nfull, h)) return;
+    const int lane = threadIdx.x & 63;
+    const uint32_t q = (uint32_t(lane) & 3u) ^ ((uint32_t(lane) >> 4) & 3u);
+    const uint8_t* src[4];
+    uint32_t nf[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int j = 16 * k + (lane >> 2);
+        const uint64_t pj = uint64_t(__shfl(int64_t(reinterpret_cast<uintptr_t>(p)), j));
+        src[k] = reinterpret_cast<const uint8_t*>(pj) + 16 * q;
+        nf[k] = uint32_t(__shfl(int(my_nfull), j));
+    }
+    auto issue = [&](uint32_t b) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (b < nf[k]) __builtin_amdgcn_global_load_lds(src[k] + 64ull * b, wbuf + 1024 * k, 16, 0, 0);
+    };
+    sha1_blocks_lds(wbuf, wave_max_u32(my_nfull), my_nfull, issue, h);
+}
+
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+    v = min(v, swz_xor<1>(v));
+    v = min(v, swz_xor<2>(v));
+    v = min(v, swz_xor<4>(v));
+    v = min(v, swz_xor<8>(v));
+    v = min(v, swz_xor<16>(v));
+    return min(uint32_t(__builtin_amdgcn_readlane(int(v), 0)), uint32_t(__builtin_amdgcn_readlane(int(v), 32)));
+}
+
 // MODE 0: value i at base + i*stride, length L.  MODE 1: base + off[i], len[i].
 // perm (MODE 1 only, nullable): lane i hashes leaf perm[i] (length bucketing).
 // No tree level is fused here: a wave-level step costs a whole SHA-1
@@ -1061,8 +1128,9 @@ __global__ __launch_bounds__(kBlock, (LOAD == 6 || LOAD == 7) ? 2 : ((LOAD == 4 
     const uint64_t g = blockIdx.x;
     const uint64_t t = g * kBlock + threadIdx.x;
     uint32_t h[5] = {0u, 0u, 0u, 0u, 0u};
-    const bool live = t < n;
     uint64_t leaf = t;
+    // a length-sorted batch after k_leaf_records skips the values it hashed
+    const bool live = t < n && (MODE == 0 || !perm || off[perm[t]] != kDone);
     const uint8_t* p = nullptr;
     uint64_t ln = 0;
     if (live) {
@@ -1341,9 +1409,10 @@ __global__ __launch_bounds__(64, queue_ring_slots<LOAD>() == 4 ? 2 : (queue_ring
         if (g == 0xFFFFFFFFu) break;
         const uint64_t i = uint64_t(g) * 64 + lane;
         if constexpr (LOAD >= 8) {
-            const bool live = i < n;
-            const uint64_t leaf = live ? perm[i] : 0;
-            const uint8_t* p = live ? base + off[leaf] : base;
+            const uint64_t leaf = i < n ? perm[i] : 0;
+            const uint64_t vo = i < n ? off[leaf] : kDone;
+            const bool live = vo != kDone;  // kDone: hashed by k_leaf_records
+            const uint8_t* p = live ? base + vo : base;
             const uint64_t ln = live ? len[leaf] : 0;
             uint32_t h[5];
             sha1_init(h);
@@ -1354,7 +1423,7 @@ __global__ __launch_bounds__(64, queue_ring_slots<LOAD>() == 4 ? 2 : (queue_ring
                 sha1_tail<false>(p, ln, h);
                 store_digest(nodes, leaf, h);
             }
-        } else if (i < n) {
+        } else if (i < n && off[perm[i]] != kDone) {
             const uint64_t leaf = perm[i];
             const uint8_t* p = base + off[leaf];
             const uint64_t ln = len[leaf];
@@ -1585,10 +1654,15 @@ __global__ __launch_bounds__(kBlock) void k_locate_fold(const uint32_t* __restri
                                                          unsigned int* __restrict__ range) {
     uint32_t lo = 0xFFFFFFFFu, hi = 0u, bad = 0u;
     unsigned long long none = 0;
-    for (uint32_t b = threadIdx.x; b < nb; b += kBlock) {
-        lo = min(lo, part[3 * b]);
-        hi = max(hi, part[3 * b + 1]);
-        bad |= part[3 * b + 2];
+    // coalesced, independent loads over the flat triples (one per workgroup)
+    const uint32_t words = 3u * nb;
+#pragma unroll 8
+    for (uint32_t x = threadIdx.x; x < words; x += kBlock) {
+        const uint32_t v = part[x];
+        const uint32_t kind = x % 3u;
+        if (kind == 0u) lo = min(lo, v);
+        else if (kind == 1u) hi = max(hi, v);
+        else bad |= v;
     }
     block_fold(lo, hi, bad, none);
     if (threadIdx.x == 0) {
@@ -1597,6 +1671,91 @@ __global__ __launch_bounds__(kBlock) void k_locate_fold(const uint32_t* __restri
             range[0] = lo;
             range[1] = hi;
         }
+    }
+}
+
+// K1r: the records form's leaf pass in one launch (nkv_tree_from_records*):
+// k_locate's header parse (value = rec + 30 + KeySize, ValueSize bytes;
+// record.go:191-199) and k_leaf's hash of the value, so the header line is
+// read once and no separate locate pass runs.  policy 0 hashes every wave in
+// input order; 1 (auto) hashes the waves whose full-block counts are narrow
+// by the plan rule (max <= min + max(1, min / 16), Gate) and defers the others
+// to the length-sorted work queue; 2 defers all.  A hashed value's voff is
+// set to kDone (vlen 0): the sorted pass skips it.  A deferred value keeps its
+// voff / vlen.  Each workgroup leaves (0, deferred ? ~0 : 0, bad) in part,
+// which k_locate_fold turns into err and a range whose wide Gate opens the
+// sorted pass only when something was deferred.  A header outside the
+// stream flags bad and hashes the empty value (as k_locate).
+__global__ __launch_bounds__(kBlock, kLeafWavesPerSimd) void k_leaf_records(
+    const uint8_t* __restrict__ stream, uint64_t stream_len, const uint64_t* __restrict__ rec_off, uint64_t n,
+    int policy, uint64_t* __restrict__ voff, uint64_t* __restrict__ vlen, uint8_t* __restrict__ nodes,
+    uint32_t* __restrict__ part) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kBlock * 80];
+    const uint64_t t = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
+    const bool live = t < n;
+    uint64_t o = 0, l = 0;
+    uint32_t bad = 0u;
+    if (live) {
+        const uint64_t r = rec_off[t];
+        if (header_in(r, stream_len)) {
+            uint64_t ks, vs;
+            ld_header_sizes(stream + r, ks, vs);
+            o = r + 30 + ks;
+            l = vs;
+            if (ks > stream_len || vs > stream_len || o + l > stream_len) {
+                bad = 1u;
+                o = 0;
+                l = 0;
+            }
+        } else {
+            bad = 1u;
+        }
+        voff[t] = o;
+        vlen[t] = l;
+    }
+    const uint64_t bl = l >> 6;
+    const uint32_t b32 = bl > 0xFFFFFFFFull ? 0xFFFFFFFFu : uint32_t(bl);
+    const uint32_t wlo = wave_min_u32(live ? b32 : 0xFFFFFFFFu);
+    const uint32_t whi = wave_max_u32(live ? b32 : 0u);
+    const bool any = __any(live);
+    const bool hash = any && (policy == 0 || (policy == 1 && whi <= wlo + max(1u, wlo / 16u)));
+    // wave-level partials, so no per-lane flag stays live through the stage
+    const bool wbad = __any(bad != 0u);
+    const bool wdefer = any && !hash;
+    if (hash) {
+        const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        uint32_t h[5];
+        sha1_init(h);
+        sha1_blocks_any(smem + 5120 * wave, stream + o, live, live ? b32 : 0u, h);
+        // reload the value's place (written above by this lane) rather than
+        // keeping it, or its addresses, live through the stage
+        asm volatile("" ::: "memory");
+        uint32_t tid = threadIdx.x;
+        asm volatile("" : "+v"(tid));
+        const uint64_t u = uint64_t(blockIdx.x) * kBlock + tid;
+        if (u < n) {
+            o = voff[u];
+            l = vlen[u];
+            sha1_tail<false>(stream + o, l, h);
+            store_digest(nodes, u, h);
+            voff[u] = kDone;
+            vlen[u] = 0;
+        }
+    }
+    // one partial per workgroup, folded through the (now idle) stage LDS: a
+    // block_fold of its own would cost LDS, i.e. a workgroup per CU
+    const int wv = threadIdx.x >> 6;
+    uint32_t* flags = reinterpret_cast<uint32_t*>(smem);
+    __syncthreads();  // every wave is done with its stage
+    if ((threadIdx.x & 63) == 0) flags[wv] = (wdefer ? 2u : 0u) | (wbad ? 1u : 0u);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t f = 0u;
+#pragma unroll
+        for (int k = 0; k < kBlock / 64; ++k) f |= flags[k];
+        part[3 * blockIdx.x] = 0u;
+        part[3 * blockIdx.x + 1] = (f & 2u) ? 0xFFFFFFFFu : 0u;
+        part[3 * blockIdx.x + 2] = f & 1u;
     }
 }
 
@@ -1808,6 +1967,7 @@ hipError_t launch_bfs_image(const uint8_t* nodes, const BfsLayout& lay, uint8_t*
     return hipGetLastError();
 }
 
+// one (lo, hi, flag) triple per workgroup (k_locate, k_leaf_records)
 uint64_t locate_part_words(uint64_t n) { return 3 * uint64_t(grid_for(n)); }
 
 hipError_t launch_locate(const uint8_t* stream, uint64_t stream_len, const uint64_t* rec_off,
@@ -1815,6 +1975,16 @@ hipError_t launch_locate(const uint8_t* stream, uint64_t stream_len, const uint6
                          uint32_t* part, hipStream_t s) {
     const unsigned nb = grid_for(n);
     hipLaunchKernelGGL(k_locate, dim3(nb), dim3(kBlock), 0, s, stream, stream_len, rec_off, n, voff, vlen, part);
+    hipLaunchKernelGGL(k_locate_fold, dim3(1), dim3(kBlock), 0, s, part, nb, err, range);
+    return hipGetLastError();
+}
+
+hipError_t launch_leaf_records(const uint8_t* stream, uint64_t stream_len, const uint64_t* rec_off, uint64_t n,
+                               int policy, uint64_t* voff, uint64_t* vlen, uint8_t* nodes, unsigned int* err,
+                               unsigned int* range, uint32_t* part, hipStream_t s) {
+    const unsigned nb = grid_for(n);
+    hipLaunchKernelGGL(k_leaf_records, dim3(nb), dim3(kBlock), 0, s, stream, stream_len, rec_off, n, policy, voff,
+                       vlen, nodes, part);
     hipLaunchKernelGGL(k_locate_fold, dim3(1), dim3(kBlock), 0, s, part, nb, err, range);
     return hipGetLastError();
 }
