@@ -405,6 +405,33 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
     return max(uint32_t(__builtin_amdgcn_readlane(int(v), 0)), uint32_t(__builtin_amdgcn_readlane(int(v), 32)));
 }
 
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+    v = min(v, swz_xor<1>(v));
+    v = min(v, swz_xor<2>(v));
+    v = min(v, swz_xor<4>(v));
+    v = min(v, swz_xor<8>(v));
+    v = min(v, swz_xor<16>(v));
+    return min(uint32_t(__builtin_amdgcn_readlane(int(v), 0)), uint32_t(__builtin_amdgcn_readlane(int(v), 32)));
+}
+
+template <int X>
+__device__ __forceinline__ uint64_t min_swz64(uint64_t v) {
+    const uint64_t u = (uint64_t(swz_xor<X>(uint32_t(v >> 32))) << 32) | swz_xor<X>(uint32_t(v));
+    return u < v ? u : v;
+}
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+    v = min_swz64<1>(v);
+    v = min_swz64<2>(v);
+    v = min_swz64<4>(v);
+    v = min_swz64<8>(v);
+    v = min_swz64<16>(v);
+    const uint64_t a = (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(uint32_t(v >> 32)), 0))) << 32) |
+                       uint32_t(__builtin_amdgcn_readlane(int(uint32_t(v)), 0));
+    const uint64_t b = (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(uint32_t(v >> 32)), 32))) << 32) |
+                       uint32_t(__builtin_amdgcn_readlane(int(uint32_t(v)), 32));
+    return a < b ? a : b;
+}
+
 // issue(b) starts the four DMA instructions of block b (each lane for its DMA
 // role); nmax = the wave's largest full-block count (wave-uniform).  raw(c)
 // sees each of this lane's blocks as loaded (four little-endian quads) before
@@ -622,6 +649,12 @@ __device__ __forceinline__ u32x4 ds_read_b128_asm(uint32_t addr) {
     asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr) : "memory");
     return v;
 }
+template <int OFF>
+__device__ __forceinline__ u32x4 ds_read_b128_off(uint32_t addr) {
+    u32x4 v;
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF) : "memory");
+    return v;
+}
 
 // The ring above with R >= 3 slots and explicit waits, software-pipelined:
 // while block b is compressed, the DMA of chunk b+R and the LDS reads of window
@@ -734,7 +767,7 @@ __device__ __forceinline__ void wait_vmcnt() {
 // so the LDS row already holds block c and no funnel is needed (16 v_perm
 // byte swaps per block instead of 52).  Only full blocks are fetched, so every
 // byte read belongs to the value.  A lane past its value's last block re-reads
-// that block (a value with none reads g_ring_dummy), so each issue is four
+// that block (a value with none re-reads another of the wave), so each issue is four
 // wave-instructions.  Window b = chunk b; at block b the ring holds chunks
 // b+1 .. b+R, and vmcnt(4 (R-1)) before reading window b+1 lets chunks
 // b+2 .. b+R fly (R-1 blocks of lookahead).
@@ -743,35 +776,75 @@ __device__ __forceinline__ void sha1_blocks_ring_vc(uint8_t* wbuf, const uint8_t
                                                     uint32_t h[5]) {
     static_assert(R >= 2 && R <= 4, "ring depth");
     const int lane = threadIdx.x & 63;
-    const uint32_t dq = (uint32_t(lane) & 3u) ^ ((uint32_t(lane) >> 4) & 3u);
-    const uint8_t* src[4];
-    uint32_t lastoff[4];  // byte offset of the role value's last full block (< 4 GiB)
+    // DMA role k of this lane: chunk (lane & 3) of value 16 k + (lane >> 2),
+    // which lands at wbuf + 1024 k + 16 lane = row 64 j + 16 (lane & 3): rows
+    // unswizzled, so a lane reads its window at one base + immediate offsets
+    // (the 4-way bank conflicts cost LDS cycles the VALU-bound loop has spare)
+    const uint32_t dq = uint32_t(lane) & 3u;
+    const uint32_t nmax = wave_max_u32(my_nfull);
+    if (nmax == 0) return;
+    // wave base: the lowest value address among lanes with a full block
+    const uint64_t pa = reinterpret_cast<uintptr_t>(p);
+    const uint64_t wb = wave_min_u64(my_nfull ? pa : ~uint64_t(0));
+    const uint32_t minfull = wave_min_u32(my_nfull ? my_nfull : 0xFFFFFFFFu);
+    const uint32_t wb_nfull = wave_max_u32(my_nfull && pa == wb ? my_nfull : 0u);
+    uint64_t relk[4];
+    uint32_t lastk[4];  // byte offset of the role value's last full block
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int j = 16 * k + (lane >> 2);
-        const uint64_t aj = uint64_t(__shfl(int64_t(reinterpret_cast<uintptr_t>(p)), j));
+        const uint64_t aj = uint64_t(__shfl(int64_t(pa), j));
         const uint32_t nj = uint32_t(__shfl(int(my_nfull), j));
-        src[k] = (nj ? reinterpret_cast<const uint8_t*>(aj) : g_ring_dummy) + 16 * dq;
-        lastoff[k] = nj ? 64u * (nj - 1) : 0u;
+        // a role whose value has no full block re-reads the wave base's value
+        relk[k] = (nj ? aj - wb : 0ull) + 16u * dq;
+        lastk[k] = 64u * ((nj ? nj : wb_nfull) - 1u);
     }
-    const uint32_t nmax = wave_max_u32(my_nfull);
-    if (nmax == 0) return;
-    // one v_min and one 64-bit add per DMA instruction: the chunk offset 64 c
-    // is wave-uniform
+    const uint8_t* base = reinterpret_cast<const uint8_t*>(wb);
+    const bool near = __all(relk[0] + lastk[0] <= 0xFFFFFFFFull && relk[1] + lastk[1] <= 0xFFFFFFFFull &&
+                            relk[2] + lastk[2] <= 0xFFFFFFFFull && relk[3] + lastk[3] <= 0xFFFFFFFFull);
+    uint32_t rel[4], lastabs[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        rel[k] = uint32_t(relk[k]);
+        lastabs[k] = uint32_t(relk[k]) + lastk[k];
+    }
+    // Chunk c: while every live value still has block c (c < minfull) the
+    // offsets are the per-role constants rel[k] from the uniform base + 64 c
+    // (saddr-form DMA, no VALU); past that, each role clamps to its value's
+    // last full block (a lane past its value re-reads it).  Waves whose values
+    // lie more than 4 GiB apart take 64-bit addresses throughout.
+    // buffer descriptor over [wb, wb + 4 GiB): the uniform chunk offset rides
+    // in soffset, so the in-range issue has no VALU at all
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base), short(0), int(0xFFFFFFFF), 0x00020000);
     auto issue = [&](uint32_t c) {
         uint8_t* dst = wbuf + 4096 * (c % R);
         const uint32_t cb = 64u * c;
+        if (near && c < minfull) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-            __builtin_amdgcn_global_load_lds(src[k] + min(cb, lastoff[k]), dst + 1024 * k, 16, 0, 0);
+            for (int k = 0; k < 4; ++k)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    rsrc, (__attribute__((address_space(3))) void*)(dst + 1024 * k), 16, rel[k],
+                    int(cb), 0, 0);
+        } else if (near) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    rsrc, (__attribute__((address_space(3))) void*)(dst + 1024 * k), 16,
+                    min(rel[k] + cb, lastabs[k]), 0, 0, 0);
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                __builtin_amdgcn_global_load_lds(base + (relk[k] + min(cb, lastk[k])), dst + 1024 * k, 16, 0, 0);
+        }
     };
-    const uint32_t lds0 = uint32_t(reinterpret_cast<uintptr_t>(wbuf));
-    const uint32_t row = lds0 + 64u * uint32_t(lane);
-    const uint32_t swz = (uint32_t(lane) >> 2) & 3u;
+    const uint32_t row = uint32_t(reinterpret_cast<uintptr_t>(wbuf)) + 64u * uint32_t(lane);
     auto read_window = [&](uint32_t b, u32x4 v[4]) {
-        const uint32_t s0 = row + 4096u * (b % R);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = ds_read_b128_asm(s0 + 16u * (uint32_t(q) ^ swz));
+        const uint32_t s0 = row + 4096u * (b % R);  // one VALU; the chunks at immediate offsets
+        v[0] = ds_read_b128_off<0>(s0);
+        v[1] = ds_read_b128_off<16>(s0);
+        v[2] = ds_read_b128_off<32>(s0);
+        v[3] = ds_read_b128_off<48>(s0);
     };
     // block b from cur while window b+1 lands in nxt; the loop below runs it
     // twice per iteration with the roles swapped, so no window is copied
@@ -790,15 +863,15 @@ __device__ __forceinline__ void sha1_blocks_ring_vc(uint8_t* wbuf, const uint8_t
 #pragma unroll
     for (uint32_t c = 0; c < uint32_t(R); ++c) issue(c);
     wait_vmcnt<4 * (R - 1)>();
-    u32x4 wa[4], wb[4];
+    u32x4 wa[4], wb4[4];
     read_window(0u, wa);
     asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(wa[0]), "+v"(wa[1]), "+v"(wa[2]), "+v"(wa[3]) : : "memory");
     uint32_t b = 0;
     for (; b + 2 <= nmax; b += 2) {
-        step(b, wa, wb);
-        step(b + 1, wb, wa);
+        step(b, wa, wb4);
+        step(b + 1, wb4, wa);
     }
-    if (b < nmax) step(b, wa, wb);
+    if (b < nmax) step(b, wa, wb4);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
@@ -817,23 +890,6 @@ __device__ __forceinline__ void sha1_blocks_ring_vc(uint8_t* wbuf, const uint8_t
 // of the wave to have the same full-block count and the wave's pairs to lie
 // within 4 GiB of the base.  Otherwise it returns false and does nothing (the
 // caller runs the LOAD 8 stream).  Stage: 8 KiB per wave.
-template <int X>
-__device__ __forceinline__ uint64_t min_swz64(uint64_t v) {
-    const uint64_t u = (uint64_t(swz_xor<X>(uint32_t(v >> 32))) << 32) | swz_xor<X>(uint32_t(v));
-    return u < v ? u : v;
-}
-__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
-    v = min_swz64<1>(v);
-    v = min_swz64<2>(v);
-    v = min_swz64<4>(v);
-    v = min_swz64<8>(v);
-    v = min_swz64<16>(v);
-    const uint64_t a = (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(uint32_t(v >> 32)), 0))) << 32) |
-                       uint32_t(__builtin_amdgcn_readlane(int(uint32_t(v)), 0));
-    const uint64_t b = (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(uint32_t(v >> 32)), 32))) << 32) |
-                       uint32_t(__builtin_amdgcn_readlane(int(uint32_t(v)), 32));
-    return a < b ? a : b;
-}
 
 // kWindow (LOAD 10): the same stream with only each value's 80-byte window row
 // (five aligned quads from (o & ~15), clamped like the pair's), so a wave's
@@ -1097,14 +1153,6 @@ __device__ __forceinline__ void sha1_blocks_any(uint8_t* wbuf, const uint8_t* p,
     sha1_blocks_lds(wbuf, wave_max_u32(my_nfull), my_nfull, issue, h);
 }
 
-__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
-    v = min(v, swz_xor<1>(v));
-    v = min(v, swz_xor<2>(v));
-    v = min(v, swz_xor<4>(v));
-    v = min(v, swz_xor<8>(v));
-    v = min(v, swz_xor<16>(v));
-    return min(uint32_t(__builtin_amdgcn_readlane(int(v), 0)), uint32_t(__builtin_amdgcn_readlane(int(v), 32)));
-}
 
 // MODE 0: value i at base + i*stride, length L.  MODE 1: base + off[i], len[i].
 // perm (MODE 1 only, nullable): lane i hashes leaf perm[i] (length bucketing).
