@@ -271,10 +271,33 @@ def main():
             _lib.check(L.nkv_tree_from_values_dev(ctx.h, data.data_ptr(), d_off.data_ptr(), d_len.data_ptr(),
                                                   n, nodes.data_ptr()))
 
+    # C1, the root gather, overlapped with the next
+    # table: step i builds into bufs[i % 2] and all-gathers that buffer's root
+    # asynchronously on RCCL's stream while step i + 1 hashes into the other
+    # buffer; step i + 2 first waits for gather i (long done: a 20-byte
+    # all-gather against a 1.2 ms table) before it rewrites bufs[i % 2].
+    # Every gather still completes inside the timed region (the final
+    # synchronize waits for it).
+    gather = world > 1 and not one_tree
+    bufs = [nodes, torch.empty_like(nodes)] if gather else [nodes]
+    root_out = [roots, torch.empty_like(roots)] if gather else [roots]
+    pending = []  # (step index, async work)
+    nstep = [0]
+
     def step():
+        nonlocal nodes
+        i = nstep[0]
+        nstep[0] += 1
+        while pending and pending[0][0] <= i - 2:
+            pending.pop(0)[1].wait()
+        nodes = bufs[i % len(bufs)]
         tree()
-        if world > 1 and not one_tree:  # C1: gather the per-table roots
-            dist.all_gather_into_tensor(roots, nodes[-20:])
+        if gather:
+            pending.append((i, dist.all_gather_into_tensor(root_out[i % 2], nodes[-20:], async_op=True)))
+
+    def drain():
+        while pending:
+            pending.pop(0)[1].wait()
 
     # Untimed pre-roll, independent of --warmup: the shader clock settles only
     # after ~30 ms of back-to-back launches ("The clock"),
@@ -285,13 +308,16 @@ def main():
         step()
         preroll_steps += 1
         if preroll_steps % 8 == 0:
+            drain()
             torch.cuda.synchronize()
+    drain()
     torch.cuda.synchronize()
     if records and (int(d_err.item()) != 0 or (verify_crc and int(d_stats[2].item()) != 0)):
         # a malformed synthetic stream would time empty hashes
         raise SystemExit("bench.py: the record stream failed the header checks")
     for _ in range(args.warmup):
         step()
+    drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -300,6 +326,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -311,6 +338,7 @@ def main():
         ctx.set_timing(True)
         for _ in range(args.steps):
             step()
+        drain()
         calls, leaf_ms_tot, reduce_ms_tot = ctx.timing_summary()
         ctx.set_timing(False)
     if world > 1:
