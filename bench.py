@@ -156,6 +156,38 @@ def ensure_ranks(args, argv, run=None) -> "int | None":
     return (run or subprocess.call)(launcher_cmd(argv, args.gpus, port))
 
 
+class RootGather:
+    """Per-step RCCL all-gather of the table roots, overlapped with the next
+    step: step i builds into bufs[i % 2] and gathers that buffer's 20-byte root
+    asynchronously into outs[i % 2]; begin() of step i + 2 waits for gather i
+    before bufs[i % 2] is rewritten.  dist None: one rank, nothing to gather."""
+
+    def __init__(self, nodes, roots, dist=None):
+        self.dist = dist
+        self.bufs = [nodes, nodes.new_empty(nodes.shape)] if dist else [nodes]
+        self.outs = [roots, roots.new_empty(roots.shape)] if dist else [roots]
+        self.pending = []  # (step index, async work)
+        self.i = -1
+
+    def begin(self):
+        self.i += 1
+        while self.pending and self.pending[0][0] <= self.i - 2:
+            self.pending.pop(0)[1].wait()
+        return self.bufs[self.i % len(self.bufs)]
+
+    def end(self, nodes):
+        if self.dist:
+            work = self.dist.all_gather_into_tensor(self.outs[self.i % 2], nodes[-20:], async_op=True)
+            self.pending.append((self.i, work))
+
+    def drain(self):
+        while self.pending:
+            self.pending.pop(0)[1].wait()
+
+    def last_roots(self):
+        return self.outs[self.i % 2]
+
+
 def main():
     args = parse()
     if args.config in ("records", "records_verify") and args.value_bytes <= 30 + args.key_bytes:
@@ -278,26 +310,15 @@ def main():
     # all-gather against a 1.2 ms table) before it rewrites bufs[i % 2].
     # Every gather still completes inside the timed region (the final
     # synchronize waits for it).
-    gather = world > 1 and not one_tree
-    bufs = [nodes, torch.empty_like(nodes)] if gather else [nodes]
-    root_out = [roots, torch.empty_like(roots)] if gather else [roots]
-    pending = []  # (step index, async work)
-    nstep = [0]
+    rg = RootGather(nodes, roots, dist if (world > 1 and not one_tree) else None)
 
     def step():
         nonlocal nodes
-        i = nstep[0]
-        nstep[0] += 1
-        while pending and pending[0][0] <= i - 2:
-            pending.pop(0)[1].wait()
-        nodes = bufs[i % len(bufs)]
+        nodes = rg.begin()
         tree()
-        if gather:
-            pending.append((i, dist.all_gather_into_tensor(root_out[i % 2], nodes[-20:], async_op=True)))
+        rg.end(nodes)
 
-    def drain():
-        while pending:
-            pending.pop(0)[1].wait()
+    drain = rg.drain
 
     # Untimed pre-roll, independent of --warmup: the shader clock settles only
     # after ~30 ms of back-to-back launches ("The clock"),

@@ -2,7 +2,8 @@
 
 `python bench.py --gpus N` without a launcher must start N ranks through
 torch.distributed.run (a child process, before any GPU call) instead of
-silently measuring one GPU; under a launcher WORLD_SIZE must equal N.
+silently measuring one GPU; under a launcher WORLD_SIZE must equal N.  The
+per-step root all-gather (RootGather) is pipelined over two tree buffers.
 """
 import os
 import sys
@@ -17,6 +18,15 @@ import bench  # noqa: E402
 
 def _args(gpus):
     return types.SimpleNamespace(gpus=gpus)
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
 
 
 def test_single_gpu_runs_in_process(monkeypatch):
@@ -52,8 +62,45 @@ def test_spawned_ranks_see_their_rank(tmp_path):
     out.mkdir()
     script.write_text("import os\nopen(os.path.join(%r, os.environ['LOCAL_RANK']), 'w').write("
                       "os.environ['WORLD_SIZE'])\n" % str(out))
-    cmd = bench.launcher_cmd([], 2, 29731)
+    cmd = bench.launcher_cmd([], 2, _free_port())
     cmd[cmd.index(os.path.abspath(bench.__file__))] = str(script)
     assert subprocess.call(cmd, timeout=120) == 0
     assert sorted(os.listdir(out)) == ["0", "1"]
     assert all((out / r).read_text() == "2" for r in ("0", "1"))
+
+
+def _gather_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rg = bench.RootGather(torch.zeros(100, dtype=torch.uint8), torch.zeros(world * 20, dtype=torch.uint8), dist)
+    seen = []
+    for i in range(7):
+        buf = rg.begin()
+        if i >= 2:  # begin() waited for gather i - 2: its output is final until end()
+            seen.append(rg.outs[i % 2].tolist())
+        buf[-20:] = (rank * 16 + i) % 256  # this step's "root"
+        rg.end(buf)
+    rg.drain()
+    seen += [rg.outs[5 % 2].tolist(), rg.last_roots().tolist()]
+    q.put((rank, seen))
+    dist.destroy_process_group()
+
+
+def test_root_gather_pipeline_world2():
+    """RootGather over gloo, world size 2: every step's gathered roots are every
+    rank's root of that step, though step i + 1 runs while gather i is in flight."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    # step i's gathered roots: rank 0's i, then rank 1's 16 + i
+    want = [[i] * 20 + [16 + i] * 20 for i in range(7)]
+    assert res[0] == want and res[1] == want
