@@ -411,11 +411,17 @@ def main():
         value = total_bytes / elapsed / 2**30
         achieved = nbytes / (leaf_ms * 1e-3) / 1e9  # algorithmic payload bytes per K1 launch
         traffic, traffic_bounds = None, None
-        pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc_path) and args.config == "sstable4k":
+        # PMC-measured HBM bytes of this config's leaf kernel (separate rocprofv3
+        # passes: tools/pmc_sizes.sh for cfg2, tools/pmc_config.sh for the others)
+        pmc_name = {"sstable4k": "pmc_traffic.json", "records": "pmc_traffic_records.json",
+                    "mixed": "pmc_traffic_mixed.json"}.get(args.config)
+        pmc_path = os.path.join(ROOT, "profiles", pmc_name) if pmc_name else None
+        if pmc_path and os.path.exists(pmc_path):
             with open(pmc_path) as f:
                 pmc = json.load(f)
-            if pmc.get("leaves") == n and pmc.get("value_bytes") == vlen:
+            same = pmc.get("leaves") == n and (pmc.get("value_bytes") in (None, vlen)) and \
+                pmc.get("algorithmic_bytes_per_launch") in (None, nbytes)
+            if same:
                 traffic = pmc.get("hbm_bytes_per_launch")
                 traffic_bounds = pmc.get("hbm_read_bytes_bounds_per_launch")
         out = {

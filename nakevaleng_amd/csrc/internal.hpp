@@ -8,10 +8,10 @@ namespace nkv {
 constexpr int kBlock = 256;       // threads per workgroup = leaves per K1 block
 constexpr int kSlabLevels = 8;    // log2(kBlock): levels one k_reduce workgroup builds
 #ifndef NKV_REDUCE2_MIN
-#define NKV_REDUCE2_MIN 65536
+#define NKV_REDUCE2_MIN 524288
 #endif
 // levels of at least this many nodes are reduced two at a time at full lane
-// use (k_reduce2) before the 8-level slabs take over
+// use (k_reduce2) before the slabs take over (launch_reduce)
 constexpr uint64_t kReduce2Min = NKV_REDUCE2_MIN;
 constexpr int kMaxLevels = 64;
 #ifndef NKV_LEAF_WAVES

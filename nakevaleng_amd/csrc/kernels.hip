@@ -179,13 +179,14 @@ __device__ __forceinline__ void load_digest(const uint8_t* nodes, uint64_t idx, 
 // Levels j0+1 .. jmax are computed; each level's nodes are written to the
 // global nodes buffer.  Node i of level j is SHA-1(c[2i] || c[2i+1]) when
 // 2i+1 < n_{j-1}, else SHA-1(c[2i]) (the empty pad, merkletree.go:32-34).
-__device__ __forceinline__ void subtree_reduce(uint32_t (*lds)[kBlock], uint64_t n, int j0, int jmax, uint64_t lo,
+template <int B>
+__device__ __forceinline__ void subtree_reduce(uint32_t (*lds)[B], uint64_t n, int j0, int jmax, uint64_t lo,
                                uint8_t* nodes) {
     const int tid = threadIdx.x;
     uint64_t nprev = lvl_count(n, j0);
     uint64_t start_cur = lvl_start(n, j0) + nprev;
     uint64_t lo_prev = lo;
-    int span = kBlock;
+    int span = B;
     for (int j = j0 + 1; j <= jmax; ++j) {
         const uint64_t ncur = ((nprev - 1) >> 1) + 1;
         const uint64_t lo_cur = lo_prev >> 1;
@@ -1170,7 +1171,11 @@ __global__ __launch_bounds__(kBlock, (LOAD == 6 || LOAD == 7) ? 2 : ((LOAD == 4 
                                                   uint64_t L, const uint32_t* __restrict__ perm,
                                                   uint64_t n, uint8_t* __restrict__ nodes, Gate gate) {
     // 16 KiB: four wave-private 4 KiB LDS-DMA stages (LOAD 1, 8); 8 KiB each for LOAD 9, 5 KiB for LOAD 10
-    __shared__ __attribute__((aligned(16))) uint8_t smem[kBlock * (LOAD == 9 ? 128 : (LOAD == 10 || LOAD == 11 ? 80 : 64))];
+#ifndef NKV_LEAF_LDS_PAD
+#define NKV_LEAF_LDS_PAD 0  // experiment builds only: extra LDS per workgroup to cap occupancy
+#endif
+    __shared__ __attribute__((aligned(16))) uint8_t
+        smem[kBlock * (LOAD == 9 ? 128 : (LOAD == 10 || LOAD == 11 ? 80 : 64)) + NKV_LEAF_LDS_PAD];
     if (!gate.open()) return;
     NKV_STAMP(0);
     const uint64_t g = blockIdx.x;
@@ -1502,19 +1507,22 @@ __global__ __launch_bounds__(64, queue_ring_slots<LOAD>() == 4 ? 2 : (queue_ring
 #endif
 }
 
-// K2: reduce one level j0 (already in nodes) up to min(j0 + 8, top).
-__global__ __launch_bounds__(kBlock) void k_reduce(uint8_t* __restrict__ nodes, uint64_t n, int j0,
-                                                    int jmax, Gate gate) {
-    __shared__ uint32_t lds[5][kBlock];
+// K2: a B-node slab of level j0 (already in nodes) reduced up to
+// min(j0 + log2 B, top) in LDS, one workgroup of B threads per slab: 8 levels
+// per launch with B = 256, 10 with B = 1024 (the narrow levels are a chain of
+// one compression per level, so fewer launches is a shorter tree).
+template <int B>
+__global__ __launch_bounds__(B) void k_reduce(uint8_t* __restrict__ nodes, uint64_t n, int j0, int jmax, Gate gate) {
+    __shared__ uint32_t lds[5][B];
     if (!gate.open()) return;
-    const uint64_t lo = uint64_t(blockIdx.x) * kBlock;
+    const uint64_t lo = uint64_t(blockIdx.x) * B;
     const uint64_t cnt = lvl_count(n, j0);
     const uint64_t idx = lo + threadIdx.x;
     uint32_t h[5] = {0u, 0u, 0u, 0u, 0u};
     if (idx < cnt) load_digest(nodes, lvl_start(n, j0) + idx, h);
 #pragma unroll
     for (int k = 0; k < 5; ++k) lds[k][threadIdx.x] = h[k];
-    subtree_reduce(lds, n, j0, jmax, lo, nodes);
+    subtree_reduce<B>(lds, n, j0, jmax, lo, nodes);
 }
 
 // K2w: the wide bottom levels at full lane use.  A wavefront takes 256 nodes
@@ -1987,7 +1995,14 @@ uint64_t queue_words(uint64_t n) { return kQueueHeader + kSimdKeys + (n + 63) / 
 
 hipError_t launch_reduce(uint8_t* nodes, uint64_t n, int from_level, int top, hipStream_t s, Gate gate) {
     int j0 = from_level;
-    // wide levels two at a time (k_reduce2), then 8-level slabs
+    // The widest levels two at a time at full lane use (k_reduce2, while a
+    // level holds >= kReduce2Min = 512 Ki nodes: that launch is
+    // compression-bound); then slabs, which are a chain of one compression per
+    // level: 1024-node slabs (10 levels per launch) while a level holds more
+    // than 256 nodes, then the last <= 8 levels in 256-node slabs.  At
+    // n = 2^20: k_reduce2 0 -> 2, 1024-slabs 2 -> 12, 256-slab 12 -> 20: 52.5 us
+    // against 60.7 us for r01's three k_reduce2 and two 256-slab launches
+    // (tools/ab_reduce.sh, one box).
     for (uint64_t cnt = j0 == 0 ? n : ((n - 1) >> j0) + 1; top - j0 >= 2 && cnt >= kReduce2Min;
          cnt = ((cnt - 1) >> 2) + 1) {
         const uint64_t waves = (cnt + 255) / 256;
@@ -1998,12 +2013,19 @@ hipError_t launch_reduce(uint8_t* nodes, uint64_t n, int from_level, int top, hi
         j0 += 2;
     }
     while (j0 < top) {
-        const int jmax = (j0 + kSlabLevels < top) ? j0 + kSlabLevels : top;
         const uint64_t cnt = j0 == 0 ? n : ((n - 1) >> j0) + 1;
-        hipLaunchKernelGGL(k_reduce, dim3(grid_for(cnt)), dim3(kBlock), 0, s, nodes, n, j0, jmax, gate);
+        if (cnt > 256 && top - j0 > kSlabLevels) {
+            const int jmax = (j0 + 10 < top) ? j0 + 10 : top;
+            hipLaunchKernelGGL(k_reduce<1024>, dim3(unsigned((cnt + 1023) / 1024)), dim3(1024), 0, s, nodes, n, j0,
+                               jmax, gate);
+            j0 = jmax;
+        } else {
+            const int jmax = (j0 + kSlabLevels < top) ? j0 + kSlabLevels : top;
+            hipLaunchKernelGGL(k_reduce<kBlock>, dim3(grid_for(cnt)), dim3(kBlock), 0, s, nodes, n, j0, jmax, gate);
+            j0 = jmax;
+        }
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
-        j0 = jmax;
     }
     return hipSuccess;
 }
