@@ -63,7 +63,7 @@ def build(force: bool = False, verbose: bool = False, diag: bool = False, quiet:
             print(last_status, file=sys.stderr)
         return so
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    tmp = so + ".tmp"
+    tmp = f"{so}.tmp{os.getpid()}"  # concurrent builders (ranks) never share a temp file
     cmd = [hipcc] + FLAGS + ["-I", os.path.join(ROOT, "include"), "-I", CSRC, f'-DNKV_SRC_HASH="{want}"']
     if diag:
         cmd.append("-DNKV_DIAG")
