@@ -13,6 +13,12 @@ constexpr int kSlabLevels = 8;    // log2(kBlock): levels one k_reduce workgroup
 // levels of at least this many nodes are reduced two at a time at full lane
 // use (k_reduce2) before the slabs take over (launch_reduce)
 constexpr uint64_t kReduce2Min = NKV_REDUCE2_MIN;
+#ifndef NKV_REDUCE_WIDE_MIN
+#define NKV_REDUCE_WIDE_MIN 65536
+#endif
+// levels of at least this many nodes (and at least 12 below the top) take the
+// bottom-twelve-levels launch (k_reduce_wide) first
+constexpr uint64_t kReduceWideMin = NKV_REDUCE_WIDE_MIN;
 constexpr int kMaxLevels = 64;
 #ifndef NKV_LEAF_WAVES
 #define NKV_LEAF_WAVES 8

@@ -1573,6 +1573,59 @@ __global__ __launch_bounds__(kBlock) void k_reduce2(uint8_t* __restrict__ nodes,
     }
 }
 
+// K2x: the bottom twelve levels in one launch.  A workgroup of 1024 threads
+// (16 waves) takes 4096 nodes of level j0: each wave builds the two levels
+// above its 256 nodes at full lane use exactly as k_reduce2 does (128 parents,
+// two per lane, then their 64 parents by shuffles), the workgroup's 1024
+// level-(j0 + 2) nodes go to LDS, and subtree_reduce<1024> builds ten more
+// levels: jmax = min(j0 + 12, top).  Replaces k_reduce2 + one 1024-slab launch
+// (the slab part is a chain of one compression per level either way).
+__global__ __launch_bounds__(1024) void k_reduce_wide(uint8_t* __restrict__ nodes, uint64_t n, int j0, int jmax,
+                                                      Gate gate) {
+    __shared__ uint32_t lds[5][1024];
+    if (!gate.open()) return;
+    const int lane = threadIdx.x & 63;
+    const int wv = threadIdx.x >> 6;
+    const uint64_t w = uint64_t(blockIdx.x) * 16 + uint64_t(wv);
+    const uint64_t n0 = lvl_count(n, j0), s0 = lvl_start(n, j0);
+    const uint64_t n1 = ((n0 - 1) >> 1) + 1, s1 = s0 + n0;
+    uint32_t hp[2][5];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+#pragma unroll
+        for (int k = 0; k < 5; ++k) hp[p][k] = 0u;
+        const uint64_t i1 = 128 * w + uint64_t(lane) + 64 * p;
+        if (i1 < n1) {
+            const bool lone = 2 * i1 + 1 >= n0;
+            uint32_t l[5], r[5] = {0u, 0u, 0u, 0u, 0u};
+            load_digest(nodes, s0 + 2 * i1, l);
+            if (!lone) load_digest(nodes, s0 + 2 * i1 + 1, r);
+            sha1_parent(l, r, lone, hp[p]);
+            store_digest(nodes, s1 + i1, hp[p]);
+        }
+    }
+    const uint64_t n2 = ((n1 - 1) >> 1) + 1, s2 = s1 + n1;
+    const uint64_t i2 = 64 * w + uint64_t(lane);
+    const int src = (2 * lane) & 63;
+    uint32_t l[5], r[5], h[5] = {0u, 0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        const uint32_t l0 = uint32_t(__shfl(int(hp[0][k]), src)), l1 = uint32_t(__shfl(int(hp[1][k]), src));
+        const uint32_t r0 = uint32_t(__shfl(int(hp[0][k]), src + 1)), r1 = uint32_t(__shfl(int(hp[1][k]), src + 1));
+        l[k] = lane < 32 ? l0 : l1;
+        r[k] = lane < 32 ? r0 : r1;
+    }
+    if (i2 < n2) {
+        const bool lone = 2 * i2 + 1 >= n1;
+        sha1_parent(l, r, lone, h);
+        store_digest(nodes, s2 + i2, h);
+    }
+    // level j0 + 2 of this workgroup's 4096 nodes: 1024 nodes, node 64 wv + lane
+#pragma unroll
+    for (int k = 0; k < 5; ++k) lds[k][threadIdx.x] = h[k];
+    subtree_reduce<1024>(lds, n, j0 + 2, jmax, uint64_t(blockIdx.x) * 1024, nodes);
+}
+
 // ---------------------------------------------------------------------------
 // Length bucketing for ragged values: one lane per value means a wavefront
 // runs for its longest value, so values are ordered by compression count,
@@ -2003,6 +2056,19 @@ hipError_t launch_reduce(uint8_t* nodes, uint64_t n, int from_level, int top, hi
     // n = 2^20: k_reduce2 0 -> 2, 1024-slabs 2 -> 12, 256-slab 12 -> 20: 52.5 us
     // against 60.7 us for r01's three k_reduce2 and two 256-slab launches
     // (tools/ab_reduce.sh, one box).
+    // 4096-node workgroups build the bottom twelve levels in one launch
+    // (k_reduce_wide) when the tree is that tall and the level between 64 Ki
+    // and 2 Mi nodes: at most two 1024-thread workgroups per CU, so beyond
+    // that the ten-level chains run in several rounds (at 8 Mi nodes 231 us
+    // against 209 us for k_reduce2 + slabs; at 1 Mi 50.5 against 53.9 us)
+    for (uint64_t cnt = j0 == 0 ? n : ((n - 1) >> j0) + 1;
+         top - j0 >= 12 && cnt >= kReduceWideMin && cnt <= (uint64_t(2) << 20); cnt = ((cnt - 1) >> 12) + 1) {
+        hipLaunchKernelGGL(k_reduce_wide, dim3(unsigned((cnt + 4095) / 4096)), dim3(1024), 0, s, nodes, n, j0,
+                           j0 + 12, gate);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        j0 += 12;
+    }
     for (uint64_t cnt = j0 == 0 ? n : ((n - 1) >> j0) + 1; top - j0 >= 2 && cnt >= kReduce2Min;
          cnt = ((cnt - 1) >> 2) + 1) {
         const uint64_t waves = (cnt + 255) / 256;
