@@ -313,7 +313,9 @@ int plan_of(nkv_ctx* c, const uint64_t* len, const uint64_t* host_len, uint64_t 
     }
     TRY(grow(c->d_range, 8));
     unsigned int* d = static_cast<unsigned int*>(c->d_range.p);
-    HIPTRY(launch_len_range(len, n, d, sync_slot(c, kSyncRange), c->stream));
+    uint32_t* part = nullptr;
+    TRY(locate_parts(c, n, &part));
+    HIPTRY(launch_len_range(len, n, d, part, c->stream));
     gate->range = d;
     *plan = kGated;
     return NKV_OK;

@@ -155,7 +155,8 @@ hipError_t launch_bloom_staged(int mode, const uint8_t* base, const uint64_t* of
                                uint64_t stream_len, uint64_t n, uint32_t m, uint32_t k, uint32_t seed0,
                                uint32_t* bits, unsigned int* err, uint32_t* scratch, hipStream_t s);
 hipError_t launch_fill(uint8_t* buf, uint64_t nbytes, uint64_t seed, hipStream_t s);
-// out[0] / out[1] = min / max of len[i] / 64 over the batch (2 u32 on the device)
-hipError_t launch_len_range(const uint64_t* len, uint64_t n, unsigned int* out, SyncSlot* sync, hipStream_t s);
+// out[0] / out[1] = min / max of len[i] / 64 over the batch (2 u32 on the
+// device); part: scratch of locate_part_words(n) u32
+hipError_t launch_len_range(const uint64_t* len, uint64_t n, unsigned int* out, uint32_t* part, hipStream_t s);
 
 }  // namespace nkv
