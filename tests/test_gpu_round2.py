@@ -181,3 +181,60 @@ def test_locate_header_only_record_at_stream_end(nkv, r8):
         assert rc == _lib.NKV_ERR_INVALID
     finally:
         ctx.set_stream(_lib._OWN)
+
+
+@pytest.mark.parametrize("bucket", [0, 1, 2])
+@pytest.mark.parametrize("fused", [1, 0])
+def test_records_partly_ragged_every_policy(nkv, oracle, bucket, fused):
+    """k_leaf_records' deferral: a table whose first waves hold records of one
+    size (narrow: hashed in place) and whose later waves hold random sizes
+    (ragged: deferred to the length-sorted pass, which must skip the values
+    already hashed), plus a bad header in a ragged wave; every NKV_OPT_BUCKET
+    policy and both records plans give the oracle's tree and report the header."""
+    import torch
+    from nakevaleng_amd import record
+    _lib, ctx = nkv
+    L = _lib.lib()
+    rng = np.random.default_rng(100 + bucket)
+    recs = [record.New(rng.bytes(16), rng.bytes(2000), timestamp=i) for i in range(64 * 40)]
+    recs += [record.New(rng.bytes(int(rng.integers(0, 40))), rng.bytes(int(rng.integers(0, 20000))), timestamp=i)
+             for i in range(3000)]
+    recs += [record.New(rng.bytes(16), rng.bytes(2000), timestamp=i) for i in range(64 * 10 + 17)]
+    stream, sizes = record.data_table(recs)
+    n = len(sizes)
+    roff = np.zeros(n, np.uint64)
+    roff[1:] = np.cumsum(np.asarray(sizes, np.uint64)[:-1])
+    off, ln = record.value_spans(stream, sizes)
+    want = oracle.tree_from_digests(oracle.leaf_hashes(np.frombuffer(stream, np.uint8), off, ln, threads=8))
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    ctx.set_option(_lib.NKV_OPT_BUCKET, bucket)
+    ctx.set_option(_lib.NKV_OPT_RECORDS_FUSED, fused)
+    try:
+        d_stream = torch.from_numpy(np.frombuffer(stream, np.uint8).copy()).cuda()
+        d_roff = torch.from_numpy(roff.view(np.int64)).cuda()
+        d_err = torch.full((1,), 7, dtype=torch.int32, device="cuda")
+        for _ in range(2):  # the gate's range and the fold restore themselves between calls
+            d_nodes = torch.zeros(L.nkv_total_nodes(n) * 20, dtype=torch.uint8, device="cuda")
+            _lib.check(L.nkv_tree_from_records_dev(ctx.h, d_stream.data_ptr(), len(stream), d_roff.data_ptr(), n,
+                                                   d_nodes.data_ptr(), d_err.data_ptr()))
+            torch.cuda.synchronize()
+            assert int(d_err.item()) == 0
+            assert np.array_equal(d_nodes.cpu().numpy().reshape(-1, 20), want)
+        bad = np.frombuffer(stream, np.uint8).copy()
+        j = 64 * 40 + 100  # inside the ragged part
+        bad[int(roff[j]) + 22:int(roff[j]) + 30] = np.frombuffer(np.uint64(10**12).tobytes(), np.uint8)
+        d_bad = torch.from_numpy(bad).cuda()
+        d_nodes = torch.zeros(L.nkv_total_nodes(n) * 20, dtype=torch.uint8, device="cuda")
+        _lib.check(L.nkv_tree_from_records_dev(ctx.h, d_bad.data_ptr(), len(stream), d_roff.data_ptr(), n,
+                                               d_nodes.data_ptr(), d_err.data_ptr()))
+        torch.cuda.synchronize()
+        assert int(d_err.item()) == 1
+        got = d_nodes.cpu().numpy().reshape(-1, 20)
+        ln_bad = ln.copy()
+        ln_bad[j] = 0  # the bad record's leaf hashes the empty value
+        leaves = oracle.leaf_hashes(bad, off, ln_bad, threads=8)
+        assert np.array_equal(got[:n], leaves.reshape(n, 20))
+    finally:
+        ctx.set_option(_lib.NKV_OPT_BUCKET, 2)
+        ctx.set_option(_lib.NKV_OPT_RECORDS_FUSED, 1)
+        ctx.set_stream(_lib._OWN)
