@@ -237,33 +237,34 @@ class MerkleTree {  // merkletree.go:13-15
             nodes_.push_back(std::move(n));
         }
         Root = nodes_.empty() ? nullptr : &nodes_.front();
+        n_ = 0;  // no longer a tree New built
     }
 
-    // merkletree.go:162-171: recompute the root from the leaves' Data.  A tree
-    // New built (Root unchanged) is rehashed in one device call over its
-    // leaves' current Data (nkv_tree_validate); any other tree per depth.
+    // merkletree.go:162-171: recompute the root from the leaves' Data.  When the
+    // pointer tree under Root has exactly the shape New builds for its n leaves
+    // (checked link by link: NewShapedLeaves), rehash (merklenode.go:99-108)
+    // equals the tree rebuilt from the leaves' current Data -- one device call,
+    // nkv_tree_validate.  Any other tree (Deserialize's root-only tree, a
+    // hand-built or relinked one) is rehashed per depth.
     bool Validate() {
         if (!Root) throw std::runtime_error("Validate: nil root");
-        if (Root == built_root_ && !leaves_.empty()) {
-            bool childless = true;
-            for (MerkleNode* x : leaves_) childless = childless && !x->Left && !x->Right;
-            if (childless) {
-                if (Root->Resolve().size() < 20) throw std::runtime_error("Validate: index out of range");
-                std::vector<uint8_t> flat;
-                std::vector<uint64_t> off, len;
-                for (MerkleNode* x : leaves_) {
-                    const auto& d = x->Resolve();
-                    off.push_back(flat.size());
-                    len.push_back(d.size());
-                    flat.insert(flat.end(), d.begin(), d.end());
-                }
-                flat.push_back(0);
-                int ok = 0;
-                check(nkv_tree_validate(Session::Default().ctx(), flat.data(), off.data(), len.data(), leaves_.size(),
-                                        Root->Data.data(), &ok),
-                      "Validate");
-                return ok != 0;
+        std::vector<MerkleNode*> leaves;
+        if (n_ && NewShapedLeaves(Root, n_, &leaves)) {
+            if (Root->Resolve().size() < 20) throw std::runtime_error("Validate: index out of range");
+            std::vector<uint8_t> flat;
+            std::vector<uint64_t> off, len;
+            for (MerkleNode* x : leaves) {
+                const auto& d = x->Resolve();
+                off.push_back(flat.size());
+                len.push_back(d.size());
+                flat.insert(flat.end(), d.begin(), d.end());
             }
+            flat.push_back(0);
+            int ok = 0;
+            check(nkv_tree_validate(Session::Default().ctx(), flat.data(), off.data(), len.data(), leaves.size(),
+                                    Root->Data.data(), &ok),
+                  "Validate");
+            return ok != 0;
         }
         std::vector<uint8_t> h = Rehash(Root);
         if (Root->Resolve().size() < 20 || h.size() < 20)
@@ -279,6 +280,36 @@ class MerkleTree {  // merkletree.go:13-15
     friend std::unique_ptr<MerkleTree> New(std::vector<MerkleNode> level, std::string* err);
 
    private:
+    // The n level-0 nodes under root when the tree has New's shape for n leaves
+    // (merkletree.go:31-64): every internal node has two children, each odd level
+    // below the top ends in an empty childless pad, level-0 nodes are childless.
+    static bool NewShapedLeaves(MerkleNode* root, uint64_t n, std::vector<MerkleNode*>* out) {
+        const int top = nkv_num_levels(n) - 1;
+        std::vector<MerkleNode*> cur{root};
+        auto pad_ok = [](const MerkleNode* p) { return !p->Left && !p->Right && p->Data.empty() && !p->pend; };
+        for (int L = top; L >= 0; --L) {
+            const uint64_t real = nkv_level_count(n, L);
+            const bool pad = (real & 1) && L < top;
+            if (cur.size() != real + (pad ? 1 : 0)) return false;
+            if (pad && !pad_ok(cur.back())) return false;
+            if (L == 0) {
+                for (uint64_t i = 0; i < real; ++i)
+                    if (cur[i]->Left || cur[i]->Right) return false;
+                out->assign(cur.begin(), cur.begin() + real);
+                return true;
+            }
+            std::vector<MerkleNode*> nxt;
+            nxt.reserve(2 * real);
+            for (uint64_t i = 0; i < real; ++i) {
+                if (!cur[i]->Left || !cur[i]->Right) return false;
+                nxt.push_back(cur[i]->Left);
+                nxt.push_back(cur[i]->Right);
+            }
+            cur.swap(nxt);
+        }
+        return false;
+    }
+
     // merklenode.go:99-108 by depth on the device (pads make the tree ragged)
     static std::vector<uint8_t> Rehash(MerkleNode* root) {
         std::vector<std::vector<MerkleNode*>> lv{{root}};
@@ -320,8 +351,7 @@ class MerkleTree {  // merkletree.go:13-15
 
     std::deque<MerkleNode> nodes_;  // owns every node of the tree (stable addresses)
     std::vector<uint8_t> levels_;
-    std::vector<MerkleNode*> leaves_;  // level 0 as New built it
-    MerkleNode* built_root_ = nullptr;
+    uint64_t n_ = 0;  // leaves New built the tree from
 };
 
 inline std::vector<std::vector<uint8_t>> Sha1Many(const std::vector<std::vector<uint8_t>>& msgs) {
@@ -397,7 +427,7 @@ inline std::unique_ptr<MerkleTree> New(std::vector<MerkleNode> level, std::strin
         pool.push_back(x);
         below.push_back(&pool.back());
     }
-    t->leaves_ = below;
+    t->n_ = n;
     const int lv = nkv_num_levels(n);
     for (int L = 1; L < lv; ++L) {
         if (below.size() % 2) {
@@ -415,7 +445,7 @@ inline std::unique_ptr<MerkleTree> New(std::vector<MerkleNode> level, std::strin
         }
         below.swap(cur);
     }
-    t->Root = t->built_root_ = below[0];
+    t->Root = below[0];
     return t;
 }
 

@@ -152,7 +152,6 @@ class MerkleTree:  # merkletree.go:13-15
         self._leaves: Optional[List[MerkleNode]] = None  # copies of the level given to New
         self._image: Optional[bytes] = None
         self._materialized = False
-        self._built_root: Optional[MerkleNode] = None  # the root New materialized
 
     # ---- Root (pointer tree) ----
     @property
@@ -181,7 +180,7 @@ class MerkleTree:  # merkletree.go:13-15
             for i in range(counts[L]):
                 cur.append(MerkleNode(self.nodes[s + i].tobytes(), prev[2 * i], prev[2 * i + 1]))
             below = cur
-        self._root = self._built_root = below[0]
+        self._root = below[0]
         self._materialized = True
 
     # ---- Serialize ----
@@ -224,16 +223,58 @@ class MerkleTree:  # merkletree.go:13-15
 
     # ---- Validate ----
     def Validate(self) -> bool:  # merkletree.go:162-171
-        if self._leaves is not None and (not self._materialized or self._root is self._built_root):
-            # a tree New built, links unchanged: rehash is the tree over the
-            # leaves' current Data -- one device call (nkv_tree_validate)
+        if self._leaves is not None and not self._materialized:
+            # a tree New built whose pointer tree was never handed out: rehash
+            # is the tree over its leaves -- one device call (nkv_tree_validate)
             return _validate_leaves(self._leaves, root_of(self))
         root = self.Root
+        leaves = _new_shaped_leaves(root, self.n) if self.n else None
+        if leaves is not None:
+            # New's shape (checked link by link, pads empty and childless):
+            # rehash is again the tree over the leaves' current Data
+            return _validate_leaves(leaves, root.Data)
         h = _rehash(root)
         for i in range(20):
             if root.Data[i] != h[i]:
                 return False
         return True
+
+
+def _new_shaped_leaves(root: Optional[MerkleNode], n: int) -> Optional[List[MerkleNode]]:
+    """The n level-0 nodes under root if the pointer tree has exactly the shape
+    New builds for n leaves (merkletree.go:31-64: every internal node has two
+    children, an odd level below the top ends in an empty childless pad,
+    level-0 nodes are childless), else None.  On that shape rehash
+    (merklenode.go:99-108) equals the tree rebuilt from the leaves' Data."""
+    if root is None or n < 1:
+        return None
+    counts = _level_counts(n)
+    top = len(counts) - 1
+    cur = [root]
+    for L in range(top, 0, -1):
+        if len(cur) != counts[L] + (1 if (counts[L] & 1) and L < top else 0):
+            return None
+        if len(cur) > counts[L]:
+            pad = cur[-1]
+            if pad.Left is not None or pad.Right is not None or len(pad.Data) != 0:
+                return None
+        nxt: List[MerkleNode] = []
+        for x in cur[:counts[L]]:
+            if x.Left is None or x.Right is None:
+                return None
+            nxt.append(x.Left)
+            nxt.append(x.Right)
+        cur = nxt
+    if len(cur) != counts[0] + (1 if (counts[0] & 1) and top > 0 else 0):
+        return None
+    if len(cur) > counts[0]:
+        pad = cur[-1]
+        if pad.Left is not None or pad.Right is not None or len(pad.Data) != 0:
+            return None
+    leaves = cur[:counts[0]]
+    if any(x.Left is not None or x.Right is not None for x in leaves):
+        return None
+    return leaves
 
 
 def _validate_leaves(leaves: List[MerkleNode], root: bytes) -> bool:

@@ -103,6 +103,10 @@ int main(int argc, char** argv) {
             std::printf("flush%d_allocs_total %llu\n", k, (unsigned long long)S.arena_allocs());
             std::printf("flush%d_root %s\n", k, t->Root->String().c_str());
             std::printf("flush%d_validate %d\n", k, int(t->Validate()));
+            // children swapped: still New's shape, leaves re-collected in the new order
+            std::swap(t->Root->Left, t->Root->Right);
+            std::printf("flush%d_swapped_validate %d\n", k, int(t->Validate()));
+            std::swap(t->Root->Left, t->Root->Right);
             t->Root->Data[0] ^= 1;  // the stored root no longer matches the leaves
             std::printf("flush%d_bad_root_validate %d\n", k, int(t->Validate()));
         }

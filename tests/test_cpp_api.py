@@ -60,3 +60,4 @@ def test_cpp_mirror_on_gpu(tmp_path, oracle):
         want = oracle.tree_from_digests(oracle.leaf_hashes_strided(data, 512, 512, 4096))
         assert kv[f"flush{k}_root"] == want[-1].tobytes().hex()
         assert kv[f"flush{k}_validate"] == "1" and kv[f"flush{k}_bad_root_validate"] == "0"
+        assert kv[f"flush{k}_swapped_validate"] == "0"  # rehash over swapped children differs

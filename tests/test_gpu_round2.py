@@ -238,3 +238,43 @@ def test_records_partly_ragged_every_policy(nkv, oracle, bucket, fused):
         ctx.set_option(_lib.NKV_OPT_BUCKET, 2)
         ctx.set_option(_lib.NKV_OPT_RECORDS_FUSED, 1)
         ctx.set_stream(_lib._OWN)
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 7, 100, 1001])
+def test_mirror_validate_relinked_trees_match_rehash(nkv, n):
+    """Validate on a materialized tree after link changes agrees with the
+    reference's recursive rehash every time: swapped children (New's shape
+    kept: the device call over the re-collected leaves), a pad replaced by a
+    non-empty node and a subtree grafted as a leaf (shape broken: per-depth
+    rehash)."""
+    from nakevaleng_amd import merkletree as mt
+    vals = [bytes([i % 256, 7]) * (i % 90) for i in range(n)]
+
+    def fresh():
+        t = mt.New([mt.NewLeaf(v) for v in vals])
+        return t, t.Root
+
+    t, root = fresh()
+    assert t.Validate() and mt._rehash(root) == root.Data
+    if n > 1:
+        root.Left, root.Right = root.Right, root.Left
+        assert t.Validate() == (mt._rehash(root) == root.Data)
+    t, root = fresh()
+    pads = []
+    stack = [root]
+    while stack:
+        x = stack.pop()
+        if x.Left is not None:
+            stack += [x.Left, x.Right]
+        elif x.Data == b"":
+            pads.append(x)
+    if pads:
+        pads[0].Data = b"not a pad"
+        assert t.Validate() == (mt._rehash(root) == root.Data)
+    t, root = fresh()
+    leaf = root
+    while leaf.Left is not None:
+        leaf = leaf.Left
+    sub = mt.New([mt.NewLeaf(b"a"), mt.NewLeaf(b"b")]).Root
+    leaf.Left, leaf.Right = sub.Left, sub.Right
+    assert t.Validate() == (mt._rehash(root) == root.Data)
