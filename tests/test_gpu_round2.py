@@ -278,3 +278,47 @@ def test_mirror_validate_relinked_trees_match_rehash(nkv, n):
     sub = mt.New([mt.NewLeaf(b"a"), mt.NewLeaf(b"b")]).Root
     leaf.Left, leaf.Right = sub.Left, sub.Right
     assert t.Validate() == (mt._rehash(root) == root.Data)
+
+
+@pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 127, 4095, 4096, 4097, 9000])
+@pytest.mark.parametrize("shape", ["uniform_small", "uniform_unaligned", "random"])
+def test_records_fused_shapes(nkv, oracle, n, shape):
+    """k_leaf_records over record tables at every wave-count edge: one record
+    size (narrow waves, shared offset mod 64 -> the segment stage), one size
+    whose value starts mid-line, and random key/value sizes (empty values,
+    empty keys, sub-block values), through the device entry and the host
+    entry (which stages the stream through pinned chunks first)."""
+    import torch
+    from nakevaleng_amd import record
+    _lib, ctx = nkv
+    L = _lib.lib()
+    rng = np.random.default_rng(n * 7 + len(shape))
+    if shape == "uniform_small":
+        recs = [record.New(rng.bytes(8), rng.bytes(100), timestamp=i) for i in range(n)]
+    elif shape == "uniform_unaligned":
+        recs = [record.New(rng.bytes(5), rng.bytes(1000), timestamp=i) for i in range(n)]
+    else:
+        recs = [record.New(rng.bytes(int(rng.integers(0, 70))), rng.bytes(int(rng.integers(0, 700))), timestamp=i)
+                for i in range(n)]
+    stream, sizes = record.data_table(recs)
+    off, ln = record.value_spans(stream, sizes)
+    want = oracle.tree_from_digests(oracle.leaf_hashes(np.frombuffer(stream, np.uint8), off, ln, threads=8))
+    roff = np.zeros(n, np.uint64)
+    roff[1:] = np.cumsum(np.asarray(sizes, np.uint64)[:-1])
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    try:
+        d_stream = torch.from_numpy(np.frombuffer(stream, np.uint8).copy()).cuda()
+        d_roff = torch.from_numpy(roff.view(np.int64)).cuda()
+        d_nodes = torch.zeros(L.nkv_total_nodes(n) * 20, dtype=torch.uint8, device="cuda")
+        _lib.check(L.nkv_tree_from_records_dev(ctx.h, d_stream.data_ptr(), len(stream), d_roff.data_ptr(), n,
+                                               d_nodes.data_ptr(), None))
+        assert np.array_equal(d_nodes.cpu().numpy().reshape(-1, 20), want)
+    finally:
+        ctx.set_stream(_lib._OWN)
+    buf = np.frombuffer(stream + b"\0", np.uint8)
+    rs = np.ascontiguousarray(sizes, dtype=np.uint64)
+    root = np.zeros(20, np.uint8)
+    nodes = np.zeros((L.nkv_total_nodes(n), 20), np.uint8)
+    _lib.check(L.nkv_tree_from_records(ctx.h, _lib.p8(buf), len(stream), _lib.p64(rs), n, _lib.p8(root),
+                                       _lib.p8(nodes), None))
+    assert np.array_equal(nodes, want) and root.tobytes() == want[-1].tobytes()

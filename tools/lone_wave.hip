@@ -8,6 +8,7 @@
 #include "../nakevaleng_amd/csrc/kernels.hip"
 
 #include <stdio.h>
+#include <stdlib.h>
 #include <vector>
 
 namespace nkv {
@@ -34,6 +35,17 @@ __global__ __launch_bounds__(64, 1) void k_lone(const uint8_t* __restrict__ base
         sha1_blocks_ring_vc<V + 1>(smem, p, nblk, h);
     } else if constexpr (V == 4) {
         sha1_blocks_ring_pipe<3>(smem, p, nblk, h);
+    } else if constexpr (V == 5 || V == 6) {
+        // V 5: only lanes 0..31 active; V 6: only lanes 0..15 (does a lone
+        // wave with a partial exec mask issue faster?)
+        if (lane < (V == 5 ? 32 : 16)) {
+            for (uint32_t b = 0; b < nblk; ++b) {
+                uint32_t w[16];
+#pragma unroll
+                for (int i = 0; i < 16; ++i) w[i] = bswap32(uint32_t(v) + i * 0x9E3779B9u + b);
+                sha1_compress(h, w);
+            }
+        }
     }
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
     const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
@@ -88,6 +100,15 @@ int main() {
     uint8_t* d;
     if (hipMalloc(&d, bytes + 4096) != hipSuccess) return 1;
     (void)hipMemset(d, 0x5a, bytes + 4096);
+    if (getenv("NKV_LONE_EXEC")) {
+        for (int waves : {256, 1024}) {
+            run<0>("regs only, 64 lanes", d, vstride, nblk, waves, 0);
+            run<5>("regs only, 32 lanes", d, vstride, nblk, waves, 0);
+            run<6>("regs only, 16 lanes", d, vstride, nblk, waves, 0);
+        }
+        (void)hipFree(d);
+        return 0;
+    }
     for (int hbm = 0; hbm < 2; ++hbm)
         for (int waves : {256, 512, 1024, 2048}) {
             run<0>("regs only", d, vstride, nblk, waves, hbm);
