@@ -322,3 +322,87 @@ def test_records_fused_shapes(nkv, oracle, n, shape):
     _lib.check(L.nkv_tree_from_records(ctx.h, _lib.p8(buf), len(stream), _lib.p64(rs), n, _lib.p8(root),
                                        _lib.p8(nodes), None))
     assert np.array_equal(nodes, want) and root.tobytes() == want[-1].tobytes()
+
+
+def test_full_size_config3_mixed_bit_exact(nkv, oracle):
+    """BASELINE configs[2] at its full size: log-uniform 64 B - 64 KiB values packed
+    back to back up to 4 GiB (bench.py's generator and seed), whole tree vs the C
+    oracle: the work-queue kernel, the length sort and the split on the bench's
+    own batch."""
+    import torch
+    import bench
+    _lib, ctx = nkv
+    L = _lib.lib()
+    lens, off = bench.mixed_lengths(4 << 30, bench.SEED_MIXED)
+    n, nbytes = len(lens), int(lens.sum())
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    try:
+        d = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+        _lib.check(L.nkv_fill_splitmix64_dev(ctx.h, d.data_ptr(), nbytes, bench.SEED_MIXED))
+        d_off = torch.from_numpy(off.view(np.int64)).cuda()
+        d_len = torch.from_numpy(lens.view(np.int64)).cuda()
+        d_nodes = torch.zeros(L.nkv_total_nodes(n) * 20, dtype=torch.uint8, device="cuda")
+        _lib.check(L.nkv_tree_from_values_dev(ctx.h, d.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n,
+                                              d_nodes.data_ptr()))
+        got = d_nodes.cpu().numpy().reshape(-1, 20)
+        del d
+        torch.cuda.empty_cache()
+    finally:
+        ctx.set_stream(_lib._OWN)
+    host = oracle.splitmix64_bytes(nbytes, bench.SEED_MIXED)
+    want = oracle.tree_from_digests(oracle.leaf_hashes(host, off, lens, threads=16))
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("verify", [False, True])
+def test_full_size_records_bit_exact(nkv, oracle, verify):
+    """The SSTable form of configs[1] at full size: 1 Mi records of TotalSize
+    4,096 (16-B key, 4,050-B Value at record + 46) in one Data stream, hashed in
+    place (nkv_tree_from_records_dev) or checked and hashed in one pass
+    (nkv_tree_verify_records_dev, stored Crcs right, then one corrupted)."""
+    import torch
+    import bench
+    _lib, ctx = nkv
+    L = _lib.lib()
+    n, rb, ks = 1 << 20, 4096, 16
+    vlen = rb - 30 - ks
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    try:
+        data = torch.empty(n * rb, dtype=torch.uint8, device="cuda")
+        _lib.check(L.nkv_fill_splitmix64_dev(ctx.h, data.data_ptr(), n * rb, bench.SEED))
+        v = data.view(n, rb)
+        v[:, 14:22] = torch.from_numpy(np.frombuffer(np.uint64(ks).tobytes(), np.uint8).copy()).cuda()
+        v[:, 22:30] = torch.from_numpy(np.frombuffer(np.uint64(vlen).tobytes(), np.uint8).copy()).cuda()
+        d_roff = torch.arange(n, dtype=torch.int64, device="cuda") * rb
+        nodes = torch.zeros(L.nkv_total_nodes(n) * 20, dtype=torch.uint8, device="cuda")
+        if verify:
+            d_crc = torch.empty(n, dtype=torch.int32, device="cuda")
+            stats = torch.zeros(3, dtype=torch.int64, device="cuda")
+            _lib.check(L.nkv_record_crc_dev(ctx.h, data.data_ptr(), n * rb, d_roff.data_ptr(), n, d_crc.data_ptr(),
+                                            stats.data_ptr()))
+            v[:, 0:4] = d_crc.view(torch.uint8).view(n, 4)
+            stats.zero_()
+            _lib.check(L.nkv_tree_verify_records_dev(ctx.h, data.data_ptr(), n * rb, d_roff.data_ptr(), n,
+                                                     nodes.data_ptr(), None, stats.data_ptr()))
+            assert stats.cpu().tolist() == [0, -1, 0]
+        else:
+            err = torch.zeros(1, dtype=torch.int32, device="cuda")
+            _lib.check(L.nkv_tree_from_records_dev(ctx.h, data.data_ptr(), n * rb, d_roff.data_ptr(), n,
+                                                   nodes.data_ptr(), err.data_ptr()))
+            assert int(err.item()) == 0
+        got = nodes.cpu().numpy().reshape(-1, 20)
+        if verify:  # one flipped Value byte in record 777,777: one bad Crc, the tree follows the bytes
+            v[777777, 3000] ^= 1
+            stats.zero_()
+            _lib.check(L.nkv_tree_verify_records_dev(ctx.h, data.data_ptr(), n * rb, d_roff.data_ptr(), n,
+                                                     nodes.data_ptr(), None, stats.data_ptr()))
+            assert stats.cpu().tolist() == [1, 777777, 0]
+            v[777777, 3000] ^= 1
+        host = data.cpu().numpy()
+        del data, v
+        torch.cuda.empty_cache()
+    finally:
+        ctx.set_stream(_lib._OWN)
+    voff = np.arange(n, dtype=np.uint64) * rb + 30 + ks
+    want = oracle.tree_from_digests(oracle.leaf_hashes(host, voff, np.full(n, vlen, np.uint64), threads=16))
+    assert np.array_equal(got, want)
