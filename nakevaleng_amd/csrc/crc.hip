@@ -70,8 +70,7 @@ __device__ __forceinline__ uint32_t crc_span(const uint8_t* s, uint64_t len, con
                                     v[2].x, v[2].y, v[2].z, v[2].w, v[3].x, v[3].y, v[3].z, v[3].w};
             const uint64_t b0 = A + 64ull * c;
             if (b0 >= s4 && b0 + 64 <= e4) {
-#pragma unroll
-                for (int j = 0; j < 16; ++j) crc = crc_word<C>(crc, w[j], tab);
+                crc = crc_block16<C>(crc, w, tab);
             } else {
                 const uint64_t lo = s4 > b0 ? (s4 - b0) >> 2 : 0;
                 const uint64_t hi = e4 - b0 >= 64 ? 16 : (e4 - b0) >> 2;
@@ -138,8 +137,7 @@ __device__ __forceinline__ uint32_t crc_span_ring(const uint8_t* s, uint64_t len
                                     v[2].x, v[2].y, v[2].z, v[2].w, v[3].x, v[3].y, v[3].z, v[3].w};
             const uint64_t b0 = 64ull * c;  // chunk start, relative
             if (b0 >= o && b0 + 64 <= e) {
-#pragma unroll
-                for (int j = 0; j < 16; ++j) crc = crc_word<C>(crc, w[j], tab);
+                crc = crc_block16<C>(crc, w, tab);
             } else {
 #pragma unroll
                 for (int j = 0; j < 16; ++j) {
@@ -292,22 +290,10 @@ __device__ __forceinline__ uint32_t crc_group_span(const uint8_t* s, uint64_t L,
 #pragma unroll
                 for (int i = 0; i < 4; ++i) v[i] = q[i];
                 uint32_t a = c == 0 ? 0xFFFFFFFFu : 0u, b = 0u, g = 0u, d = 0u;
-                a = crc_word<C>(a, v[0].x, tab);
-                b = crc_word<C>(b, v[1].x, tab);
-                g = crc_word<C>(g, v[2].x, tab);
-                d = crc_word<C>(d, v[3].x, tab);
-                a = crc_word<C>(a, v[0].y, tab);
-                b = crc_word<C>(b, v[1].y, tab);
-                g = crc_word<C>(g, v[2].y, tab);
-                d = crc_word<C>(d, v[3].y, tab);
-                a = crc_word<C>(a, v[0].z, tab);
-                b = crc_word<C>(b, v[1].z, tab);
-                g = crc_word<C>(g, v[2].z, tab);
-                d = crc_word<C>(d, v[3].z, tab);
-                a = crc_word<C>(a, v[0].w, tab);
-                b = crc_word<C>(b, v[1].w, tab);
-                g = crc_word<C>(g, v[2].w, tab);
-                d = crc_word<C>(d, v[3].w, tab);
+                a = crc_quad<C>(a, v[0], tab);
+                b = crc_quad<C>(b, v[1], tab);
+                g = crc_quad<C>(g, v[2], tab);
+                d = crc_quad<C>(d, v[3], tab);
                 const uint32_t* s16 = sh + 5 * 1024;
                 st = lds_advance(s16, lds_advance(s16, lds_advance(s16, a) ^ b) ^ g) ^ d;
             } else {

@@ -38,6 +38,52 @@ __device__ __forceinline__ uint32_t crc_word(uint32_t crc, uint32_t w, const uin
            crc_lut<C>(tab, 1, (x >> 16) & 0xFFu) ^ crc_lut<C>(tab, 0, x >> 24);
 }
 
+// a ^ b ^ c in one v_bitop3_b32 (the backend leaves xor chains as two-input v_xor)
+__device__ __forceinline__ uint32_t crc_xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+// The same step carried in x = crc ^ w form: from this word's x and the next
+// word, the next x (six VALU: four byte indices, two three-input XORs, and no
+// separate crc ^ w); crc_x_last gives the crc after the last word.
+template <int C>
+__device__ __forceinline__ uint32_t crc_x_next(uint32_t x, uint32_t w_next, const uint32_t* tab) {
+    return crc_xor3(crc_xor3(crc_lut<C>(tab, 3, x & 0xFFu), crc_lut<C>(tab, 2, (x >> 8) & 0xFFu),
+                     crc_lut<C>(tab, 1, (x >> 16) & 0xFFu)),
+                crc_lut<C>(tab, 0, x >> 24), w_next);
+}
+template <int C>
+__device__ __forceinline__ uint32_t crc_x_last(uint32_t x, const uint32_t* tab) {
+    return crc_xor3(crc_lut<C>(tab, 3, x & 0xFFu), crc_lut<C>(tab, 2, (x >> 8) & 0xFFu),
+                crc_lut<C>(tab, 1, (x >> 16) & 0xFFu)) ^
+           crc_lut<C>(tab, 0, x >> 24);
+}
+
+// 16 little-endian words (one 64-byte block) in x form; NKV_CRC_WORD_STEP
+// builds the plain word steps instead (A/B only)
+template <int C>
+__device__ __forceinline__ uint32_t crc_block16(uint32_t crc, const uint32_t w[16], const uint32_t* tab) {
+#ifdef NKV_CRC_WORD_STEP
+#pragma unroll
+    for (int i = 0; i < 16; ++i) crc = crc_word<C>(crc, w[i], tab);
+    return crc;
+#else
+    uint32_t x = crc ^ w[0];
+#pragma unroll
+    for (int i = 1; i < 16; ++i) x = crc_x_next<C>(x, w[i], tab);
+    return crc_x_last<C>(x, tab);
+#endif
+}
+
+template <int C>
+__device__ __forceinline__ uint32_t crc_quad(uint32_t crc, uint4 v, const uint32_t* tab) {
+#ifdef NKV_CRC_WORD_STEP
+    return crc_word<C>(crc_word<C>(crc_word<C>(crc_word<C>(crc, v.x, tab), v.y, tab), v.z, tab), v.w, tab);
+#else
+    return crc_x_last<C>(crc_x_next<C>(crc_x_next<C>(crc_x_next<C>(crc ^ v.x, v.y, tab), v.z, tab), v.w, tab), tab);
+#endif
+}
+
 template <int C>
 __device__ __forceinline__ uint32_t crc_byte(uint32_t crc, uint32_t b, const uint32_t* tab) {
     return crc_lut<C>(tab, 0, (crc ^ b) & 0xFFu) ^ (crc >> 8);
