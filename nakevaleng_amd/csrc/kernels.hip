@@ -1700,33 +1700,56 @@ __global__ __launch_bounds__(kBlock) void k_len_scatter(const uint64_t* __restri
 // ---------------------------------------------------------------------------
 // K3: BFS image.  Levels are written top-down; level L contributes 21 bytes
 // per node (0x00 flag + digest) plus one 0x01 byte for the pad of an odd
-// level below the top.  Each thread produces 16 consecutive image bytes.
+// level below the top.  One workgroup builds one 4 KiB segment of the image
+// in LDS: for every level that overlaps the segment, each thread takes nodes
+// of it (one 64-bit division by 21 per level, not per byte) and writes their
+// 21-byte records, clipped to the segment, as byte stores into LDS; then each
+// thread stores 16 aligned bytes of the segment.  A record that straddles two
+// segments is written, clipped, by both workgroups.
+constexpr uint32_t kBfsSeg = kBlock * 16;
 __global__ __launch_bounds__(kBlock) void k_bfs_image(const uint8_t* __restrict__ nodes,
                                                        BfsLayout lay, uint8_t* __restrict__ img) {
-    const uint64_t p0 = (uint64_t(blockIdx.x) * kBlock + threadIdx.x) * 16;
-    if (p0 >= lay.total) return;
-    int L = 0;  // index into the image-ordered tables (0 = top level)
-    while (L + 1 < lay.nlev && lay.img_start[L + 1] <= p0) ++L;
-    uint32_t wv[4] = {0u, 0u, 0u, 0u};
-    const int nb = (lay.total - p0) < 16 ? int(lay.total - p0) : 16;
-    for (int b = 0; b < nb; ++b) {
-        const uint64_t p = p0 + b;
-        while (L + 1 < lay.nlev && lay.img_start[L + 1] <= p) ++L;
-        const uint64_t rel = p - lay.img_start[L];
-        uint32_t byte;
-        if (rel < 21 * lay.count[L]) {
-            const uint64_t node = rel / 21;
-            const uint32_t r = uint32_t(rel - node * 21);
-            byte = r == 0 ? 0u : nodes[20 * (lay.node_start[L] + node) + r - 1];
-        } else {
-            byte = 0x01u;  // MERKLE_NODE_EMPTY pad (merklenode.go:11, merkletree.go:32-34)
+    __shared__ __attribute__((aligned(16))) uint8_t seg[kBfsSeg];
+    const uint64_t s0 = uint64_t(blockIdx.x) * kBfsSeg;
+    if (s0 >= lay.total) return;
+    const uint64_t s1 = min(s0 + kBfsSeg, lay.total);
+    for (int L = 0; L < lay.nlev; ++L) {
+        const uint64_t A = lay.img_start[L];
+        const uint64_t E = A + 21 * lay.count[L];           // end of the node records
+        const uint64_t Z = L + 1 < lay.nlev ? lay.img_start[L + 1] : lay.total;  // E or E + 1 (pad)
+        if (Z <= s0 || A >= s1) continue;
+        if (E < Z && E >= s0 && E < s1 && threadIdx.x == 0)
+            seg[E - s0] = 0x01u;  // MERKLE_NODE_EMPTY pad (merklenode.go:11, merkletree.go:32-34)
+        if (E <= s0) continue;
+        const uint64_t k0 = s0 > A ? (s0 - A) / 21 : 0;
+        const uint64_t k1 = (min(s1, E) - 1 - A) / 21;  // last node with a byte in the segment
+        for (uint64_t k = k0 + threadIdx.x; k <= k1; k += kBlock) {
+            const uint32_t* d = reinterpret_cast<const uint32_t*>(nodes + 20 * (lay.node_start[L] + k));
+            uint32_t w[5];
+#pragma unroll
+            for (int i = 0; i < 5; ++i) w[i] = d[i];
+            const int64_t pos = int64_t(A + 21 * k) - int64_t(s0);  // record start in the segment
+            if (pos >= 0 && pos + 21 <= int64_t(kBfsSeg)) {
+                uint8_t* o = seg + pos;
+                o[0] = 0u;
+#pragma unroll
+                for (int j = 0; j < 20; ++j) o[1 + j] = uint8_t(w[j >> 2] >> (8 * (j & 3)));
+            } else {
+#pragma unroll
+                for (int j = 0; j < 21; ++j) {
+                    const int64_t q = pos + j;
+                    if (q >= 0 && q < int64_t(kBfsSeg))
+                        seg[q] = j == 0 ? 0u : uint8_t(w[(j - 1) >> 2] >> (8 * ((j - 1) & 3)));
+                }
+            }
         }
-        wv[b >> 2] |= byte << (8 * (b & 3));
     }
-    if (nb == 16) {
-        *reinterpret_cast<uint4*>(img + p0) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+    __syncthreads();
+    const uint64_t p0 = s0 + 16 * threadIdx.x;
+    if (p0 + 16 <= s1) {
+        *reinterpret_cast<uint4*>(img + p0) = *reinterpret_cast<const uint4*>(seg + 16 * threadIdx.x);
     } else {
-        for (int b = 0; b < nb; ++b) img[p0 + b] = uint8_t(wv[b >> 2] >> (8 * (b & 3)));
+        for (uint64_t p = p0; p < s1; ++p) img[p] = seg[p - s0];
     }
 }
 
@@ -2128,8 +2151,9 @@ hipError_t launch_reduce(uint8_t* nodes, uint64_t n, int from_level, int top, hi
 
 hipError_t launch_bfs_image(const uint8_t* nodes, const BfsLayout& lay, uint8_t* img,
                             hipStream_t s) {
-    const uint64_t threads = (lay.total + 15) / 16;
-    hipLaunchKernelGGL(k_bfs_image, dim3(grid_for(threads)), dim3(kBlock), 0, s, nodes, lay, img);
+    const uint64_t segs = (lay.total + kBfsSeg - 1) / kBfsSeg;
+    if (segs == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_bfs_image, dim3(uint32_t(segs)), dim3(kBlock), 0, s, nodes, lay, img);
     return hipGetLastError();
 }
 

@@ -406,3 +406,27 @@ def test_full_size_records_bit_exact(nkv, oracle, verify):
     voff = np.arange(n, dtype=np.uint64) * rb + 30 + ks
     want = oracle.tree_from_digests(oracle.leaf_hashes(host, voff, np.full(n, vlen, np.uint64), threads=16))
     assert np.array_equal(got, want)
+
+
+def test_bfs_image_segment_edges(nkv, oracle):
+    """k_bfs_image builds the image in 4 KiB LDS segments: trees whose records and
+    pad bytes straddle segment edges at every offset, against the oracle."""
+    import torch
+    _lib, ctx = nkv
+    L = _lib.lib()
+    ns = [4, 6, 7, 9, 97, 195, 196, 197, 390, 391, 392, 4095, 4097, 8191, 65537, 131071, 262147]
+    ns += [int(x) for x in np.random.default_rng(5).integers(2, 20000, 12)]
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    try:
+        for n in ns:
+            leaf20 = oracle.splitmix64_bytes(20 * n, n)
+            want = oracle.tree_from_digests(leaf20.reshape(n, 20))
+            d_nodes = torch.from_numpy(want.reshape(-1).copy()).cuda()
+            d_img = torch.full((L.nkv_bfs_size(n) + 64,), 0xAB, dtype=torch.uint8, device="cuda")
+            _lib.check(L.nkv_bfs_image_dev(ctx.h, d_nodes.data_ptr(), n, d_img.data_ptr()))
+            got = d_img.cpu().numpy().tobytes()
+            size = L.nkv_bfs_size(n)
+            assert got[:size] == oracle.bfs_image(want, n), n
+            assert got[size:] == b"\xab" * 64, n  # nothing written past the image
+    finally:
+        ctx.set_stream(_lib._OWN)
