@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <new>
 #include <vector>
 
 #include "host_stage.hpp"
@@ -136,6 +137,19 @@ int st(hipError_t e) {
         if (_rc != NKV_OK) return _rc; \
     } while (0)
 #define HIPTRY(x) TRY(st(x))
+// Every C-ABI entry is a function-try-block: a host allocation or thread start
+// that throws inside the library becomes a status code, never an exception
+// crossing the C boundary (cgo / ctypes callers cannot catch it).
+#define NKV_CATCH                      \
+    catch (const std::bad_alloc&) {    \
+        return NKV_ERR_NOMEM;          \
+    }                                  \
+    catch (...) {                      \
+        return NKV_ERR_DEVICE;         \
+    }
+// Largest batch: leaf indices are 32-bit in the sort and queue kernels
+// (2^31 - 1 values of 4 KiB would be 8 TiB, far beyond one GPU's HBM).
+constexpr uint64_t kMaxN = 0x7fffffffull;
 
 int bind(nkv_ctx* c) {
     if (!c) return NKV_ERR_INVALID;
@@ -436,7 +450,7 @@ const char* nkv_strerror(int s) {
     }
 }
 
-int nkv_device_count(int* count) {
+int nkv_device_count(int* count) try {
     if (!count) return NKV_ERR_INVALID;
     int n = 0;
     hipError_t e = hipGetDeviceCount(&n);
@@ -447,9 +461,9 @@ int nkv_device_count(int* count) {
     }
     *count = n;
     return NKV_OK;
-}
+} NKV_CATCH
 
-int nkv_ctx_create(int device, nkv_ctx** out) {
+int nkv_ctx_create(int device, nkv_ctx** out) try {
     if (!out) return NKV_ERR_INVALID;
     *out = nullptr;
     int cnt = 0;
@@ -475,7 +489,7 @@ int nkv_ctx_create(int device, nkv_ctx** out) {
         c->simds = uint32_t(prop.multiProcessorCount) * 4;
     *out = c;
     return NKV_OK;
-}
+} NKV_CATCH
 
 void nkv_ctx_destroy(nkv_ctx* c) {
     if (!c) return;
@@ -492,19 +506,19 @@ void nkv_ctx_destroy(nkv_ctx* c) {
     delete c;
 }
 
-int nkv_ctx_set_stream(nkv_ctx* c, void* s) {
+int nkv_ctx_set_stream(nkv_ctx* c, void* s) try {
     TRY(bind(c));
     c->stream = static_cast<hipStream_t>(s);  // NULL = the device's null stream
     return NKV_OK;
-}
+} NKV_CATCH
 
-int nkv_ctx_use_own_stream(nkv_ctx* c) {
+int nkv_ctx_use_own_stream(nkv_ctx* c) try {
     TRY(bind(c));
     c->stream = c->own;
     return NKV_OK;
-}
+} NKV_CATCH
 
-int nkv_ctx_set_option(nkv_ctx* c, int key, int64_t value) {
+int nkv_ctx_set_option(nkv_ctx* c, int key, int64_t value) try {
     TRY(bind(c));
     switch (key) {
         case NKV_OPT_LEAF_LOAD:
@@ -555,22 +569,22 @@ int nkv_ctx_set_option(nkv_ctx* c, int key, int64_t value) {
         default:
             return NKV_ERR_INVALID;
     }
-}
+} NKV_CATCH
 
-int nkv_ctx_sync(nkv_ctx* c) {
+int nkv_ctx_sync(nkv_ctx* c) try {
     TRY(bind(c));
     return st(hipStreamSynchronize(c->stream));
-}
+} NKV_CATCH
 
-int nkv_ctx_set_timing(nkv_ctx* c, int enable) {
+int nkv_ctx_set_timing(nkv_ctx* c, int enable) try {
     TRY(bind(c));
     c->timing = enable != 0;
     c->timed = false;
     c->ring_used = 0;
     return NKV_OK;
-}
+} NKV_CATCH
 
-int nkv_ctx_timing_summary(nkv_ctx* c, int* calls, float* leaf_ms_total, float* reduce_ms_total) {
+int nkv_ctx_timing_summary(nkv_ctx* c, int* calls, float* leaf_ms_total, float* reduce_ms_total) try {
     TRY(bind(c));
     if (!calls || !leaf_ms_total || !reduce_ms_total) return NKV_ERR_INVALID;
     const size_t k = c->ring_used / 3;
@@ -587,9 +601,9 @@ int nkv_ctx_timing_summary(nkv_ctx* c, int* calls, float* leaf_ms_total, float* 
     *leaf_ms_total = float(a);
     *reduce_ms_total = float(b);
     return NKV_OK;
-}
+} NKV_CATCH
 
-int nkv_ctx_last_timing(nkv_ctx* c, float* leaf_ms, float* reduce_ms) {
+int nkv_ctx_last_timing(nkv_ctx* c, float* leaf_ms, float* reduce_ms) try {
     TRY(bind(c));
     if (!c->timed) return NKV_ERR_INVALID;
     hipEvent_t* ev = &c->ring[c->ring_used - 3];
@@ -600,7 +614,7 @@ int nkv_ctx_last_timing(nkv_ctx* c, float* leaf_ms, float* reduce_ms) {
     if (leaf_ms) *leaf_ms = a;
     if (reduce_ms) *reduce_ms = b;
     return NKV_OK;
-}
+} NKV_CATCH
 
 // ---- shape ----
 int nkv_num_levels(uint64_t n) { return levels_of(n); }
@@ -614,7 +628,7 @@ uint64_t nkv_total_nodes(uint64_t n) { return total_of(n); }
 uint64_t nkv_bfs_size(uint64_t n) { return n == 0 ? 0 : layout_of(counts_of(n)).total; }
 
 // ---- pinned arena ----
-int nkv_host_alloc(nkv_ctx* c, uint64_t bytes, void** out) {
+int nkv_host_alloc(nkv_ctx* c, uint64_t bytes, void** out) try {
     if (!out) return NKV_ERR_INVALID;
     TRY(bind(c));
     if (hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) {
@@ -623,17 +637,18 @@ int nkv_host_alloc(nkv_ctx* c, uint64_t bytes, void** out) {
         return NKV_ERR_NOMEM;
     }
     return NKV_OK;
-}
+} NKV_CATCH
 
-int nkv_host_free(nkv_ctx* c, void* p) {
+int nkv_host_free(nkv_ctx* c, void* p) try {
     TRY(bind(c));
     return p ? st(hipHostFree(p)) : NKV_OK;
-}
+} NKV_CATCH
 
 // ---- host-buffer API ----
 int nkv_leaf_hash(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint64_t* len,
-                  uint64_t n, uint8_t* out20) {
+                  uint64_t n, uint8_t* out20) try {
     TRY(bind(c));
+    if (n > kMaxN) return NKV_ERR_INVALID;
     if (n == 0) return NKV_OK;
     if (!base || !off || !len || !out20) return NKV_ERR_INVALID;
     TRY(stage_values(c, base, off, len, n));
@@ -643,11 +658,12 @@ int nkv_leaf_hash(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const ui
                    static_cast<const uint64_t*>(c->d_len.p), n, true, nodes, len));
     HIPTRY(c->stage.download(out20, nodes, 20 * n, c->stream));
     return st(hipStreamSynchronize(c->stream));
-}
+} NKV_CATCH
 
 int nkv_tree_build(nkv_ctx* c, const uint8_t* leaf20, uint64_t n, uint8_t* root20,
-                   uint8_t* nodes_out, uint8_t* img_out) {
+                   uint8_t* nodes_out, uint8_t* img_out) try {
     TRY(bind(c));
+    if (n > kMaxN) return NKV_ERR_INVALID;
     if (n == 0) return NKV_ERR_EMPTY;
     if (!leaf20) return NKV_ERR_INVALID;
     TRY(grow(c->d_nodes, 20 * total_of(n)));
@@ -655,11 +671,12 @@ int nkv_tree_build(nkv_ctx* c, const uint8_t* leaf20, uint64_t n, uint8_t* root2
     HIPTRY(c->stage.upload(leaf20, 20 * n, nodes, c->stream));
     HIPTRY(launch_reduce(nodes, n, 0, levels_of(n) - 1, c->stream));
     return finish_tree(c, nodes, n, root20, nodes_out, img_out);
-}
+} NKV_CATCH
 
 int nkv_tree_from_values(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint64_t* len,
-                         uint64_t n, uint8_t* root20, uint8_t* nodes_out, uint8_t* img_out) {
+                         uint64_t n, uint8_t* root20, uint8_t* nodes_out, uint8_t* img_out) try {
     TRY(bind(c));
+    if (n > kMaxN) return NKV_ERR_INVALID;
     if (n == 0) return NKV_ERR_EMPTY;
     if (!base || !off || !len) return NKV_ERR_INVALID;
     TRY(stage_values(c, base, off, len, n));
@@ -669,7 +686,7 @@ int nkv_tree_from_values(nkv_ctx* c, const uint8_t* base, const uint64_t* off, c
                                 static_cast<const uint64_t*>(c->d_off.p),
                                 static_cast<const uint64_t*>(c->d_len.p), n, true, nodes, len));
     return finish_tree(c, nodes, n, root20, nodes_out, img_out);
-}
+} NKV_CATCH
 
 uint64_t nkv_generic_bfs_size(const uint64_t* len, uint64_t n) {
     if (n == 0 || !len) return 0;
@@ -680,8 +697,9 @@ uint64_t nkv_generic_bfs_size(const uint64_t* len, uint64_t n) {
 }
 
 int nkv_tree_generic(nkv_ctx* c, const uint8_t* data, const uint64_t* off, const uint64_t* len,
-                     uint64_t n, uint8_t* root20, uint8_t* upper_out, uint8_t* img_out) {
+                     uint64_t n, uint8_t* root20, uint8_t* upper_out, uint8_t* img_out) try {
     TRY(bind(c));
+    if (n > kMaxN) return NKV_ERR_INVALID;
     if (n == 0) return NKV_ERR_EMPTY;
     if (!data || !off || !len) return NKV_ERR_INVALID;
     // Level 1 node i = SHA-1(leaf[2i].Data || leaf[2i+1].Data) (merkletree.go:44-46;
@@ -745,11 +763,12 @@ int nkv_tree_generic(nkv_ctx* c, const uint8_t* data, const uint64_t* off, const
         if (n & 1) *q++ = NKV_MERKLE_NODE_EMPTY;
     }
     return NKV_OK;
-}
+} NKV_CATCH
 
 int nkv_tree_validate(nkv_ctx* c, const uint8_t* leaf_data, const uint64_t* off, const uint64_t* len,
-                      uint64_t n, const uint8_t* root20, int* ok) {
+                      uint64_t n, const uint8_t* root20, int* ok) try {
     TRY(bind(c));
+    if (n > kMaxN) return NKV_ERR_INVALID;
     if (!ok) return NKV_ERR_INVALID;
     *ok = 0;
     if (n == 0) return NKV_ERR_EMPTY;  // New never builds an empty tree (merkletree.go:19-21)
@@ -776,12 +795,13 @@ int nkv_tree_validate(nkv_ctx* c, const uint8_t* leaf_data, const uint64_t* off,
     }
     *ok = memcmp(got, root20, NKV_DIGEST_SIZE) == 0;
     return NKV_OK;
-}
+} NKV_CATCH
 
 int nkv_tree_from_records(nkv_ctx* c, const uint8_t* stream, uint64_t stream_len,
                           const uint64_t* rec_size, uint64_t n, uint8_t* root20,
-                          uint8_t* nodes_out, uint8_t* img_out) {
+                          uint8_t* nodes_out, uint8_t* img_out) try {
     TRY(bind(c));
+    if (n > kMaxN) return NKV_ERR_INVALID;
     if (n == 0) return NKV_ERR_EMPTY;
     if (!stream || !rec_size) return NKV_ERR_INVALID;
     if (!records_fit(rec_size, n, stream_len)) return NKV_ERR_INVALID;
@@ -800,11 +820,12 @@ int nkv_tree_from_records(nkv_ctx* c, const uint8_t* stream, uint64_t stream_len
     HIPTRY(hipStreamSynchronize(c->stream));
     if (h) return NKV_ERR_INVALID;
     return finish_tree(c, nodes, n, root20, nodes_out, img_out);
-}
+} NKV_CATCH
 
 int nkv_record_crc(nkv_ctx* c, const uint8_t* stream, uint64_t stream_len, const uint64_t* rec_size,
-                   uint64_t n, uint32_t* crc_out, uint64_t* n_bad, uint64_t* first_bad) {
+                   uint64_t n, uint32_t* crc_out, uint64_t* n_bad, uint64_t* first_bad) try {
     TRY(bind(c));
+    if (n > kMaxN) return NKV_ERR_INVALID;
     if (n_bad) *n_bad = 0;
     if (first_bad) *first_bad = ~0ull;
     if (n == 0) return NKV_OK;
@@ -829,9 +850,9 @@ int nkv_record_crc(nkv_ctx* c, const uint8_t* stream, uint64_t stream_len, const
     if (crc_out) HIPTRY(c->stage.download(reinterpret_cast<uint8_t*>(crc_out), reinterpret_cast<const uint8_t*>(d_crc),
                                           4 * n, c->stream));
     return NKV_OK;
-}
+} NKV_CATCH
 
-int nkv_bloom_params(uint64_t n, double p, uint32_t* m, uint32_t* k) {
+int nkv_bloom_params(uint64_t n, double p, uint32_t* m, uint32_t* k) try {
     if (!m || !k || n == 0 || !(p > 0.0 && p < 1.0)) return NKV_ERR_INVALID;
     const double ln2 = std::log(2.0);  // bloomfilter.go:18-24
     const double mm = std::ceil(double(n) * std::fabs(std::log(p)) / std::pow(ln2, 2.0));
@@ -839,13 +860,14 @@ int nkv_bloom_params(uint64_t n, double p, uint32_t* m, uint32_t* k) {
     *m = uint32_t(mm);
     *k = uint32_t(std::ceil((double(*m) / double(n)) * ln2));
     return NKV_OK;
-}
+} NKV_CATCH
 
 static uint64_t bloom_words(uint32_t m) { return (uint64_t(m) + 31) / 32; }
 
 int nkv_bloom_build(nkv_ctx* c, const uint8_t* keys, const uint64_t* off, const uint64_t* len, uint64_t n,
-                    uint32_t m, uint32_t k, uint32_t seed0, uint8_t* bits_out) {
+                    uint32_t m, uint32_t k, uint32_t seed0, uint8_t* bits_out) try {
     TRY(bind(c));
+    if (n > kMaxN) return NKV_ERR_INVALID;
     if (m == 0 || !bits_out || (n && (!keys || !off || !len))) return NKV_ERR_INVALID;
     const uint64_t nbytes = (uint64_t(m) + 7) / 8, wbytes = 4 * bloom_words(m);
     TRY(grow(c->d_img, wbytes));
@@ -868,11 +890,12 @@ int nkv_bloom_build(nkv_ctx* c, const uint8_t* keys, const uint64_t* off, const 
     }
     HIPTRY(c->stage.download(bits_out, static_cast<const uint8_t*>(c->d_img.p), nbytes, c->stream));
     return st(hipStreamSynchronize(c->stream));
-}
+} NKV_CATCH
 
 int nkv_bloom_from_records(nkv_ctx* c, const uint8_t* stream, uint64_t stream_len, const uint64_t* rec_size,
-                           uint64_t n, uint32_t m, uint32_t k, uint32_t seed0, uint8_t* bits_out) {
+                           uint64_t n, uint32_t m, uint32_t k, uint32_t seed0, uint8_t* bits_out) try {
     TRY(bind(c));
+    if (n > kMaxN) return NKV_ERR_INVALID;
     if (m == 0 || !bits_out || (n && (!stream || !rec_size))) return NKV_ERR_INVALID;
     const uint64_t nbytes = (uint64_t(m) + 7) / 8, wbytes = 4 * bloom_words(m);
     TRY(grow(c->d_img, wbytes));
@@ -887,9 +910,9 @@ int nkv_bloom_from_records(nkv_ctx* c, const uint8_t* stream, uint64_t stream_le
     }
     HIPTRY(c->stage.download(bits_out, static_cast<const uint8_t*>(c->d_img.p), nbytes, c->stream));
     return st(hipStreamSynchronize(c->stream));
-}
+} NKV_CATCH
 
-int nkv_write_file(const char* fname, const uint8_t* data, uint64_t len) {
+int nkv_write_file(const char* fname, const uint8_t* data, uint64_t len) try {
     if (!fname || (!data && len)) return NKV_ERR_INVALID;
     int fd = open(fname, O_WRONLY | O_CREAT, 0666);  // no O_TRUNC: merkletree.go:68
     if (fd < 0) return NKV_ERR_IO;
@@ -903,46 +926,51 @@ int nkv_write_file(const char* fname, const uint8_t* data, uint64_t len) {
         done += uint64_t(w);
     }
     return close(fd) == 0 ? NKV_OK : NKV_ERR_IO;
-}
+} NKV_CATCH
 
 // ---- device-resident API ----
 int nkv_leaf_hash_dev(nkv_ctx* c, const void* d_base, const uint64_t* d_off,
-                      const uint64_t* d_len, uint64_t n, void* d_nodes) {
+                      const uint64_t* d_len, uint64_t n, void* d_nodes) try {
     TRY(bind(c));
+    if (n > kMaxN) return NKV_ERR_INVALID;
     if (n == 0) return NKV_OK;
     if (!d_base || !d_off || !d_len || !d_nodes) return NKV_ERR_INVALID;
     return leaf_level(c, static_cast<const uint8_t*>(d_base), d_off, d_len, n, false,
                       static_cast<uint8_t*>(d_nodes), nullptr);
-}
+} NKV_CATCH
 
 int nkv_leaf_hash_strided_dev(nkv_ctx* c, const void* d_base, uint64_t stride, uint64_t len,
-                              uint64_t n, void* d_nodes) {
+                              uint64_t n, void* d_nodes) try {
     TRY(bind(c));
+    if (n > kMaxN) return NKV_ERR_INVALID;
     if (n == 0) return NKV_OK;
     if (!d_base || !d_nodes) return NKV_ERR_INVALID;
     return st(launch_leaf_strided(static_cast<const uint8_t*>(d_base), stride, len, n,
                                   c->leaf_load, static_cast<uint8_t*>(d_nodes), c->stream));
-}
+} NKV_CATCH
 
-int nkv_tree_reduce_dev(nkv_ctx* c, void* d_nodes, uint64_t n) {
+int nkv_tree_reduce_dev(nkv_ctx* c, void* d_nodes, uint64_t n) try {
     TRY(bind(c));
+    if (n > kMaxN) return NKV_ERR_INVALID;
     if (n == 0) return NKV_ERR_EMPTY;
     if (!d_nodes) return NKV_ERR_INVALID;
     return st(launch_reduce(static_cast<uint8_t*>(d_nodes), n, 0, levels_of(n) - 1, c->stream));
-}
+} NKV_CATCH
 
 int nkv_tree_from_values_dev(nkv_ctx* c, const void* d_base, const uint64_t* d_off,
-                             const uint64_t* d_len, uint64_t n, void* d_nodes) {
+                             const uint64_t* d_len, uint64_t n, void* d_nodes) try {
     TRY(bind(c));
+    if (n > kMaxN) return NKV_ERR_INVALID;
     if (n == 0) return NKV_ERR_EMPTY;
     if (!d_base || !d_off || !d_len || !d_nodes) return NKV_ERR_INVALID;
     return tree_from_device_values(c, static_cast<const uint8_t*>(d_base), d_off, d_len, n, false,
                                    static_cast<uint8_t*>(d_nodes));
-}
+} NKV_CATCH
 
 int nkv_tree_from_strided_dev(nkv_ctx* c, const void* d_base, uint64_t stride, uint64_t len,
-                              uint64_t n, void* d_nodes) {
+                              uint64_t n, void* d_nodes) try {
     TRY(bind(c));
+    if (n > kMaxN) return NKV_ERR_INVALID;
     if (n == 0) return NKV_ERR_EMPTY;
     if (!d_base || !d_nodes) return NKV_ERR_INVALID;
     uint8_t* nodes = static_cast<uint8_t*>(d_nodes);
@@ -953,32 +981,35 @@ int nkv_tree_from_strided_dev(nkv_ctx* c, const void* d_base, uint64_t stride, u
     TRY(mark(c, 1));
     HIPTRY(launch_reduce(nodes, n, 0, top, c->stream));
     return mark(c, 2);
-}
+} NKV_CATCH
 
-int nkv_bfs_image_dev(nkv_ctx* c, const void* d_nodes, uint64_t n, void* d_img) {
+int nkv_bfs_image_dev(nkv_ctx* c, const void* d_nodes, uint64_t n, void* d_img) try {
     TRY(bind(c));
+    if (n > kMaxN) return NKV_ERR_INVALID;
     if (n == 0) return NKV_ERR_EMPTY;
     if (!d_nodes || !d_img) return NKV_ERR_INVALID;
     BfsLayout lay = layout_of(counts_of(n));
     return st(launch_bfs_image(static_cast<const uint8_t*>(d_nodes), lay,
                                static_cast<uint8_t*>(d_img), c->stream));
-}
+} NKV_CATCH
 
 int nkv_record_offsets_dev(nkv_ctx* c, const uint64_t* d_rec_size, uint64_t n,
-                           uint64_t* d_rec_off) {
+                           uint64_t* d_rec_off) try {
     TRY(bind(c));
+    if (n > kMaxN) return NKV_ERR_INVALID;
     if (n == 0) return NKV_OK;
     if (!d_rec_size || !d_rec_off || n > 0x7fffffffull) return NKV_ERR_INVALID;
     size_t tb = 0;
     HIPTRY(scan_exclusive_u64(d_rec_size, d_rec_off, n, nullptr, &tb, c->stream));
     TRY(grow(c->d_tmp, tb));
     return st(scan_exclusive_u64(d_rec_size, d_rec_off, n, c->d_tmp.p, &tb, c->stream));
-}
+} NKV_CATCH
 
 int nkv_locate_values_dev(nkv_ctx* c, const void* d_stream, uint64_t stream_len,
                           const uint64_t* d_rec_off, uint64_t n, uint64_t* d_voff,
-                          uint64_t* d_vlen) {
+                          uint64_t* d_vlen) try {
     TRY(bind(c));
+    if (n > kMaxN) return NKV_ERR_INVALID;
     if (n == 0) return NKV_OK;
     if (!d_stream || !d_rec_off || !d_voff || !d_vlen) return NKV_ERR_INVALID;
     TRY(grow(c->d_err, 4));
@@ -991,11 +1022,12 @@ int nkv_locate_values_dev(nkv_ctx* c, const void* d_stream, uint64_t stream_len,
     HIPTRY(hipMemcpyAsync(&h, err, 4, hipMemcpyDeviceToHost, c->stream));
     HIPTRY(hipStreamSynchronize(c->stream));
     return h ? NKV_ERR_INVALID : NKV_OK;
-}
+} NKV_CATCH
 
 int nkv_tree_from_records_dev(nkv_ctx* c, const void* d_stream, uint64_t stream_len, const uint64_t* d_rec_off,
-                              uint64_t n, void* d_nodes, uint32_t* d_err) {
+                              uint64_t n, void* d_nodes, uint32_t* d_err) try {
     TRY(bind(c));
+    if (n > kMaxN) return NKV_ERR_INVALID;
     if (n == 0) return NKV_ERR_EMPTY;
     if (!d_stream || !d_rec_off || !d_nodes) return NKV_ERR_INVALID;
     unsigned int* err = reinterpret_cast<unsigned int*>(d_err);
@@ -1010,15 +1042,16 @@ int nkv_tree_from_records_dev(nkv_ctx* c, const void* d_stream, uint64_t stream_
     HIPTRY(hipMemcpyAsync(&h, err, 4, hipMemcpyDeviceToHost, c->stream));
     HIPTRY(hipStreamSynchronize(c->stream));
     return h ? NKV_ERR_INVALID : NKV_OK;
-}
+} NKV_CATCH
 
 // Compaction read in one pass: the Merkle tree of the records' Values and the
 // check of every record's Crc.  Batches of similar record sizes (the range rule
 // of plan_of) run k_leaf_verify, which reads each record once for both; ragged
 // batches run the checksum kernel and the length-sorted leaf kernel instead.
 int nkv_tree_verify_records_dev(nkv_ctx* c, const void* d_stream, uint64_t stream_len, const uint64_t* d_rec_off,
-                                uint64_t n, void* d_nodes, uint32_t* d_crc, uint64_t* d_stats) {
+                                uint64_t n, void* d_nodes, uint32_t* d_crc, uint64_t* d_stats) try {
     TRY(bind(c));
+    if (n > kMaxN) return NKV_ERR_INVALID;
     if (n == 0) return NKV_ERR_EMPTY;
     if (!d_stream || !d_rec_off || !d_nodes) return NKV_ERR_INVALID;
     const uint8_t* stream = static_cast<const uint8_t*>(d_stream);
@@ -1063,19 +1096,21 @@ int nkv_tree_verify_records_dev(nkv_ctx* c, const void* d_stream, uint64_t strea
     TRY(mark(c, 1));
     HIPTRY(launch_reduce(nodes, n, 0, levels_of(n) - 1, c->stream));
     return mark(c, 2);
-}
+} NKV_CATCH
 
 int nkv_crc32_dev(nkv_ctx* c, const void* d_base, const uint64_t* d_off, const uint64_t* d_len, uint64_t n,
-                  uint32_t* d_crc) {
+                  uint32_t* d_crc) try {
     TRY(bind(c));
+    if (n > kMaxN) return NKV_ERR_INVALID;
     if (n == 0) return NKV_OK;
     if (!d_base || !d_off || !d_len || !d_crc) return NKV_ERR_INVALID;
     return st(launch_crc_spans(static_cast<const uint8_t*>(d_base), d_off, d_len, n, d_crc, c->crc_load, c->stream));
-}
+} NKV_CATCH
 
 int nkv_record_crc_dev(nkv_ctx* c, const void* d_stream, uint64_t stream_len, const uint64_t* d_rec_off,
-                       uint64_t n, uint32_t* d_crc, uint64_t* d_stats) {
+                       uint64_t n, uint32_t* d_crc, uint64_t* d_stats) try {
     TRY(bind(c));
+    if (n > kMaxN) return NKV_ERR_INVALID;
     if (!d_stream && n) return NKV_ERR_INVALID;
     if (n && !d_rec_off) return NKV_ERR_INVALID;
     if (n == 0) {
@@ -1092,7 +1127,7 @@ int nkv_record_crc_dev(nkv_ctx* c, const void* d_stream, uint64_t stream_len, co
     }
     return st(launch_record_crc(static_cast<const uint8_t*>(d_stream), stream_len, d_rec_off, n, d_crc, stats,
                                 c->crc_load, c->stream));
-}
+} NKV_CATCH
 
 // Filter inserts: the range-privatised build (bloom.hip) for batches of at least
 // 4096 keys when its scratch applies, else one device atomicOr per bit.
@@ -1115,18 +1150,20 @@ static int bloom_insert(nkv_ctx* c, int mode, const uint8_t* base, const uint64_
 }
 
 int nkv_bloom_insert_dev(nkv_ctx* c, const void* d_keys, const uint64_t* d_off, const uint64_t* d_len, uint64_t n,
-                         uint32_t m, uint32_t k, uint32_t seed0, void* d_bits) {
+                         uint32_t m, uint32_t k, uint32_t seed0, void* d_bits) try {
     TRY(bind(c));
+    if (n > kMaxN) return NKV_ERR_INVALID;
     if (m == 0 || !d_bits) return NKV_ERR_INVALID;
     if (n == 0) return NKV_OK;
     if (!d_keys || !d_off || !d_len) return NKV_ERR_INVALID;
     return bloom_insert(c, 0, static_cast<const uint8_t*>(d_keys), d_off, d_len, 0, n, m, k, seed0,
                         static_cast<uint32_t*>(d_bits), nullptr);
-}
+} NKV_CATCH
 
 int nkv_bloom_insert_records_dev(nkv_ctx* c, const void* d_stream, uint64_t stream_len, const uint64_t* d_rec_off,
-                                 uint64_t n, uint32_t m, uint32_t k, uint32_t seed0, void* d_bits) {
+                                 uint64_t n, uint32_t m, uint32_t k, uint32_t seed0, void* d_bits) try {
     TRY(bind(c));
+    if (n > kMaxN) return NKV_ERR_INVALID;
     if (m == 0 || !d_bits) return NKV_ERR_INVALID;
     if (n == 0) return NKV_OK;
     if (!d_stream || !d_rec_off) return NKV_ERR_INVALID;
@@ -1139,11 +1176,12 @@ int nkv_bloom_insert_records_dev(nkv_ctx* c, const void* d_stream, uint64_t stre
     HIPTRY(hipMemcpyAsync(&h, err, 4, hipMemcpyDeviceToHost, c->stream));
     HIPTRY(hipStreamSynchronize(c->stream));
     return h ? NKV_ERR_INVALID : NKV_OK;
-}
+} NKV_CATCH
 
 int nkv_bloom_query_dev(nkv_ctx* c, const void* d_keys, const uint64_t* d_off, const uint64_t* d_len, uint64_t n,
-                        uint32_t m, uint32_t k, uint32_t seed0, const void* d_bits, uint8_t* d_out) {
+                        uint32_t m, uint32_t k, uint32_t seed0, const void* d_bits, uint8_t* d_out) try {
     TRY(bind(c));
+    if (n > kMaxN) return NKV_ERR_INVALID;
     if (m == 0 || !d_bits) return NKV_ERR_INVALID;
     if (n == 0) return NKV_OK;
     if (!d_keys || !d_off || !d_len || !d_out) return NKV_ERR_INVALID;
@@ -1151,13 +1189,13 @@ int nkv_bloom_query_dev(nkv_ctx* c, const void* d_keys, const uint64_t* d_off, c
     return st(launch_bloom(0, true, static_cast<const uint8_t*>(d_keys), d_off, d_len, 0, n, m, k, seed0,
                            const_cast<uint32_t*>(static_cast<const uint32_t*>(d_bits)), d_out, nullptr,
                            c->stream));
-}
+} NKV_CATCH
 
-int nkv_fill_splitmix64_dev(nkv_ctx* c, void* d_buf, uint64_t nbytes, uint64_t seed) {
+int nkv_fill_splitmix64_dev(nkv_ctx* c, void* d_buf, uint64_t nbytes, uint64_t seed) try {
     TRY(bind(c));
     if (nbytes == 0) return NKV_OK;
     if (!d_buf) return NKV_ERR_INVALID;
     return st(launch_fill(static_cast<uint8_t*>(d_buf), nbytes, seed, c->stream));
-}
+} NKV_CATCH
 
 }  // extern "C"

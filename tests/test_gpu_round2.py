@@ -430,3 +430,19 @@ def test_bfs_image_segment_edges(nkv, oracle):
             assert got[size:] == b"\xab" * 64, n  # nothing written past the image
     finally:
         ctx.set_stream(_lib._OWN)
+
+
+def test_batch_size_bound(nkv):
+    """Batches past 2^31 - 1 values (the kernels' 32-bit leaf indices) are
+    rejected with NKV_ERR_INVALID before any buffer is touched."""
+    _lib, ctx = nkv
+    L = _lib.lib()
+    big = (1 << 31)
+    one = np.zeros(1, np.uint64)
+    buf = np.zeros(64, np.uint8)
+    assert L.nkv_tree_build(ctx.h, _lib.p8(buf), big, None, None, None) == _lib.NKV_ERR_INVALID
+    assert L.nkv_leaf_hash(ctx.h, _lib.p8(buf), _lib.p64(one), _lib.p64(one), big, _lib.p8(buf)) == _lib.NKV_ERR_INVALID
+    assert L.nkv_tree_reduce_dev(ctx.h, 16, big) == _lib.NKV_ERR_INVALID
+    assert L.nkv_tree_from_strided_dev(ctx.h, 16, 64, 64, big, 16) == _lib.NKV_ERR_INVALID
+    # the largest accepted count still reaches the argument checks (null pointers)
+    assert L.nkv_tree_build(ctx.h, None, big - 1, None, None, None) == _lib.NKV_ERR_INVALID
