@@ -68,9 +68,10 @@ extern "C" {
 typedef enum nkv_status {
     NKV_OK = 0,
     NKV_ERR_EMPTY = 1,   /* "cannot build Merkle Tree from 0 nodes" (merkletree.go:20) */
-    NKV_ERR_INVALID = 2, /* bad argument (null pointer, size overflow, bad record) */
+    NKV_ERR_INVALID = 2, /* bad argument (null pointer, size overflow, bad record,
+                            more than 2^31 - 1 values in one batch) */
     NKV_ERR_DEVICE = 3,  /* HIP runtime / kernel launch failure, or no such device */
-    NKV_ERR_NOMEM = 4,   /* device or pinned-host allocation failed */
+    NKV_ERR_NOMEM = 4,   /* device, pinned-host or host allocation failed */
     NKV_ERR_IO = 5       /* file open/write failed (nkv_write_file) */
 } nkv_status;
 
