@@ -1045,9 +1045,11 @@ int nkv_tree_from_records_dev(nkv_ctx* c, const void* d_stream, uint64_t stream_
 } NKV_CATCH
 
 // Compaction read in one pass: the Merkle tree of the records' Values and the
-// check of every record's Crc.  Batches of similar record sizes (the range rule
-// of plan_of) run k_leaf_verify, which reads each record once for both; ragged
-// batches run the checksum kernel and the length-sorted leaf kernel instead.
+// check of every record's Crc.  k_leaf_verify parses the headers, checks every
+// Crc and hashes the waves whose value sizes are narrow (the range rule of
+// plan_of), reading each record once for both; it defers ragged waves (after
+// their checksums) to the length-sorted leaf pass behind a device Gate, as
+// records_tree does.
 int nkv_tree_verify_records_dev(nkv_ctx* c, const void* d_stream, uint64_t stream_len, const uint64_t* d_rec_off,
                                 uint64_t n, void* d_nodes, uint32_t* d_crc, uint64_t* d_stats) try {
     TRY(bind(c));
@@ -1063,36 +1065,23 @@ int nkv_tree_verify_records_dev(nkv_ctx* c, const void* d_stream, uint64_t strea
     }
     HIPTRY(hipMemsetAsync(stats, 0, 24, c->stream));
     HIPTRY(hipMemsetAsync(stats + 1, 0xFF, 8, c->stream));
+    // records_tree's policy rule: input order without bucketing or for tiny
+    // batches; auto for >= 4096 records; else everything sorted
+    const int policy = (c->bucket == 0 || n <= 64) ? 0 : ((c->bucket == 2 && n >= 4096) ? 1 : 2);
+    TRY(grow(c->d_off, 8 * n));
+    TRY(grow(c->d_len, 8 * n));
+    TRY(grow(c->d_range, 8));
+    uint64_t* voff = static_cast<uint64_t*>(c->d_off.p);
+    uint64_t* vlen = static_cast<uint64_t*>(c->d_len.p);
+    unsigned int* range = static_cast<unsigned int*>(c->d_range.p);
+    uint32_t* part = nullptr;
+    TRY(locate_parts(c, n, &part));
     TRY(mark(c, 0));
-    int plan = kInputOrder;
-    Gate g;
-    uint64_t* voff = nullptr;
-    uint64_t* vlen = nullptr;
-    if (c->bucket != 0 && n > 64) {
-        // the lengths decide the order (and feed the sorted branch)
-        TRY(grow(c->d_off, 8 * n));
-        TRY(grow(c->d_len, 8 * n));
-        TRY(grow(c->d_err, 4));
-        voff = static_cast<uint64_t*>(c->d_off.p);
-        vlen = static_cast<uint64_t*>(c->d_len.p);
-        unsigned int* err = static_cast<unsigned int*>(c->d_err.p);
-        const bool gated = c->bucket == 2 && n >= 4096;
-        if (gated) TRY(grow(c->d_range, 8));
-        unsigned int* range = gated ? static_cast<unsigned int*>(c->d_range.p) : nullptr;
-        uint32_t* part = nullptr;
-        TRY(locate_parts(c, n, &part));
-        HIPTRY(launch_locate(stream, stream_len, d_rec_off, n, voff, vlen, err, range, part, c->stream));
-        TRY(plan_of(c, vlen, nullptr, n, &plan, &g, range));
-    }
-    if (plan != kSorted)
-        HIPTRY(launch_leaf_verify(stream, stream_len, d_rec_off, n, nodes, d_crc, stats, c->stream,
-                                  plan == kGated ? Gate{g.range, 1} : Gate{}));
-    if (plan != kInputOrder) {
-        const Gate wide = plan == kGated ? Gate{g.range, 2} : Gate{};
-        HIPTRY(launch_record_crc(stream, stream_len, d_rec_off, n, d_crc, stats, c->crc_load, c->stream, wide,
-                                 false));
-        TRY(leaf_level(c, stream, voff, vlen, n, false, nodes, plan, g, false));
-    }
+    HIPTRY(launch_leaf_verify(stream, stream_len, d_rec_off, n, policy, voff, vlen, nodes, d_crc, stats, range,
+                              part, c->stream));
+    if (policy != 0)
+        TRY(leaf_level(c, stream, voff, vlen, n, false, nodes, policy == 2 ? kSorted : kGated, Gate{range, 0},
+                       false));
     TRY(mark(c, 1));
     HIPTRY(launch_reduce(nodes, n, 0, levels_of(n) - 1, c->stream));
     return mark(c, 2);

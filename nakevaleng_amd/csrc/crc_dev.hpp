@@ -89,4 +89,52 @@ __device__ __forceinline__ uint32_t crc_byte(uint32_t crc, uint32_t b, const uin
     return crc_lut<C>(tab, 0, (crc ^ b) & 0xFFu) ^ (crc >> 8);
 }
 
+__device__ __forceinline__ uint32_t crc_wave_max(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, uint32_t(__shfl_xor(int(v), o)));
+    return __builtin_amdgcn_readfirstlane(v);
+}
+
+// CRC-32/IEEE of [s, s + len) (finalised).  Every lane of the wave calls it
+// (dead lanes with len 0).
+template <int C>
+__device__ __forceinline__ uint32_t crc_span(const uint8_t* s, uint64_t len, const uint32_t* tab) {
+    uint32_t crc = 0xFFFFFFFFu;
+    const uint64_t sa = uint64_t(reinterpret_cast<uintptr_t>(s));
+    const uint64_t ea = sa + len;
+    const uint64_t s4 = (sa + 3) & ~uint64_t(3);
+    const uint64_t e4 = ea & ~uint64_t(3);
+    const uint64_t hb = s4 < ea ? s4 : ea;
+    for (uint64_t a = sa; a < hb; ++a) crc = crc_byte<C>(crc, s[a - sa], tab);
+    const uint64_t A = s4 & ~uint64_t(63);
+    const uint32_t nch = e4 > s4 ? uint32_t((e4 - A + 63) >> 6) : 0u;
+    const uint32_t nmax = crc_wave_max(nch);
+    // s + (A - sa): stays a global pointer (no integer-to-pointer cast)
+    const uint4* q = reinterpret_cast<const uint4*>(s + (A - sa));
+    for (uint32_t c = 0; c < nmax; ++c) {
+        if (c < nch) {
+            uint4 v[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = q[4 * c + i];
+            const uint32_t w[16] = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w,
+                                    v[2].x, v[2].y, v[2].z, v[2].w, v[3].x, v[3].y, v[3].z, v[3].w};
+            const uint64_t b0 = A + 64ull * c;
+            if (b0 >= s4 && b0 + 64 <= e4) {
+                crc = crc_block16<C>(crc, w, tab);
+            } else {
+                const uint64_t lo = s4 > b0 ? (s4 - b0) >> 2 : 0;
+                const uint64_t hi = e4 - b0 >= 64 ? 16 : (e4 - b0) >> 2;
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    const uint32_t u = crc_word<C>(crc, w[j], tab);
+                    crc = (uint64_t(j) >= lo && uint64_t(j) < hi) ? u : crc;
+                }
+            }
+        }
+    }
+    const uint64_t tb = e4 > hb ? e4 : hb;
+    for (uint64_t a = tb; a < ea; ++a) crc = crc_byte<C>(crc, s[a - sa], tab);
+    return ~crc;
+}
+
 }  // namespace nkv

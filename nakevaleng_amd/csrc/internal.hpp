@@ -130,12 +130,16 @@ hipError_t launch_record_crc(const uint8_t* stream, uint64_t stream_len, const u
                              uint32_t* out, unsigned long long* stats, int variant, hipStream_t s,
                              Gate gate = Gate{}, bool init_stats = true);
 // The compaction read in one pass (kernels.hip k_leaf_verify): for the record at
-// stream + rec_off[i], the leaf digest of its Value into nodes (level 0), its
-// CRC of Key ++ Value into crc_out[i] (nullable), checked against the stored
-// Crc into stats as launch_record_crc does (stats initialised by the caller).
+// stream + rec_off[i], its CRC of Key ++ Value into crc_out[i] (nullable),
+// checked against the stored Crc into stats as launch_record_crc does (stats
+// initialised by the caller), and the leaf digest of its Value into nodes
+// (level 0) -- for every wave (policy 0), for the narrow waves (1: the others
+// leave voff / vlen for the sorted pass, hashed ones kDone, and range opens
+// its wide Gate only if a wave was deferred), or for none (2).  part: scratch
+// of locate_part_words(n) u32; voff / vlen / range / part unused for policy 0.
 hipError_t launch_leaf_verify(const uint8_t* stream, uint64_t stream_len, const uint64_t* rec_off, uint64_t n,
-                              uint8_t* nodes, uint32_t* crc_out, unsigned long long* stats, hipStream_t s,
-                              Gate gate = Gate{});
+                              int policy, uint64_t* voff, uint64_t* vlen, uint8_t* nodes, uint32_t* crc_out,
+                              unsigned long long* stats, unsigned int* range, uint32_t* part, hipStream_t s);
 // bloom.hip: mode 0 = keys at base + off[i], len[i]; 1 = keys of the records at
 // base + off[i].  query: out[i] = all k bits set; else OR the bits in.
 hipError_t launch_bloom(int mode, bool query, const uint8_t* base, const uint64_t* off, const uint64_t* len,

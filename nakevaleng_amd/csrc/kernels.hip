@@ -1318,14 +1318,22 @@ struct CrcRaw {
 // the LDS nearly idle, so the lookups ride along.  A record whose header points
 // outside the stream sets stats[2] and gets the digest of an empty value, as
 // in nkv_tree_from_records_dev.
+//
+// The header parse is k_locate's, so no separate locate pass runs.  policy
+// (as k_leaf_records): 0 hashes every wave here; 1 (auto) hashes the waves
+// whose value block counts are narrow by the plan rule and defers the others;
+// 2 defers all.  A deferred wave only checksums its records here (crc_span
+// over Key ++ Value, the CRC is cheap next to SHA-1) and leaves each value's
+// voff / vlen for the length-sorted leaf pass; a hashed value's voff becomes
+// kDone.  Each workgroup leaves (0, deferred ? ~0 : 0, 0) in part, folded by
+// k_locate_fold into the range whose wide Gate opens the sorted pass.
 __global__ __launch_bounds__(kBlock, kLeafWavesPerSimd) void k_leaf_verify(
     const uint8_t* __restrict__ stream, uint64_t stream_len, const uint64_t* __restrict__ rec_off, uint64_t n,
-    uint8_t* __restrict__ nodes, uint32_t* __restrict__ crc_out, unsigned long long* __restrict__ stats,
-    Gate gate) {
+    int policy, uint64_t* __restrict__ voff, uint64_t* __restrict__ vlen, uint8_t* __restrict__ nodes,
+    uint32_t* __restrict__ crc_out, unsigned long long* __restrict__ stats, uint32_t* __restrict__ part) {
     // ONE LDS object (a second one can cost the DMA loop its waits): four
     // 4 KiB wave stages, then the 4 KiB of CRC tables
     __shared__ __attribute__((aligned(16))) uint8_t smem[kBlock * 64 + 4096];
-    if (!gate.open()) return;
     uint32_t* tab = reinterpret_cast<uint32_t*>(smem + kBlock * 64);
     for (int i = threadIdx.x; i < 4 * 256; i += kBlock) tab[i] = (&c_crc_leaf.t[0][0])[i];
     __syncthreads();
@@ -1356,40 +1364,77 @@ __global__ __launch_bounds__(kBlock, kLeafWavesPerSimd) void k_leaf_verify(
             hdr_bad = true;
         }
     }
-    uint32_t crc = 0xFFFFFFFFu;
-    for (uint64_t j = 0; j < ks; ++j) crc = crc_byte<1>(crc, key[j], tab);
-    uint8_t* wbuf = smem + 4096 * wave;
-    const uint32_t q = (uint32_t(lane) & 3u) ^ ((uint32_t(lane) >> 4) & 3u);
-    const uint32_t my_nfull = uint32_t(ln >> 6);
-    uint32_t h[5];
-    sha1_init(h);
-    const uint8_t* src[4];
-    uint32_t nf[4];
+    const uint64_t bl = ln >> 6;
+    const uint32_t my_nfull = bl > 0xFFFFFFFFull ? 0xFFFFFFFFu : uint32_t(bl);
+    const uint32_t wlo = wave_min_u32(live ? my_nfull : 0xFFFFFFFFu);
+    const uint32_t whi = wave_max_u32(live ? my_nfull : 0u);
+    const bool any = __any(live);
+    const bool hash = any && (policy == 0 || (policy == 1 && whi <= wlo + max(1u, wlo / 16u)));
+    uint32_t crc;
+    if (hash) {
+        crc = 0xFFFFFFFFu;
+        for (uint64_t j = 0; j < ks; ++j) crc = crc_byte<1>(crc, key[j], tab);
+        uint8_t* wbuf = smem + 4096 * wave;
+        const uint32_t q = (uint32_t(lane) & 3u) ^ ((uint32_t(lane) >> 4) & 3u);
+        uint32_t h[5];
+        sha1_init(h);
+        const uint8_t* src[4];
+        uint32_t nf[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int j = 16 * k + (lane >> 2);
-        const uint64_t pj = uint64_t(__shfl(int64_t(reinterpret_cast<uintptr_t>(p)), j));
-        src[k] = reinterpret_cast<const uint8_t*>(pj) + 16 * q;
-        nf[k] = uint32_t(__shfl(int(my_nfull), j));
+        for (int k = 0; k < 4; ++k) {
+            const int j = 16 * k + (lane >> 2);
+            const uint64_t pj = uint64_t(__shfl(int64_t(reinterpret_cast<uintptr_t>(p)), j));
+            src[k] = reinterpret_cast<const uint8_t*>(pj) + 16 * q;
+            nf[k] = uint32_t(__shfl(int(my_nfull), j));
+        }
+        auto issue = [&](uint32_t b) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (b < nf[k]) __builtin_amdgcn_global_load_lds(src[k] + 64ull * b, wbuf + 1024 * k, 16, 0, 0);
+        };
+        CrcRaw raw{crc, tab};
+        sha1_blocks_lds(wbuf, whi, my_nfull, issue, h, raw);
+        for (uint64_t j = uint64_t(my_nfull) * 64; j < ln; ++j) crc = crc_byte<1>(crc, p[j], tab);
+        crc = ~crc;
+        if (live) {
+            sha1_tail<false>(p, ln, h);
+            store_digest(nodes, t, h);
+            if (voff) {
+                voff[t] = kDone;
+                vlen[t] = 0;
+            }
+        }
+    } else {
+        // deferred: Key ++ Value is one contiguous span of the record
+        crc = crc_span<1>(key, ks + ln, tab);
+        if (live) {
+            voff[t] = uint64_t(p - stream);
+            vlen[t] = ln;
+        }
     }
-    auto issue = [&](uint32_t b) {
+    if (live) {
+        if (crc_out) crc_out[t] = crc;
+        if (hdr_bad) {
+            atomicOr(stats + 2, 1ull);
+        } else if (crc != stored) {
+            atomicAdd(stats, 1ull);
+            atomicMin(stats + 1, (unsigned long long)t);
+        }
+    }
+    if (part) {  // one partial per workgroup, through the (now idle) stage LDS
+        const bool wdefer = any && !hash;
+        uint32_t* flags = reinterpret_cast<uint32_t*>(smem);
+        __syncthreads();
+        if (lane == 0) flags[threadIdx.x >> 6] = wdefer ? 1u : 0u;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t f = 0u;
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if (b < nf[k]) __builtin_amdgcn_global_load_lds(src[k] + 64ull * b, wbuf + 1024 * k, 16, 0, 0);
-    };
-    CrcRaw raw{crc, tab};
-    sha1_blocks_lds(wbuf, wave_max_u32(my_nfull), my_nfull, issue, h, raw);
-    for (uint64_t j = uint64_t(my_nfull) * 64; j < ln; ++j) crc = crc_byte<1>(crc, p[j], tab);
-    if (!live) return;
-    sha1_tail<false>(p, ln, h);
-    store_digest(nodes, t, h);
-    crc = ~crc;
-    if (crc_out) crc_out[t] = crc;
-    if (hdr_bad) {
-        atomicOr(stats + 2, 1ull);
-    } else if (crc != stored) {
-        atomicAdd(stats, 1ull);
-        atomicMin(stats + 1, (unsigned long long)t);
+            for (int k = 0; k < kBlock / 64; ++k) f |= flags[k];
+            part[3 * blockIdx.x] = 0u;
+            part[3 * blockIdx.x + 1] = f ? 0xFFFFFFFFu : 0u;
+            part[3 * blockIdx.x + 2] = 0u;
+        }
     }
 }
 
@@ -2028,9 +2073,12 @@ hipError_t launch_leaf_offsets(const uint8_t* base, const uint64_t* off, const u
 }
 
 hipError_t launch_leaf_verify(const uint8_t* stream, uint64_t stream_len, const uint64_t* rec_off, uint64_t n,
-                              uint8_t* nodes, uint32_t* crc_out, unsigned long long* stats, hipStream_t s, Gate gate) {
-    hipLaunchKernelGGL(k_leaf_verify, dim3(grid_for(n)), dim3(kBlock), 0, s, stream, stream_len, rec_off, n, nodes,
-                       crc_out, stats, gate);
+                              int policy, uint64_t* voff, uint64_t* vlen, uint8_t* nodes, uint32_t* crc_out,
+                              unsigned long long* stats, unsigned int* range, uint32_t* part, hipStream_t s) {
+    const unsigned nb = grid_for(n);
+    hipLaunchKernelGGL(k_leaf_verify, dim3(nb), dim3(kBlock), 0, s, stream, stream_len, rec_off, n, policy, voff,
+                       vlen, nodes, crc_out, stats, policy == 0 ? nullptr : part);
+    if (policy != 0) hipLaunchKernelGGL(k_locate_fold, dim3(1), dim3(kBlock), 0, s, part, nb, nullptr, range);
     return hipGetLastError();
 }
 

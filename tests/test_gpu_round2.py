@@ -446,3 +446,51 @@ def test_batch_size_bound(nkv):
     assert L.nkv_tree_from_strided_dev(ctx.h, 16, 64, 64, big, 16) == _lib.NKV_ERR_INVALID
     # the largest accepted count still reaches the argument checks (null pointers)
     assert L.nkv_tree_build(ctx.h, None, big - 1, None, None, None) == _lib.NKV_ERR_INVALID
+
+
+@pytest.mark.parametrize("bucket", [0, 1, 2])
+def test_verify_records_partly_ragged_every_policy(nkv, oracle, bucket):
+    """k_leaf_verify's deferral: narrow waves are checksummed and hashed in one
+    pass, ragged waves are checksummed there and hashed by the length-sorted
+    pass (which skips the kDone values).  Two stored Crcs are wrong, one in a
+    narrow wave and one in a ragged wave; every policy gives the oracle's tree,
+    every record's CRC, the mismatch count and the first bad index."""
+    import zlib
+    import torch
+    from nakevaleng_amd import record
+    _lib, ctx = nkv
+    L = _lib.lib()
+    rng = np.random.default_rng(200 + bucket)
+    recs = [record.New(rng.bytes(16), rng.bytes(2000), timestamp=i) for i in range(64 * 40)]
+    recs += [record.New(rng.bytes(int(rng.integers(0, 40))), rng.bytes(int(rng.integers(0, 20000))), timestamp=i)
+             for i in range(3000)]
+    recs += [record.New(rng.bytes(16), rng.bytes(2000), timestamp=i) for i in range(64 * 10 + 17)]
+    stream, sizes = record.data_table(recs)
+    n = len(sizes)
+    roff = np.zeros(n, np.uint64)
+    roff[1:] = np.cumsum(np.asarray(sizes, np.uint64)[:-1])
+    off, ln = record.value_spans(stream, sizes)
+    buf = np.frombuffer(stream, np.uint8).copy()
+    want = oracle.tree_from_digests(oracle.leaf_hashes(buf, off, ln, threads=8))
+    crcs = np.array([zlib.crc32(buf[int(roff[i]) + 30:int(off[i] + ln[i])].tobytes()) for i in range(n)], np.uint32)
+    bad = [300, 64 * 40 + 1234]  # a narrow wave's record, a ragged wave's record
+    for j in bad:
+        buf[int(roff[j])] ^= 0x5A  # the stored Crc's low byte
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    ctx.set_option(_lib.NKV_OPT_BUCKET, bucket)
+    try:
+        d_stream = torch.from_numpy(buf).cuda()
+        d_roff = torch.from_numpy(roff.view(np.int64)).cuda()
+        for _ in range(2):  # the gate's range and the fold restore themselves between calls
+            d_nodes = torch.zeros(L.nkv_total_nodes(n) * 20, dtype=torch.uint8, device="cuda")
+            d_crc = torch.zeros(n, dtype=torch.int32, device="cuda")
+            d_stats = torch.full((3,), 5, dtype=torch.int64, device="cuda")
+            _lib.check(L.nkv_tree_verify_records_dev(ctx.h, d_stream.data_ptr(), len(stream), d_roff.data_ptr(), n,
+                                                     d_nodes.data_ptr(), d_crc.data_ptr(), d_stats.data_ptr()))
+            torch.cuda.synchronize()
+            assert np.array_equal(d_nodes.cpu().numpy().reshape(-1, 20), want)
+            assert np.array_equal(d_crc.cpu().numpy().view(np.uint32), crcs)
+            assert d_stats.cpu().tolist() == [2, min(bad), 0]
+    finally:
+        ctx.set_option(_lib.NKV_OPT_BUCKET, 2)
+        ctx.set_stream(_lib._OWN)
