@@ -157,3 +157,58 @@ def test_fuzz_parity(oracle, seed):
             assert np.array_equal(got, want), (entry, n)
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("seed", range(96))
+def test_fuzz_crc_bloom(oracle, seed):
+    """Span checksums (every NKV_OPT_CRC_LOAD kernel) and filter inserts and
+    queries (every NKV_OPT_BLOOM_PATH) over random spans at random alignments,
+    random m, k and seeds, against the oracle (record.go:51, bloomfilter.go:76-91)."""
+    import torch
+    from nakevaleng_amd import _lib
+    L = _lib.lib()
+    rng = np.random.default_rng(0xC0C + seed)
+    n = int(np.exp(rng.uniform(0, np.log(30000))))
+    lens = (rng.integers(0, 64, n) if rng.integers(0, 2) else rng.integers(0, 6000, n)).astype(np.uint64)
+    gaps = rng.integers(0, 40, n).astype(np.uint64)
+    off = np.zeros(n, np.uint64)
+    if n > 1:
+        off[1:] = np.cumsum(lens[:-1] + gaps[:-1])
+    data = oracle.splitmix64_bytes(int(off[-1] + lens[-1]) + 1, seed)
+    ctx = _lib.Context(0)
+    try:
+        ctx.set_option(_lib.NKV_OPT_CRC_LOAD, int(rng.choice([0, 1, 2, 3, 4, 5, 8, 9, 10])))
+        ctx.set_option(_lib.NKV_OPT_BLOOM_PATH, int(rng.integers(0, 3)))
+        m = int(rng.integers(1, 1 << 21))
+        k = int(rng.integers(1, 21))
+        seed0 = int(rng.integers(0, 1 << 32))
+        with ctx.on_stream(torch.cuda.current_stream().cuda_stream):
+            d = torch.from_numpy(data).cuda()
+            d_off = torch.from_numpy(off.view(np.int64)).cuda()
+            d_len = torch.from_numpy(lens.view(np.int64)).cuda()
+            d_crc = torch.zeros(n, dtype=torch.int32, device="cuda")
+            _lib.check(L.nkv_crc32_dev(ctx.h, d.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n, d_crc.data_ptr()))
+            d_bits = torch.zeros((m + 31) // 32 * 4, dtype=torch.uint8, device="cuda")  # whole words (header)
+            _lib.check(L.nkv_bloom_insert_dev(ctx.h, d.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n, m, k, seed0,
+                                              d_bits.data_ptr()))
+            # queries: the inserted keys in reverse order plus keys shifted by one byte
+            q_off = np.concatenate([off[::-1], off + 1]).astype(np.uint64)
+            q_len = np.concatenate([lens[::-1], lens]).astype(np.uint64)
+            d_qoff = torch.from_numpy(q_off.view(np.int64)).cuda()
+            d_qlen = torch.from_numpy(q_len.view(np.int64)).cuda()
+            d_hit = torch.zeros(2 * n, dtype=torch.uint8, device="cuda")
+            _lib.check(L.nkv_bloom_query_dev(ctx.h, d.data_ptr(), d_qoff.data_ptr(), d_qlen.data_ptr(), 2 * n, m, k,
+                                             seed0, d_bits.data_ptr(), d_hit.data_ptr()))
+            crc = d_crc.cpu().numpy().view(np.uint32)
+            bits = d_bits.cpu().numpy()
+            hit = d_hit.cpu().numpy()
+        want_crc = np.array([oracle.crc32(data[int(off[i]):int(off[i] + lens[i])]) for i in range(n)], np.uint32)
+        assert np.array_equal(crc, want_crc)
+        want_bits = oracle.bloom_insert(data, off, lens, m, k, seed0)
+        assert np.array_equal(bits[:(m + 7) // 8], want_bits)
+        assert not bits[(m + 7) // 8:].any()  # the word padding stays zero
+        want_hit = oracle.bloom_query(data, q_off, q_len, m, k, seed0, want_bits)
+        assert np.array_equal(hit.astype(bool), want_hit[:2 * n].astype(bool))
+        assert hit[:n].all()  # no false negatives
+    finally:
+        ctx.close()
