@@ -97,8 +97,11 @@ __device__ __forceinline__ uint32_t crc_wave_max(uint32_t v) {
 
 // CRC-32/IEEE of [s, s + len) (finalised).  Every lane of the wave calls it
 // (dead lanes with len 0).
-template <int C>
-__device__ __forceinline__ uint32_t crc_span(const uint8_t* s, uint64_t len, const uint32_t* tab) {
+// SW: the word steps run in the byte-swapped domain against swtab (slot k =
+// bswap(T[3 - k]), k_leaf_verify's layout); tab then needs only T[0] (bytes).
+template <int C, bool SW = false>
+__device__ __forceinline__ uint32_t crc_span(const uint8_t* s, uint64_t len, const uint32_t* tab,
+                                             const uint32_t* swtab = nullptr) {
     uint32_t crc = 0xFFFFFFFFu;
     const uint64_t sa = uint64_t(reinterpret_cast<uintptr_t>(s));
     const uint64_t ea = sa + len;
@@ -120,13 +123,21 @@ __device__ __forceinline__ uint32_t crc_span(const uint8_t* s, uint64_t len, con
                                     v[2].x, v[2].y, v[2].z, v[2].w, v[3].x, v[3].y, v[3].z, v[3].w};
             const uint64_t b0 = A + 64ull * c;
             if (b0 >= s4 && b0 + 64 <= e4) {
-                crc = crc_block16<C>(crc, w, tab);
+                if constexpr (SW) {
+                    uint32_t be[16];
+#pragma unroll
+                    for (int j = 0; j < 16; ++j) be[j] = __builtin_bswap32(w[j]);
+                    crc = __builtin_bswap32(crc_block16<C>(__builtin_bswap32(crc), be, swtab));
+                } else {
+                    crc = crc_block16<C>(crc, w, tab);
+                }
             } else {
                 const uint64_t lo = s4 > b0 ? (s4 - b0) >> 2 : 0;
                 const uint64_t hi = e4 - b0 >= 64 ? 16 : (e4 - b0) >> 2;
 #pragma unroll
                 for (int j = 0; j < 16; ++j) {
-                    const uint32_t u = crc_word<C>(crc, w[j], tab);
+                    const uint32_t u = SW ? __builtin_bswap32(crc_x_last<C>(__builtin_bswap32(crc ^ w[j]), swtab))
+                                          : crc_word<C>(crc, w[j], tab);
                     crc = (uint64_t(j) >= lo && uint64_t(j) < hi) ? u : crc;
                 }
             }

@@ -434,11 +434,13 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
 }
 
 // issue(b) starts the four DMA instructions of block b (each lane for its DMA
-// role); nmax = the wave's largest full-block count (wave-uniform).  raw(c)
-// sees each of this lane's blocks as loaded (four little-endian quads) before
-// the byte swap (k_leaf_verify checksums them there).
+// role); nmax = the wave's largest full-block count (wave-uniform).  raw(c, w)
+// sees each of this lane's blocks as loaded (four little-endian quads) and as
+// the 16 big-endian words SHA-1 takes (k_leaf_verify checksums them there);
+// be(w), for the stages that only form the big-endian words.
 struct NoRaw {
-    __device__ __forceinline__ void operator()(const uint4*) const {}
+    __device__ __forceinline__ void operator()(const uint4*, const uint32_t*) const {}
+    __device__ __forceinline__ void be(const uint32_t*) const {}
 };
 
 template <class Issue, class Raw = NoRaw>
@@ -464,7 +466,7 @@ __device__ __forceinline__ void sha1_blocks_lds(const uint8_t* wbuf, uint32_t nm
             issue(b + 1);
         }
         if (b < my_nfull) {
-            raw(c);
+            raw(c, w);
             sha1_compress(h, w);
         }
     }
@@ -1014,8 +1016,9 @@ __device__ __forceinline__ void load_seg(const uint4* s, uint32_t r[16]) {
     }
 }
 
+template <class Hook = NoRaw>
 __device__ __forceinline__ bool sha1_blocks_shift(uint8_t* wbuf, const uint8_t* p, bool live, uint32_t my_nfull,
-                                                  uint32_t h[5]) {
+                                                  uint32_t h[5], Hook hook = Hook{}) {
     const uint32_t o = live ? uint32_t(reinterpret_cast<uintptr_t>(p) & 63u) : 0u;
     // lane 0 is live whenever any lane is (dead lanes are the grid's tail)
     const uint32_t o0 = __builtin_amdgcn_readfirstlane(o);
@@ -1087,14 +1090,20 @@ __device__ __forceinline__ bool sha1_blocks_shift(uint8_t* wbuf, const uint8_t* 
                 if (k + 2 <= nmax) issue(k + 2);
                 funnel_u(q, a, b, sel, w);
                 __builtin_amdgcn_sched_barrier(0);
-                if (live) sha1_compress(h, w);
+                if (live) {
+                    hook.be(w);
+                    sha1_compress(h, w);
+                }
                 __builtin_amdgcn_sched_barrier(0);
                 if (k + 1 >= nmax) break;
                 take(a);  // segment k + 2
                 if (k + 3 <= nmax) issue(k + 3);
                 funnel_u(q, b, a, sel, w);
                 __builtin_amdgcn_sched_barrier(0);
-                if (live) sha1_compress(h, w);
+                if (live) {
+                    hook.be(w);
+                    sha1_compress(h, w);
+                }
                 __builtin_amdgcn_sched_barrier(0);
             }
             return true;
@@ -1112,7 +1121,10 @@ __device__ __forceinline__ bool sha1_blocks_shift(uint8_t* wbuf, const uint8_t* 
         // block k: segments k (a) and k + 1 (b)
         if (k < my_nfull) load_seg(seg + 4 * (k + 1), b);
         funnel_u(q, a, b, sel, w);
-        if (k < my_nfull) sha1_compress(h, w);
+        if (k < my_nfull) {
+            hook.be(w);
+            sha1_compress(h, w);
+        }
         // keep each load after the previous compress: hoisted above it, a
         // segment set would be live through the compress and spill at 64 VGPRs
         // (the other resident waves cover the load latency)
@@ -1121,7 +1133,10 @@ __device__ __forceinline__ bool sha1_blocks_shift(uint8_t* wbuf, const uint8_t* 
         // block k + 1: segments k + 1 (b) and k + 2 (a)
         if (k + 1 < my_nfull) load_seg(seg + 4 * (k + 2), a);
         funnel_u(q, b, a, sel, w);
-        if (k + 1 < my_nfull) sha1_compress(h, w);
+        if (k + 1 < my_nfull) {
+            hook.be(w);
+            sha1_compress(h, w);
+        }
         asm volatile("" ::: "memory");
     }
     return true;
@@ -1293,18 +1308,17 @@ __global__ __launch_bounds__(kBlock, (LOAD == 6 || LOAD == 7) ? 2 : ((LOAD == 4 
 #endif
 }
 
-// k_leaf_verify's raw-block hook: the block's 16 little-endian words step the
-// CRC in x = crc ^ w form (crc_dev.hpp) before the block's compression.
+// k_leaf_verify's block hook: the CRC steps over the 16 big-endian words SHA-1
+// takes, with the state byte-swapped (cs = bswap(crc)) against byte-swapped
+// tables stored in reverse order (slot k = bswap(T[3 - k]), crc_dev.hpp), so
+// the same x-form step indexes the right bytes and no extra byte swap runs.
 // (Spreading the 16 steps over the rounds, one per one or two rounds, ran
 // 0.3 % faster and 6 % slower: the lookups' latency is not what bounds it.)
-struct CrcRaw {
-    uint32_t& crc;
-    const uint32_t* tab;
-    __device__ __forceinline__ void operator()(const uint4* c) {
-        const uint32_t w[16] = {c[0].x, c[0].y, c[0].z, c[0].w, c[1].x, c[1].y, c[1].z, c[1].w,
-                                c[2].x, c[2].y, c[2].z, c[2].w, c[3].x, c[3].y, c[3].z, c[3].w};
-        crc = crc_block16<1>(crc, w, tab);
-    }
+struct CrcBE {
+    uint32_t& cs;
+    const uint32_t* swtab;
+    __device__ __forceinline__ void be(const uint32_t* w) { cs = crc_block16<1>(cs, w, swtab); }
+    __device__ __forceinline__ void operator()(const uint4*, const uint32_t* w) { be(w); }
 };
 
 // K1v: the compaction read of a Data table in one pass.  For every record it
@@ -1327,15 +1341,22 @@ struct CrcRaw {
 // voff / vlen for the length-sorted leaf pass; a hashed value's voff becomes
 // kDone.  Each workgroup leaves (0, deferred ? ~0 : 0, 0) in part, folded by
 // k_locate_fold into the range whose wide Gate opens the sorted pass.
-__global__ __launch_bounds__(kBlock, kLeafWavesPerSimd) void k_leaf_verify(
+#ifndef NKV_VERIFY_WAVES
+#define NKV_VERIFY_WAVES 7
+#endif
+__global__ __launch_bounds__(kBlock, NKV_VERIFY_WAVES) void k_leaf_verify(
     const uint8_t* __restrict__ stream, uint64_t stream_len, const uint64_t* __restrict__ rec_off, uint64_t n,
     int policy, uint64_t* __restrict__ voff, uint64_t* __restrict__ vlen, uint8_t* __restrict__ nodes,
     uint32_t* __restrict__ crc_out, unsigned long long* __restrict__ stats, uint32_t* __restrict__ part) {
     // ONE LDS object (a second one can cost the DMA loop its waits): four
-    // 4 KiB wave stages, then the 4 KiB of CRC tables
-    __shared__ __attribute__((aligned(16))) uint8_t smem[kBlock * 64 + 4096];
-    uint32_t* tab = reinterpret_cast<uint32_t*>(smem + kBlock * 64);
-    for (int i = threadIdx.x; i < 4 * 256; i += kBlock) tab[i] = (&c_crc_leaf.t[0][0])[i];
+    // 4 KiB wave stages, the 4 KiB of byte-swapped word tables (CrcBE), then
+    // T[0] for the bytewise steps: 21 KiB, seven workgroups per CU
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kBlock * 64 + 4096 + 1024];
+    uint32_t* swtab = reinterpret_cast<uint32_t*>(smem + kBlock * 64);
+    uint32_t* tab = swtab + 4 * 256;
+    for (int i = threadIdx.x; i < 4 * 256; i += kBlock)
+        swtab[i] = __builtin_bswap32(c_crc_leaf.t[3 - (i >> 8)][i & 255]);
+    for (int i = threadIdx.x; i < 256; i += kBlock) tab[i] = c_crc_leaf.t[0][i];
     __syncthreads();
     const uint64_t t = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
     const int lane = threadIdx.x & 63;
@@ -1392,8 +1413,12 @@ __global__ __launch_bounds__(kBlock, kLeafWavesPerSimd) void k_leaf_verify(
             for (int k = 0; k < 4; ++k)
                 if (b < nf[k]) __builtin_amdgcn_global_load_lds(src[k] + 64ull * b, wbuf + 1024 * k, 16, 0, 0);
         };
-        CrcRaw raw{crc, tab};
-        sha1_blocks_lds(wbuf, whi, my_nfull, issue, h, raw);
+        uint32_t cs = __builtin_bswap32(crc);
+        CrcBE hook{cs, swtab};
+        // records of one size share their offset mod 64: each line once
+        // through the segment stage (LOAD 11); else the value-relative stream
+        if (!sha1_blocks_shift(wbuf, p, live, my_nfull, h, hook)) sha1_blocks_lds(wbuf, whi, my_nfull, issue, h, hook);
+        crc = __builtin_bswap32(cs);
         for (uint64_t j = uint64_t(my_nfull) * 64; j < ln; ++j) crc = crc_byte<1>(crc, p[j], tab);
         crc = ~crc;
         if (live) {
@@ -1406,7 +1431,7 @@ __global__ __launch_bounds__(kBlock, kLeafWavesPerSimd) void k_leaf_verify(
         }
     } else {
         // deferred: Key ++ Value is one contiguous span of the record
-        crc = crc_span<1>(key, ks + ln, tab);
+        crc = crc_span<1, true>(key, ks + ln, tab, swtab);
         if (live) {
             voff[t] = uint64_t(p - stream);
             vlen[t] = ln;
