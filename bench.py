@@ -32,6 +32,11 @@ SHA1_VALU_CEILING_GBS = 4100.0
 # random bytes from HBM (2.04 GHz against 2.37 GHz from L2/registers, board power
 # limit; tools/pattern_power.hip -> profiles/r01_clock_power.txt).
 STREAMING_CLOCK_RATIO = 2.04 / 2.37
+# k_leaf_verify's block loop issues ~711 VALU per 64-B block (SHA-1's 614 plus
+# 97 for the CRC's byte indices and three-input XORs; ISA count, DESIGN.md
+# K1v) against ~618.5 for the plain leaf kernel, so its compute ceiling is the
+# SHA-1 one scaled by that ratio.
+VERIFY_VALU_RATIO = 618.5 / 711.0
 SEED = 0x6E616B65
 SEED_MIXED = 0x6E616B66
 
@@ -410,11 +415,12 @@ def main():
         total_bytes = nbytes * world * args.steps
         value = total_bytes / elapsed / 2**30
         achieved = nbytes / (leaf_ms * 1e-3) / 1e9  # algorithmic payload bytes per K1 launch
+        valu_ceiling = SHA1_VALU_CEILING_GBS * (VERIFY_VALU_RATIO if verify_crc else 1.0)
         traffic, traffic_bounds = None, None
         # PMC-measured HBM bytes of this config's leaf kernel (separate rocprofv3
         # passes: tools/pmc_sizes.sh for cfg2, tools/pmc_config.sh for the others)
         pmc_name = {"sstable4k": "pmc_traffic.json", "records": "pmc_traffic_records.json",
-                    "mixed": "pmc_traffic_mixed.json"}.get(args.config)
+                    "mixed": "pmc_traffic_mixed.json", "records_verify": "pmc_traffic_records_verify.json"}.get(args.config)
         pmc_path = os.path.join(ROOT, "profiles", pmc_name) if pmc_name else None
         if pmc_path and os.path.exists(pmc_path):
             with open(pmc_path) as f:
@@ -464,8 +470,11 @@ def main():
                 "bound": "hbm",
                 "kernel": ("leaf phase: length sort + ragged leaf SHA-1 (%s)" % LEAF_KERNEL.get(args.deep, "default"))
                           if mixed else
-                          ("leaf phase: k_leaf_verify (record CRC + leaf SHA-1, input order)" if verify_crc else
-                           "leaf phase: k_leaf<offsets, aligned-segment stage + register shift> (input order)") if records else
+                          ("leaf phase: k_leaf_verify (header parse + record CRC + leaf SHA-1, input order)"
+                           if verify_crc else
+                           ("leaf phase: k_locate + k_leaf<offsets, aligned-segment stage> (input order)"
+                            if args.records_fused == 0 else
+                            "leaf phase: k_leaf_records (header parse + aligned-segment stage, input order)")) if records else
                           "k_leaf<strided, LDS-DMA> (leaf SHA-1, level 0)",
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
@@ -476,10 +485,10 @@ def main():
                 "step_frac": round(nbytes / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
                 "traffic_bounds": traffic_bounds,  # RDREQ x 64 .. x 128 B (profiles/pmc_traffic.json)
-                "valu_ceiling": SHA1_VALU_CEILING_GBS,
-                "valu_frac": round(achieved / SHA1_VALU_CEILING_GBS, 4),
-                "valu_ceiling_at_streaming_clock": round(SHA1_VALU_CEILING_GBS * STREAMING_CLOCK_RATIO, 1),
-                "valu_frac_at_streaming_clock": round(achieved / (SHA1_VALU_CEILING_GBS * STREAMING_CLOCK_RATIO), 4),
+                "valu_ceiling": round(valu_ceiling, 1),
+                "valu_frac": round(achieved / valu_ceiling, 4),
+                "valu_ceiling_at_streaming_clock": round(valu_ceiling * STREAMING_CLOCK_RATIO, 1),
+                "valu_frac_at_streaming_clock": round(achieved / (valu_ceiling * STREAMING_CLOCK_RATIO), 4),
             },
             "kernel_ms": {"leaf": round(leaf_ms, 4), "tree_reduce": round(reduce_ms, 4),
                           "bfs_image": round(bfs_ms, 4)},
