@@ -275,8 +275,9 @@ __device__ __forceinline__ void load_window(const uint8_t* p, uint32_t avail, ui
 
 // ALIGNED: the caller guarantees p is 16-byte aligned (host-checked base and
 // stride, or host-packed values); otherwise a wave-uniform test picks the path.
-template <bool ALIGNED>
-__device__ __forceinline__ void sha1_tail(const uint8_t* p, uint64_t len, uint32_t h[5]);
+struct NoRaw;
+template <bool ALIGNED, class Hook = NoRaw>
+__device__ __forceinline__ void sha1_tail(const uint8_t* p, uint64_t len, uint32_t h[5], Hook hook = Hook{});
 
 // Whole message in registers: full blocks with a one-block register prefetch
 // (aligned) or the 80-byte funnel window (unaligned), then the padding blocks.
@@ -318,8 +319,10 @@ __device__ __forceinline__ void sha1_value(const uint8_t* p, uint64_t len, uint3
 // The 1-2 padding blocks: rem = len % 64 value bytes, 0x80, zeros, 64-bit
 // big-endian bit length (FIPS 180-4 5.1.1).  h holds the state after the full
 // blocks.
-template <bool ALIGNED>
-__device__ __forceinline__ void sha1_tail(const uint8_t* p, uint64_t len, uint32_t h[5]) {
+// hook.tail(w, rem): the tail block's big-endian words before the padding is
+// applied (rem = len % 64 value bytes), for k_leaf_verify's checksum.
+template <bool ALIGNED, class Hook>
+__device__ __forceinline__ void sha1_tail(const uint8_t* p, uint64_t len, uint32_t h[5], Hook hook) {
     uint32_t w[16];
     const uint64_t nfull = len >> 6;
     const uint32_t rem = uint32_t(len & 63);
@@ -349,6 +352,7 @@ __device__ __forceinline__ void sha1_tail(const uint8_t* p, uint64_t len, uint32
         load_window(pt, rem, d);
         be16_funnel(d, uint32_t(reinterpret_cast<uintptr_t>(pt) & 15), w);
     }
+    hook.tail(w, rem);
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
         const int v = int(rem) - 4 * j;  // value bytes inside word j
@@ -441,6 +445,7 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
 struct NoRaw {
     __device__ __forceinline__ void operator()(const uint4*, const uint32_t*) const {}
     __device__ __forceinline__ void be(const uint32_t*) const {}
+    __device__ __forceinline__ void tail(const uint32_t*, uint32_t) const {}
 };
 
 template <class Issue, class Raw = NoRaw>
@@ -1317,8 +1322,25 @@ __global__ __launch_bounds__(kBlock, (LOAD == 6 || LOAD == 7) ? 2 : ((LOAD == 4 
 struct CrcBE {
     uint32_t& cs;
     const uint32_t* swtab;
+    const uint32_t* tab0;  // T[0], for the last 0-3 bytes
     __device__ __forceinline__ void be(const uint32_t* w) { cs = crc_block16<1>(cs, w, swtab); }
     __device__ __forceinline__ void operator()(const uint4*, const uint32_t* w) { be(w); }
+    // the value's last rem (< 64) bytes, from the words sha1_tail loaded: whole
+    // words in the swapped domain, then the 0-3 bytes of the partial word
+    __device__ __forceinline__ void tail(const uint32_t* w, uint32_t rem) {
+        const uint32_t nfw = rem >> 2;
+#pragma unroll
+        for (int i = 0; i < 15; ++i) {
+            const uint32_t u = crc_x_last<1>(cs ^ w[i], swtab);
+            cs = uint32_t(i) < nfw ? u : cs;
+        }
+        uint32_t pw = 0u;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) pw = uint32_t(i) == nfw ? w[i] : pw;
+        uint32_t crc = __builtin_bswap32(cs);
+        for (uint32_t b = 0; b < (rem & 3u); ++b) crc = crc_byte<1>(crc, (pw >> (24u - 8u * b)) & 0xFFu, tab0);
+        cs = __builtin_bswap32(crc);
+    }
 };
 
 // K1v: the compaction read of a Data table in one pass.  For every record it
@@ -1414,21 +1436,19 @@ __global__ __launch_bounds__(kBlock, NKV_VERIFY_WAVES) void k_leaf_verify(
                 if (b < nf[k]) __builtin_amdgcn_global_load_lds(src[k] + 64ull * b, wbuf + 1024 * k, 16, 0, 0);
         };
         uint32_t cs = __builtin_bswap32(crc);
-        CrcBE hook{cs, swtab};
+        CrcBE hook{cs, swtab, tab};
         // records of one size share their offset mod 64: each line once
         // through the segment stage (LOAD 11); else the value-relative stream
         if (!sha1_blocks_shift(wbuf, p, live, my_nfull, h, hook)) sha1_blocks_lds(wbuf, whi, my_nfull, issue, h, hook);
-        crc = __builtin_bswap32(cs);
-        for (uint64_t j = uint64_t(my_nfull) * 64; j < ln; ++j) crc = crc_byte<1>(crc, p[j], tab);
-        crc = ~crc;
         if (live) {
-            sha1_tail<false>(p, ln, h);
+            sha1_tail<false>(p, ln, h, hook);  // the tail's checksum from the same loads
             store_digest(nodes, t, h);
             if (voff) {
                 voff[t] = kDone;
                 vlen[t] = 0;
             }
         }
+        crc = ~__builtin_bswap32(cs);
     } else {
         // deferred: Key ++ Value is one contiguous span of the record
         crc = crc_span<1, true>(key, ks + ln, tab, swtab);
