@@ -45,14 +45,6 @@ __device__ unsigned long long* g_diag = nullptr;
     } while (0)
 #endif
 
-// little-endian u64 at any alignment (record header fields)
-__device__ __forceinline__ uint64_t ld_le64(const uint8_t* p) {
-    uint64_t v = 0;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) v |= uint64_t(p[i]) << (8 * i);
-    return v;
-}
-
 // KeySize and ValueSize (header bytes 14..29, record.go:191-199) of the
 // record at p, from two or three aligned 8-byte loads and a funnel shift
 // instead of sixteen byte loads (one line request per lane per load rather
@@ -1325,12 +1317,12 @@ struct CrcBE {
     const uint32_t* tab0;  // T[0], for the last 0-3 bytes
     __device__ __forceinline__ void be(const uint32_t* w) { cs = crc_block16<1>(cs, w, swtab); }
     __device__ __forceinline__ void operator()(const uint4*, const uint32_t* w) { be(w); }
-    // the value's last rem (< 64) bytes, from the words sha1_tail loaded: whole
-    // words in the swapped domain, then the 0-3 bytes of the partial word
-    __device__ __forceinline__ void tail(const uint32_t* w, uint32_t rem) {
-        const uint32_t nfw = rem >> 2;
+    // the first nb (<= 64) bytes held by 16 big-endian words: whole words in
+    // the swapped domain, then the 0-3 bytes of the partial word
+    __device__ __forceinline__ void span(const uint32_t* w, uint32_t nb) {
+        const uint32_t nfw = nb >> 2;
 #pragma unroll
-        for (int i = 0; i < 15; ++i) {
+        for (int i = 0; i < 16; ++i) {
             const uint32_t u = crc_x_last<1>(cs ^ w[i], swtab);
             cs = uint32_t(i) < nfw ? u : cs;
         }
@@ -1338,9 +1330,11 @@ struct CrcBE {
 #pragma unroll
         for (int i = 0; i < 16; ++i) pw = uint32_t(i) == nfw ? w[i] : pw;
         uint32_t crc = __builtin_bswap32(cs);
-        for (uint32_t b = 0; b < (rem & 3u); ++b) crc = crc_byte<1>(crc, (pw >> (24u - 8u * b)) & 0xFFu, tab0);
+        for (uint32_t b = 0; b < (nb & 3u); ++b) crc = crc_byte<1>(crc, (pw >> (24u - 8u * b)) & 0xFFu, tab0);
         cs = __builtin_bswap32(crc);
     }
+    // the value's last rem (< 64) bytes, from the words sha1_tail loaded
+    __device__ __forceinline__ void tail(const uint32_t* w, uint32_t rem) { span(w, rem); }
 };
 
 // K1v: the compaction read of a Data table in one pass.  For every record it
@@ -1392,14 +1386,21 @@ __global__ __launch_bounds__(kBlock, NKV_VERIFY_WAVES) void k_leaf_verify(
     if (live) {
         const uint64_t r = rec_off[t];
         if (header_in(r, stream_len)) {
-            const uint64_t k = ld_le64(stream + r + 14), v = ld_le64(stream + r + 22);
+            uint64_t k, v;
+            ld_header_sizes(stream + r, k, v);
             if (k <= stream_len && v <= stream_len && r + 30 + k + v <= stream_len) {
                 key = stream + r + 30;
                 ks = k;
                 p = key + k;
                 ln = v;
-                stored = uint32_t(stream[r]) | uint32_t(stream[r + 1]) << 8 | uint32_t(stream[r + 2]) << 16 |
-                         uint32_t(stream[r + 3]) << 24;
+                // the stored Crc (header bytes 0..3) from the one or two aligned
+                // words that hold it
+                const uint8_t* c = stream + r;
+                const uint32_t mis = uint32_t(reinterpret_cast<uintptr_t>(c) & 3u);
+                const uint32_t* cw = reinterpret_cast<const uint32_t*>(c - mis);
+                const uint32_t c0 = cw[0];
+                const uint32_t c1 = mis ? cw[1] : 0u;
+                stored = mis ? (c0 >> (8u * mis)) | (c1 << (32u - 8u * mis)) : c0;
             } else {
                 hdr_bad = true;
             }
@@ -1415,8 +1416,20 @@ __global__ __launch_bounds__(kBlock, NKV_VERIFY_WAVES) void k_leaf_verify(
     const bool hash = any && (policy == 0 || (policy == 1 && whi <= wlo + max(1u, wlo / 16u)));
     uint32_t crc;
     if (hash) {
-        crc = 0xFFFFFFFFu;
-        for (uint64_t j = 0; j < ks; ++j) crc = crc_byte<1>(crc, key[j], tab);
+        uint32_t cs = 0xFFFFFFFFu;  // bswap(~0): the CRC starts in the swapped domain
+        CrcBE hook{cs, swtab, tab};
+        {  // the key, 64 bytes at a time from aligned 16-byte loads (most keys: one pass)
+            const uint32_t kch = wave_max_u32(uint32_t(min<uint64_t>((ks + 63) >> 6, 0xFFFFFFFFull)));
+            for (uint32_t c = 0; c < kch; ++c) {
+                const uint64_t done = 64ull * c;
+                const uint32_t avail = ks > done ? uint32_t(min<uint64_t>(64ull, ks - done)) : 0u;
+                const uint8_t* kc = key + (avail ? done : 0ull);
+                uint32_t d[20], w[16];
+                load_window(kc, avail, d);
+                be16_funnel(d, uint32_t(reinterpret_cast<uintptr_t>(kc) & 15u), w);
+                hook.span(w, avail);
+            }
+        }
         uint8_t* wbuf = smem + 4096 * wave;
         const uint32_t q = (uint32_t(lane) & 3u) ^ ((uint32_t(lane) >> 4) & 3u);
         uint32_t h[5];
@@ -1435,8 +1448,6 @@ __global__ __launch_bounds__(kBlock, NKV_VERIFY_WAVES) void k_leaf_verify(
             for (int k = 0; k < 4; ++k)
                 if (b < nf[k]) __builtin_amdgcn_global_load_lds(src[k] + 64ull * b, wbuf + 1024 * k, 16, 0, 0);
         };
-        uint32_t cs = __builtin_bswap32(crc);
-        CrcBE hook{cs, swtab, tab};
         // records of one size share their offset mod 64: each line once
         // through the segment stage (LOAD 11); else the value-relative stream
         if (!sha1_blocks_shift(wbuf, p, live, my_nfull, h, hook)) sha1_blocks_lds(wbuf, whi, my_nfull, issue, h, hook);

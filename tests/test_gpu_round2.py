@@ -494,3 +494,44 @@ def test_verify_records_partly_ragged_every_policy(nkv, oracle, bucket):
     finally:
         ctx.set_option(_lib.NKV_OPT_BUCKET, 2)
         ctx.set_stream(_lib._OWN)
+
+
+@pytest.mark.parametrize("klen", [0, 1, 15, 16, 63, 64, 65, 127, 128, 200, 1000])
+def test_verify_records_key_lengths(nkv, oracle, klen):
+    """k_leaf_verify checksums the Key in 64-byte pieces from aligned 16-byte
+    loads (one piece for most keys): keys of every length around the piece
+    size, at every record alignment (records of one Value size, so every wave
+    takes the checksum + hash pass), against zlib and the oracle's tree."""
+    import zlib
+    import torch
+    from nakevaleng_amd import record
+    _lib, ctx = nkv
+    L = _lib.lib()
+    rng = np.random.default_rng(900 + klen)
+    n = 64 * 9 + 5
+    recs = [record.New(rng.bytes(klen), rng.bytes(3000), timestamp=i) for i in range(n)]
+    stream, sizes = record.data_table(recs)
+    pad = int(rng.integers(1, 16))  # a leading gap: records at odd offsets
+    buf = np.frombuffer(b"\x00" * pad + stream, np.uint8).copy()
+    roff = np.zeros(n, np.uint64)
+    roff[1:] = np.cumsum(np.asarray(sizes, np.uint64)[:-1])
+    roff += pad
+    off, ln = record.value_spans(stream, sizes)
+    off = off + pad
+    want = oracle.tree_from_digests(oracle.leaf_hashes(buf, off, ln, threads=8))
+    crcs = np.array([zlib.crc32(buf[int(roff[i]) + 30:int(off[i] + ln[i])].tobytes()) for i in range(n)], np.uint32)
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    try:
+        d = torch.from_numpy(buf).cuda()
+        d_roff = torch.from_numpy(roff.view(np.int64)).cuda()
+        d_nodes = torch.zeros(L.nkv_total_nodes(n) * 20, dtype=torch.uint8, device="cuda")
+        d_crc = torch.zeros(n, dtype=torch.int32, device="cuda")
+        d_stats = torch.zeros(3, dtype=torch.int64, device="cuda")
+        _lib.check(L.nkv_tree_verify_records_dev(ctx.h, d.data_ptr(), len(buf), d_roff.data_ptr(), n,
+                                                 d_nodes.data_ptr(), d_crc.data_ptr(), d_stats.data_ptr()))
+        torch.cuda.synchronize()
+        assert np.array_equal(d_crc.cpu().numpy().view(np.uint32), crcs)
+        assert d_stats.cpu().tolist() == [0, -1, 0]
+        assert np.array_equal(d_nodes.cpu().numpy().reshape(-1, 20), want)
+    finally:
+        ctx.set_stream(_lib._OWN)
