@@ -345,7 +345,10 @@ int leaf_level(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint6
                                       c->deep != 0));
     if (n > 0x7fffffffull) return NKV_ERR_INVALID;
     const Gate wide{range.range, plan == kGated ? 2 : 0};
+    const size_t keys_cap = c->d_keys.cap;
     TRY(grow(c->d_keys, 4 * sort_hist_words(n)));
+    if (c->d_keys.cap != keys_cap)  // (re)allocated scratch: the sort's bucket totals start at zero
+        HIPTRY(hipMemsetAsync(c->d_keys.p, 0, 4 * sort_head_words(), c->stream));
     TRY(grow(c->d_perm, 4 * n));
     uint32_t* perm = static_cast<uint32_t*>(c->d_perm.p);
     HIPTRY(sort_by_length_desc(len, n, perm, static_cast<uint32_t*>(c->d_keys.p), c->stream, wide));

@@ -115,8 +115,10 @@ hipError_t scan_exclusive_u64(const uint64_t* in, uint64_t* out, uint64_t n, voi
 uint64_t scan_sums_words(uint64_t n);
 hipError_t scan_exclusive_u32(uint32_t* a, uint64_t n, uint32_t* sums, hipStream_t s, Gate gate = Gate{});
 // Length-sorted order (compression count, longest first) into perm[0..n);
-// hist: sort_hist_words(n) u32 of scratch.
+// scratch: sort_hist_words(n) u32 whose first sort_head_words() must be zero
+// when the scratch is first used (the sort leaves them zero again).
 uint64_t sort_hist_words(uint64_t n);
+uint64_t sort_head_words();
 hipError_t sort_by_length_desc(const uint64_t* len, uint64_t n, uint32_t* perm, uint32_t* hist, hipStream_t s,
                                Gate gate = Gate{});
 // crc.hip: CRC-32/IEEE of byte spans / of records' Key ++ Value (stats: 3 x u64,

@@ -1739,9 +1739,9 @@ __global__ __launch_bounds__(1024) void k_reduce_wide(uint8_t* __restrict__ node
 // longest first (longest-processing-time order for the dispatcher), and the
 // leaf kernel reads them through the permutation.  A counting sort over 640
 // buckets (exact below 256 compressions, 16 buckets per octave above, so a
-// bucket spans at most 1/16 of its length) in three gated kernels: per-tile
-// histograms, one column scan, a scatter.  Order inside a bucket is arbitrary
-// (digests are written by leaf index, so results do not depend on it).
+// bucket spans at most 1/16 of its length) in two gated kernels (below).
+// Order inside a bucket is arbitrary (digests are written by leaf index, so
+// results do not depend on it).
 __device__ __forceinline__ uint32_t len_bucket_desc(uint64_t len) {
     const uint64_t c64 = compressions(len);
     const uint32_t c = c64 > 0xFFFFFFFFull ? 0xFFFFFFFFu : uint32_t(c64);
@@ -1753,14 +1753,22 @@ __device__ __forceinline__ uint32_t len_bucket_desc(uint64_t len) {
     return kLenBuckets - 1u - k;
 }
 
-__global__ __launch_bounds__(kBlock) void k_len_hist(const uint64_t* __restrict__ len, uint64_t n,
-                                                      uint32_t* __restrict__ hist, uint32_t tiles, Gate gate) {
+// Two-launch form: k_len_hist_alloc reserves each (bucket, tile) run inside
+// its bucket with one device atomic per nonzero bucket (bucket totals at the
+// head of the scratch), and k_len_scatter_alloc scans the 640 totals itself,
+// so the three column-scan launches go away.  Runs of one bucket land in the
+// order the tiles' atomics arrive (order inside a bucket is free).  The last
+// workgroup of the scatter (a ticket after every workgroup has read the
+// totals) restores the totals to zero for the next sort.
+constexpr uint32_t kSortHead = 1024;  // [0, 640) bucket totals, [640] ticket
+__global__ __launch_bounds__(kBlock) void k_len_hist_alloc(const uint64_t* __restrict__ len, uint64_t n,
+                                                            uint32_t* __restrict__ scratch, uint32_t tiles,
+                                                            Gate gate) {
     __shared__ uint32_t h[kLenBuckets];
     if (!gate.open()) return;
     for (uint32_t i = threadIdx.x; i < kLenBuckets; i += kBlock) h[i] = 0u;
     __syncthreads();
     const uint64_t base = uint64_t(blockIdx.x) * kSortTile;
-    // all of the thread's loads first (one memory latency per tile, not four)
     uint32_t bk[kSortItems];
 #pragma unroll
     for (int j = 0; j < kSortItems; ++j) {
@@ -1771,18 +1779,47 @@ __global__ __launch_bounds__(kBlock) void k_len_hist(const uint64_t* __restrict_
     for (int j = 0; j < kSortItems; ++j)
         if (bk[j] < kLenBuckets) atomicAdd(&h[bk[j]], 1u);
     __syncthreads();
-    // bucket-major: the exclusive scan of hist is then every (bucket, tile)
-    // slot's first output position
-    for (uint32_t i = threadIdx.x; i < kLenBuckets; i += kBlock) hist[uint64_t(i) * tiles + blockIdx.x] = h[i];
+    uint32_t* hist = scratch + kSortHead;
+    for (uint32_t i = threadIdx.x; i < kLenBuckets; i += kBlock) {
+        const uint32_t c = h[i];
+        hist[uint64_t(i) * tiles + blockIdx.x] = c ? atomicAdd(scratch + i, c) : 0u;
+    }
 }
 
-__global__ __launch_bounds__(kBlock) void k_len_scatter(const uint64_t* __restrict__ len, uint64_t n,
-                                                         const uint32_t* __restrict__ hist, uint32_t tiles,
-                                                         uint32_t* __restrict__ perm, Gate gate) {
+__global__ __launch_bounds__(kBlock) void k_len_scatter_alloc(const uint64_t* __restrict__ len, uint64_t n,
+                                                               uint32_t* __restrict__ scratch, uint32_t tiles,
+                                                               uint32_t* __restrict__ perm, Gate gate) {
     __shared__ uint32_t cur[kLenBuckets];
+    __shared__ uint32_t last;
     if (!gate.open()) return;
-    for (uint32_t i = threadIdx.x; i < kLenBuckets; i += kBlock) cur[i] = hist[uint64_t(i) * tiles + blockIdx.x];
+    if (threadIdx.x < 64) {  // exclusive scan of the bucket totals, 64 at a time
+        const int lane = threadIdx.x;
+        uint32_t carry = 0u;
+        for (uint32_t c0 = 0; c0 < kLenBuckets; c0 += 64) {
+            const uint32_t v = scratch[c0 + lane];
+            uint32_t x = v;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = uint32_t(__shfl_up(int(x), o));
+                if (lane >= o) x += y;
+            }
+            cur[c0 + lane] = carry + x - v;
+            carry += uint32_t(__shfl(int(x), 63));
+        }
+    }
     __syncthreads();
+    const uint32_t* hist = scratch + kSortHead;
+    for (uint32_t i = threadIdx.x; i < kLenBuckets; i += kBlock) cur[i] += hist[uint64_t(i) * tiles + blockIdx.x];
+    __syncthreads();  // every read of the totals is done
+    if (threadIdx.x == 0) {
+        __threadfence();
+        last = atomicAdd(scratch + kLenBuckets, 1u) == tiles - 1u ? 1u : 0u;
+    }
+    __syncthreads();
+    if (last) {  // every workgroup has read the totals: restore them for the next sort
+        for (uint32_t i = threadIdx.x; i < kLenBuckets; i += kBlock) scratch[i] = 0u;
+        if (threadIdx.x == 0) scratch[kLenBuckets] = 0u;
+    }
     const uint64_t base = uint64_t(blockIdx.x) * kSortTile;
     uint32_t bk[kSortItems];
 #pragma unroll
@@ -1790,8 +1827,6 @@ __global__ __launch_bounds__(kBlock) void k_len_scatter(const uint64_t* __restri
         const uint64_t i = base + uint64_t(j) * kBlock + threadIdx.x;
         bk[j] = i < n ? len_bucket_desc(len[i]) : kLenBuckets;
     }
-    // in j order per thread, as before (the order inside a bucket is arbitrary
-    // anyway: digests are written by leaf index)
 #pragma unroll
     for (int j = 0; j < kSortItems; ++j)
         if (bk[j] < kLenBuckets)
@@ -2382,21 +2417,19 @@ hipError_t scan_exclusive_u32(uint32_t* a, uint64_t n, uint32_t* sums, hipStream
     return hipGetLastError();
 }
 
-uint64_t sort_hist_words(uint64_t n) {
-    const uint64_t h = ((n + kSortTile - 1) / kSortTile) * kLenBuckets;
-    return h + scan_sums_words(h);
-}
+uint64_t sort_hist_words(uint64_t n) { return kSortHead + ((n + kSortTile - 1) / kSortTile) * kLenBuckets; }
+uint64_t sort_head_words() { return kSortHead; }
 
-hipError_t sort_by_length_desc(const uint64_t* len, uint64_t n, uint32_t* perm, uint32_t* hist, hipStream_t s,
+// scratch: sort_hist_words(n) u32 whose first sort_head_words() are zero
+// (the two-launch form keeps them zero between calls)
+hipError_t sort_by_length_desc(const uint64_t* len, uint64_t n, uint32_t* perm, uint32_t* scratch, hipStream_t s,
                                Gate gate) {
     const uint64_t tiles = (n + kSortTile - 1) / kSortTile;
     if (tiles == 0) return hipSuccess;
-    const uint64_t h = tiles * kLenBuckets;
-    hipLaunchKernelGGL(k_len_hist, dim3(uint32_t(tiles)), dim3(kBlock), 0, s, len, n, hist, uint32_t(tiles), gate);
-    hipError_t e = scan_exclusive_u32(hist, h, hist + h, s, gate);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_len_scatter, dim3(uint32_t(tiles)), dim3(kBlock), 0, s, len, n, hist, uint32_t(tiles),
-                       perm, gate);
+    hipLaunchKernelGGL(k_len_hist_alloc, dim3(uint32_t(tiles)), dim3(kBlock), 0, s, len, n, scratch,
+                       uint32_t(tiles), gate);
+    hipLaunchKernelGGL(k_len_scatter_alloc, dim3(uint32_t(tiles)), dim3(kBlock), 0, s, len, n, scratch,
+                       uint32_t(tiles), perm, gate);
     return hipGetLastError();
 }
 
