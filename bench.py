@@ -89,6 +89,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-leaves", type=int, default=1 << 20)
     ap.add_argument("--verify", action="store_true", help="check the root against the C oracle")
+    ap.add_argument("--dist", action="store_true",
+                    help="join the RCCL group and all-gather the roots even at world size 1 (exercises the N > 1 path on one GPU)")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="do not record per-kernel HIP events inside the timed loop")
     return ap.parse_args()
@@ -206,7 +208,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    use_dist = world > 1 or args.dist
+    if use_dist:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
@@ -215,7 +218,7 @@ def main():
     from nakevaleng_amd import build as nb
     if rank == 0 or not os.path.exists(nb.SO):
         nb.build()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     from nakevaleng_amd import _lib
 
@@ -315,7 +318,7 @@ def main():
     # all-gather against a 1.2 ms table) before it rewrites bufs[i % 2].
     # Every gather still completes inside the timed region (the final
     # synchronize waits for it).
-    rg = RootGather(nodes, roots, dist if (world > 1 and not one_tree) else None)
+    rg = RootGather(nodes, roots, dist if (use_dist and not one_tree) else None)
 
     def step():
         nonlocal nodes
@@ -345,7 +348,7 @@ def main():
         step()
     drain()
     torch.cuda.synchronize()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
     ctx.set_timing(not args.no_kernel_timing)
@@ -354,7 +357,7 @@ def main():
         step()
     drain()
     torch.cuda.synchronize()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
@@ -367,12 +370,16 @@ def main():
         drain()
         calls, leaf_ms_tot, reduce_ms_tot = ctx.timing_summary()
         ctx.set_timing(False)
-    if world > 1:
+    if use_dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
     root = nodes[-20:].cpu().numpy().tobytes().hex()
+    gathered_ok = None
+    if rg.dist:  # every rank's slot of the last gather holds that rank's root
+        got = rg.last_roots().cpu().numpy().reshape(world, 20)
+        gathered_ok = got[rank].tobytes().hex() == root
     leaf_ms = leaf_ms_tot / max(calls, 1)
     reduce_ms = reduce_ms_tot / max(calls, 1)
 
@@ -497,9 +504,11 @@ def main():
         }
         if verified is not None:
             out["verified_vs_oracle"] = verified
+        if gathered_ok is not None:
+            out["root_gather_ok"] = gathered_ok
         print(json.dumps(out), flush=True)
     ctx.close()
-    if world > 1:
+    if use_dist:
         dist.barrier()
         dist.destroy_process_group()
 

@@ -104,3 +104,22 @@ def test_root_gather_pipeline_world2():
     # step i's gathered roots: rank 0's i, then rank 1's 16 + i
     want = [[i] * 20 + [16 + i] * 20 for i in range(7)]
     assert res[0] == want and res[1] == want
+
+
+@pytest.mark.gpu
+def test_rccl_root_gather_on_gpu():
+    """The N > 1 code path on hardware, at world size 1 (the GPU box has one
+    device): torch.distributed.run starts the rank, which joins the nccl (RCCL)
+    group bound to its LOCAL_RANK device and all-gathers every step's root; the
+    gathered slot must hold the rank's own root and the root must match the oracle."""
+    import json
+    import subprocess
+    cmd = bench.launcher_cmd(["--gpus", "1", "--dist", "--leaves", "65536", "--steps", "4", "--warmup", "1",
+                              "--preroll-s", "0", "--no-cpu-baseline", "--verify"], 1, _free_port())
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    line = json.loads(out.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 1 and line["steps"] == 4
+    assert line["root_gather_ok"] is True
+    assert line["verified_vs_oracle"] is True

@@ -13,6 +13,38 @@
 
 namespace nkv {
 
+// Two independent messages per lane, their rounds interleaved (does a lone
+// wave issue faster with twice the ILP?  If its rate is the issue cadence,
+// a block pair costs twice a block).
+__device__ __forceinline__ void sha1_compress2(uint32_t h[5], uint32_t w[16], uint32_t g[5], uint32_t x[16]) {
+    uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4];
+    uint32_t a2 = g[0], b2 = g[1], c2 = g[2], d2 = g[3], e2 = g[4];
+#pragma unroll
+    for (int t = 0; t < 80; ++t) {
+        uint32_t wt, xt;
+        if (t < 16) {
+            wt = w[t];
+            xt = x[t];
+        } else {
+            wt = rotl(xor3(w[(t - 3) & 15], w[(t - 8) & 15], w[(t - 14) & 15]) ^ w[t & 15], 1);
+            w[t & 15] = wt;
+            xt = rotl(xor3(x[(t - 3) & 15], x[(t - 8) & 15], x[(t - 14) & 15]) ^ x[t & 15], 1);
+            x[t & 15] = xt;
+        }
+        uint32_t f, f2, k;
+        if (t < 20) { f = ch(b, c, d); f2 = ch(b2, c2, d2); k = 0x5A827999u; }
+        else if (t < 40) { f = xor3(b, c, d); f2 = xor3(b2, c2, d2); k = 0x6ED9EBA1u; }
+        else if (t < 60) { f = maj(b, c, d); f2 = maj(b2, c2, d2); k = 0x8F1BBCDCu; }
+        else { f = xor3(b, c, d); f2 = xor3(b2, c2, d2); k = 0xCA62C1D6u; }
+        const uint32_t tmp = add3(rotl(a, 5), f, add3k(e, wt, k));
+        const uint32_t tmp2 = add3(rotl(a2, 5), f2, add3k(e2, xt, k));
+        e = d; d = c; c = rotl(b, 30); b = a; a = tmp;
+        e2 = d2; d2 = c2; c2 = rotl(b2, 30); b2 = a2; a2 = tmp2;
+    }
+    h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e;
+    g[0] += a2; g[1] += b2; g[2] += c2; g[3] += d2; g[4] += e2;
+}
+
 template <int V>
 __global__ __launch_bounds__(64, 1) void k_lone(const uint8_t* __restrict__ base, uint64_t vstride,
                                                 uint32_t nblk, int hbm, unsigned long long* __restrict__ out) {
@@ -35,6 +67,20 @@ __global__ __launch_bounds__(64, 1) void k_lone(const uint8_t* __restrict__ base
         sha1_blocks_ring_vc<V + 1>(smem, p, nblk, h);
     } else if constexpr (V == 4) {
         sha1_blocks_ring_pipe<3>(smem, p, nblk, h);
+    } else if constexpr (V == 7) {
+        // nblk blocks as nblk / 2 interleaved pairs (two messages per lane)
+        uint32_t g[5];
+        sha1_init(g);
+        for (uint32_t b = 0; b < nblk; b += 2) {
+            uint32_t w[16], x[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                w[i] = bswap32(uint32_t(v) + i * 0x9E3779B9u + b);
+                x[i] = bswap32(uint32_t(v) * 3u + i * 0x7F4A7C15u + b);
+            }
+            sha1_compress2(h, w, g, x);
+        }
+        h[0] ^= g[0];
     } else if constexpr (V == 5 || V == 6) {
         // V 5: only lanes 0..31 active; V 6: only lanes 0..15 (does a lone
         // wave with a partial exec mask issue faster?)
@@ -100,6 +146,14 @@ int main() {
     uint8_t* d;
     if (hipMalloc(&d, bytes + 4096) != hipSuccess) return 1;
     (void)hipMemset(d, 0x5a, bytes + 4096);
+    if (getenv("NKV_LONE_ILP")) {
+        for (int waves : {256, 1024}) {
+            run<0>("regs only, 1 msg/lane", d, vstride, nblk, waves, 0);
+            run<7>("regs only, 2 msg/lane", d, vstride, nblk, waves, 0);
+        }
+        (void)hipFree(d);
+        return 0;
+    }
     if (getenv("NKV_LONE_EXEC")) {
         for (int waves : {256, 1024}) {
             run<0>("regs only, 64 lanes", d, vstride, nblk, waves, 0);
