@@ -116,7 +116,8 @@ struct nkv_ctx {
     std::vector<hipEvent_t> ring;
     size_t ring_used = 0;
     DevBuf d_data, d_off, d_len, d_nodes, d_img, d_tmp, d_err, d_aux, d_keys, d_perm, d_stmp, d_queue, d_stats,
-        d_range, d_sync, d_part, d_tmp2;
+        d_range, d_part, d_tmp2, d_flags;
+    int flag_set = 0;  // which of the two pass-flag sets in d_flags the next records call uses
     void* h_stage = nullptr;  // small pinned staging (offsets, lengths, stats)
     unsigned int* h_small = nullptr;  // 64 pinned bytes for device-to-host decisions
     size_t h_cap = 0;
@@ -177,7 +178,14 @@ int grow(DevBuf& b, size_t bytes) {
     return NKV_OK;
 }
 
-SyncSlot* sync_slot(nkv_ctx* c, SyncUse u) { return static_cast<SyncSlot*>(c->d_sync.p) + u; }
+// This call's pass flags and the set its leaf kernel resets for the next call
+// (internal.hpp kPassFlagWords); flip_pass_flags once that kernel is launched.
+void pass_flags(nkv_ctx* c, uint32_t** cur, uint32_t** next) {
+    uint32_t* f = static_cast<uint32_t*>(c->d_flags.p);
+    *cur = f + kPassFlagWords * c->flag_set;
+    *next = f + kPassFlagWords * (1 - c->flag_set);
+}
+void flip_pass_flags(nkv_ctx* c) { c->flag_set ^= 1; }
 
 // scratch for k_locate's per-workgroup partials
 int locate_parts(nkv_ctx* c, uint64_t n, uint32_t** part) {
@@ -339,7 +347,9 @@ int plan_of(nkv_ctx* c, const uint64_t* len, const uint64_t* host_len, uint64_t 
 // kernel (it runs when the range is narrow) unless the caller has its own
 // (narrow_kernel = false: k_leaf_verify).
 int leaf_level(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint64_t* len, uint64_t n,
-               bool aligned, uint8_t* nodes, int plan, Gate range, bool narrow_kernel = true) {
+               bool aligned, uint8_t* nodes, int plan, Gate range, bool narrow_kernel = true,
+               CopyWords cw = CopyWords{}) {
+    if (plan == kInputOrder && cw.n) return NKV_ERR_INVALID;  // the copy rides on the sort
     if (plan == kInputOrder)
         return st(launch_leaf_offsets(base, off, len, nullptr, n, aligned, c->leaf_load, nodes, c->stream,
                                       c->deep != 0));
@@ -351,17 +361,20 @@ int leaf_level(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint6
         HIPTRY(hipMemsetAsync(c->d_keys.p, 0, 4 * sort_head_words(), c->stream));
     TRY(grow(c->d_perm, 4 * n));
     uint32_t* perm = static_cast<uint32_t*>(c->d_perm.p);
-    HIPTRY(sort_by_length_desc(len, n, perm, static_cast<uint32_t*>(c->d_keys.p), c->stream, wide));
+    QueueInit qi;
     if (c->deep >= 2) {
         TRY(grow(c->d_queue, 4 * queue_words(n)));
+        qi = QueueInit{static_cast<uint32_t*>(c->d_queue.p), queue_words(n), uint32_t(c->queue_split)};
+    }
+    HIPTRY(sort_by_length_desc(len, n, perm, static_cast<uint32_t*>(c->d_keys.p), c->stream, wide, qi, cw));
+    if (c->deep >= 2) {
         const int ring = c->deep == 3 ? c->queue_ring : 0;
         // LDS per CU (160 KiB) holds 20 / 13 / 10 rings of 2 / 3 / 4 slots
         const int slots = ring % 10;
         const int max_waves = slots == 4 ? 2 : (slots == 3 ? 3 : 5);
         const int waves = ring ? std::min(c->queue_waves, max_waves) : 2;
         HIPTRY(launch_leaf_queue(base, off, len, perm, n, aligned, ring, static_cast<uint32_t*>(c->d_queue.p),
-                                 c->simds, uint32_t(waves), uint32_t(c->queue_split), nodes,
-                                 sync_slot(c, kSyncSplit), c->stream, wide));
+                                 c->simds, uint32_t(waves), nodes, c->stream, wide));
     } else {
         HIPTRY(launch_leaf_offsets(base, off, len, perm, n, aligned, c->leaf_load, nodes, c->stream, c->deep != 0,
                                    wide));
@@ -421,11 +434,18 @@ int records_tree(nkv_ctx* c, const uint8_t* stream, uint64_t stream_len, const u
     // for >= 4096 values; else everything sorted
     const int policy = (c->bucket == 0 || n <= 64) ? 0 : ((c->bucket == 2 && n >= 4096) ? 1 : 2);
     TRY(mark(c, 0));
-    HIPTRY(launch_leaf_records(stream, stream_len, rec_off, n, policy, voff, vlen, nodes, err, range, part,
-                               c->stream));
-    if (policy != 0)
-        TRY(leaf_level(c, stream, voff, vlen, n, false, nodes, policy == 2 ? kSorted : kGated, Gate{range, 0},
-                       false));
+    if (policy == 0) {
+        HIPTRY(launch_leaf_records(stream, stream_len, rec_off, n, policy, voff, vlen, nodes, err, range, part,
+                                   c->stream));
+    } else {  // deferred plan: the pass flags gate the sorted pass, whose first launch copies err out
+        uint32_t *flags, *next;
+        pass_flags(c, &flags, &next);
+        HIPTRY(launch_leaf_records(stream, stream_len, rec_off, n, policy, voff, vlen, nodes, nullptr, nullptr,
+                                   nullptr, c->stream, flags, next));
+        flip_pass_flags(c);
+        TRY(leaf_level(c, stream, voff, vlen, n, false, nodes, policy == 2 ? kSorted : kGated, Gate{flags, 0},
+                       false, CopyWords{flags + 2, err, 1}));
+    }
     TRY(mark(c, 1));
     HIPTRY(launch_reduce(nodes, n, 0, levels_of(n) - 1, c->stream));
     return mark(c, 2);
@@ -476,11 +496,11 @@ int nkv_ctx_create(int device, nkv_ctx** out) try {
     int rc = st(hipSetDevice(device));
     if (rc == NKV_OK) rc = st(hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking));
     if (rc == NKV_OK) rc = st(hipHostMalloc(reinterpret_cast<void**>(&c->h_small), 64, hipHostMallocDefault));
-    if (rc == NKV_OK) rc = grow(c->d_sync, sizeof(SyncSlot) * kSyncSlots);
-    if (rc == NKV_OK) {  // the grid-fold accumulators start (and every launch leaves them) at kSyncInit
-        SyncSlot init[kSyncSlots];
-        for (SyncSlot& x : init) x = kSyncInit;
-        rc = st(hipMemcpy(c->d_sync.p, init, sizeof(init), hipMemcpyHostToDevice));
+    if (rc == NKV_OK) rc = grow(c->d_flags, 4 * 2 * kPassFlagWords);
+    if (rc == NKV_OK) {  // both pass-flag sets start reset (each records call resets the other)
+        uint32_t init[2 * kPassFlagWords] = {};
+        for (uint32_t k = 0; k < 2; ++k) init[kPassFlagWords * k + 6] = init[kPassFlagWords * k + 7] = ~0u;
+        rc = st(hipMemcpy(c->d_flags.p, init, sizeof(init), hipMemcpyHostToDevice));
     }
     if (rc != NKV_OK) {
         nkv_ctx_destroy(c);
@@ -500,7 +520,7 @@ void nkv_ctx_destroy(nkv_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (DevBuf* b : {&c->d_data, &c->d_off, &c->d_len, &c->d_nodes, &c->d_img, &c->d_tmp,
                       &c->d_err, &c->d_aux, &c->d_keys, &c->d_perm, &c->d_stmp, &c->d_queue, &c->d_stats,
-                      &c->d_range, &c->d_sync, &c->d_part, &c->d_tmp2})
+                      &c->d_range, &c->d_part, &c->d_tmp2, &c->d_flags})
         if (b->p) (void)hipFree(b->p);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
     if (c->h_small) (void)hipHostFree(c->h_small);
@@ -1066,11 +1086,13 @@ int nkv_tree_verify_records_dev(nkv_ctx* c, const void* d_stream, uint64_t strea
         TRY(grow(c->d_stats, 24));
         stats = static_cast<unsigned long long*>(c->d_stats.p);
     }
-    HIPTRY(hipMemsetAsync(stats, 0, 24, c->stream));
-    HIPTRY(hipMemsetAsync(stats + 1, 0xFF, 8, c->stream));
     // records_tree's policy rule: input order without bucketing or for tiny
     // batches; auto for >= 4096 records; else everything sorted
     const int policy = (c->bucket == 0 || n <= 64) ? 0 : ((c->bucket == 2 && n >= 4096) ? 1 : 2);
+    if (policy == 0) {  // else the stats start in the pass flags (reset by the previous call)
+        HIPTRY(hipMemsetAsync(stats, 0, 24, c->stream));
+        HIPTRY(hipMemsetAsync(stats + 1, 0xFF, 8, c->stream));
+    }
     TRY(grow(c->d_off, 8 * n));
     TRY(grow(c->d_len, 8 * n));
     TRY(grow(c->d_range, 8));
@@ -1080,11 +1102,18 @@ int nkv_tree_verify_records_dev(nkv_ctx* c, const void* d_stream, uint64_t strea
     uint32_t* part = nullptr;
     TRY(locate_parts(c, n, &part));
     TRY(mark(c, 0));
-    HIPTRY(launch_leaf_verify(stream, stream_len, d_rec_off, n, policy, voff, vlen, nodes, d_crc, stats, range,
-                              part, c->stream));
-    if (policy != 0)
-        TRY(leaf_level(c, stream, voff, vlen, n, false, nodes, policy == 2 ? kSorted : kGated, Gate{range, 0},
-                       false));
+    if (policy == 0) {
+        HIPTRY(launch_leaf_verify(stream, stream_len, d_rec_off, n, policy, voff, vlen, nodes, d_crc, stats, range,
+                                  part, c->stream));
+    } else {  // as records_tree: the pass flags, the stats copied out by the sort's first launch
+        uint32_t *flags, *next;
+        pass_flags(c, &flags, &next);
+        HIPTRY(launch_leaf_verify(stream, stream_len, d_rec_off, n, policy, voff, vlen, nodes, d_crc, stats,
+                                  nullptr, nullptr, c->stream, flags, next));
+        flip_pass_flags(c);
+        TRY(leaf_level(c, stream, voff, vlen, n, false, nodes, policy == 2 ? kSorted : kGated, Gate{flags, 0},
+                       false, CopyWords{flags + 4, reinterpret_cast<uint32_t*>(stats), 6}));
+    }
     TRY(mark(c, 1));
     HIPTRY(launch_reduce(nodes, n, 0, levels_of(n) - 1, c->stream));
     return mark(c, 2);

@@ -44,21 +44,20 @@ struct Gate {
     }
 };
 
-// Grid-wide results without fill launches (kernels.hip grid_fold): each block
-// folds its partial into these accumulators with device-scope atomics, then
-// draws a ticket that wraps to 0; the block drawing the last one takes the
-// totals with atomicExch, which restores every word.  nkv_ctx_create writes
-// kSyncInit once; every launch leaves a slot as it found it.
-struct SyncSlot {
-    unsigned int ticket;     // 0
-    unsigned int lo;         // running min, identity 0xFFFFFFFF
-    unsigned int hi;         // running max, identity 0
-    unsigned int flag;       // running or, identity 0
-    unsigned long long sum;  // running sum, identity 0
-    unsigned long long pad;
+// Pass flags of the records entries' deferred plan (k_leaf_records,
+// k_leaf_verify), instead of per-workgroup partials and a fold launch: two
+// sets per context, used by alternate calls, and each call's leaf kernel
+// resets the other set, so no fill launch precedes it either.  Words: [0] 0
+// (the wide Gate's lo), [1] ~0 once a wave was deferred (its hi), [2] 1 if a
+// header lies outside the stream, [3] pad, [4..9] the verify pass's stats
+// (3 u64: mismatches, first mismatch, bad header), [10..16) pad.  The first
+// length-sort launch copies [2] (or the stats) to the caller (CopyWords).
+constexpr uint32_t kPassFlagWords = 16;
+struct CopyWords {
+    const uint32_t* src = nullptr;
+    uint32_t* dst = nullptr;
+    uint32_t n = 0;  // words, at most 256
 };
-constexpr SyncSlot kSyncInit{0u, 0xFFFFFFFFu, 0u, 0u, 0ull, 0ull};
-enum SyncUse { kSyncRange = 0, kSyncSplit = 2, kSyncSlots = 4 };
 
 // BFS image layout in image order (index 0 = top level).
 struct BfsLayout {
@@ -79,17 +78,24 @@ hipError_t launch_leaf_strided(const uint8_t* base, uint64_t stride, uint64_t L,
 hipError_t launch_leaf_offsets(const uint8_t* base, const uint64_t* off, const uint64_t* len,
                                const uint32_t* perm, uint64_t n, bool aligned, int load, uint8_t* nodes,
                                hipStream_t s, bool deep = true, Gate gate = Gate{});
-// Ragged batch through the work-queue leaf kernel (perm = length-sorted order,
-// longest first); q must hold queue_words(n) u32; split = longest chain (full
-// blocks) of a group the non-priority waves take when the longest chain bounds
-// the batch.  ring: 0 = register prefetch, 2 = LDS chunk ring, 3 / 4 = pipelined
-// ring of 3 / 4 slots, 12 / 13 / 14 = pipelined ring of value-relative chunks
-// with 2 / 3 / 4 slots.
+// The work queue's state (queue_words(n) u32 at q), set up by the length sort
+// that precedes the queue kernel (sort_by_length_desc with a QueueInit): split
+// = longest chain (compressions - 1) of a group the non-priority waves take
+// when the longest chain bounds the batch.
 uint64_t queue_words(uint64_t n);
+struct QueueInit {
+    uint32_t* q = nullptr;  // nullptr: no queue follows the sort
+    uint64_t nq = 0;
+    uint32_t split = 0;
+};
+// Ragged batch through the work-queue leaf kernel (perm = length-sorted order,
+// longest first; q set up by the sort).  ring: 0 = register prefetch, 2 = LDS
+// chunk ring, 3 / 4 = pipelined ring of 3 / 4 slots, 12 / 13 / 14 = pipelined
+// ring of value-relative chunks with 2 / 3 / 4 slots.
 hipError_t launch_leaf_queue(const uint8_t* base, const uint64_t* off, const uint64_t* len,
                              const uint32_t* perm, uint64_t n, bool aligned, int ring, uint32_t* q,
-                             uint32_t simds, uint32_t waves_per_simd, uint32_t split, uint8_t* nodes,
-                             SyncSlot* sync, hipStream_t s, Gate gate = Gate{});
+                             uint32_t simds, uint32_t waves_per_simd, uint8_t* nodes, hipStream_t s,
+                             Gate gate = Gate{});
 hipError_t launch_reduce(uint8_t* nodes, uint64_t n, int from_level, int top, hipStream_t s, Gate gate = Gate{});
 hipError_t launch_bfs_image(const uint8_t* nodes, const BfsLayout& lay, uint8_t* img,
                             hipStream_t s);
@@ -106,9 +112,12 @@ hipError_t launch_locate(const uint8_t* stream, uint64_t stream_len, const uint6
 // the rest deferred to the length-sorted pass), or never (2); voff / vlen
 // receive the deferred values' places (kDone for hashed ones); err / range /
 // part as launch_locate, range opening the wide Gate iff something was deferred.
+// flags (policy != 0, nullable): this call's pass flags (kPassFlagWords u32)
+// instead of err / range / part, and flags_next the set the kernel resets.
 hipError_t launch_leaf_records(const uint8_t* stream, uint64_t stream_len, const uint64_t* rec_off, uint64_t n,
                                int policy, uint64_t* voff, uint64_t* vlen, uint8_t* nodes, unsigned int* err,
-                               unsigned int* range, uint32_t* part, hipStream_t s);
+                               unsigned int* range, uint32_t* part, hipStream_t s, uint32_t* flags = nullptr,
+                               uint32_t* flags_next = nullptr);
 hipError_t scan_exclusive_u64(const uint64_t* in, uint64_t* out, uint64_t n, void* tmp,
                               size_t* tmp_bytes, hipStream_t s);
 // In-place exclusive scan of n u32 (gated); sums: scan_sums_words(n) u32.
@@ -119,8 +128,9 @@ hipError_t scan_exclusive_u32(uint32_t* a, uint64_t n, uint32_t* sums, hipStream
 // when the scratch is first used (the sort leaves them zero again).
 uint64_t sort_hist_words(uint64_t n);
 uint64_t sort_head_words();
+// cw: words block 0 of the first launch copies before it reads the gate.
 hipError_t sort_by_length_desc(const uint64_t* len, uint64_t n, uint32_t* perm, uint32_t* hist, hipStream_t s,
-                               Gate gate = Gate{});
+                               Gate gate = Gate{}, QueueInit qi = QueueInit{}, CopyWords cw = CopyWords{});
 // crc.hip: CRC-32/IEEE of byte spans / of records' Key ++ Value (stats: 3 x u64,
 // initialised by the launcher).
 // variant: NKV_OPT_CRC_LOAD (bit 0 LDS chunk ring; bits 1-2 table copies x
@@ -139,9 +149,12 @@ hipError_t launch_record_crc(const uint8_t* stream, uint64_t stream_len, const u
 // leave voff / vlen for the sorted pass, hashed ones kDone, and range opens
 // its wide Gate only if a wave was deferred), or for none (2).  part: scratch
 // of locate_part_words(n) u32; voff / vlen / range / part unused for policy 0.
+// flags (policy != 0): the pass flags replace range / part, and the stats go to
+// flags + 4 (copied out by the sort's first launch); flags_next as above.
 hipError_t launch_leaf_verify(const uint8_t* stream, uint64_t stream_len, const uint64_t* rec_off, uint64_t n,
                               int policy, uint64_t* voff, uint64_t* vlen, uint8_t* nodes, uint32_t* crc_out,
-                              unsigned long long* stats, unsigned int* range, uint32_t* part, hipStream_t s);
+                              unsigned long long* stats, unsigned int* range, uint32_t* part, hipStream_t s,
+                              uint32_t* flags = nullptr, uint32_t* flags_next = nullptr);
 // bloom.hip: mode 0 = keys at base + off[i], len[i]; 1 = keys of the records at
 // base + off[i].  query: out[i] = all k bits set; else OR the bits in.
 hipError_t launch_bloom(int mode, bool query, const uint8_t* base, const uint64_t* off, const uint64_t* len,

@@ -65,14 +65,9 @@ __device__ __forceinline__ void ld_header_sizes(const uint8_t* p, uint64_t& ks, 
 }
 
 // ---------------------------------------------------------------------------
-// Block and grid folds (SyncSlot, internal.hpp).  block_fold leaves the
-// workgroup's min / max / or / sum in thread 0.  grid_fold then folds them
-// into the slot with device-scope atomics (performed at the coherence point
-// shared by all XCDs), waits for them to return, and draws a ticket with
-// atomicInc, which wraps to 0 at gridDim.x - 1; the block holding the last
-// ticket has every partial in the slot and takes the totals with atomicExch,
-// restoring the identities.  Only atomics cross workgroups, so no fence or
-// fill launch is needed; returns true in every thread of that last block.
+// Block fold: leaves the workgroup's min / max / or / sum in thread 0.  Grid
+// results go through per-workgroup partials and a fold launch (k_locate_fold)
+// or, in the records entries, the pass flags below.
 __device__ __forceinline__ void block_fold(uint32_t& lo, uint32_t& hi, uint32_t& flag, unsigned long long& sum) {
     __shared__ uint32_t s_lo[kBlock / 64], s_hi[kBlock / 64], s_fl[kBlock / 64];
     __shared__ unsigned long long s_sum[kBlock / 64];
@@ -100,28 +95,14 @@ __device__ __forceinline__ void block_fold(uint32_t& lo, uint32_t& hi, uint32_t&
         }
 }
 
-__device__ __forceinline__ bool grid_fold(SyncSlot* slot, uint32_t lo, uint32_t hi, uint32_t flag,
-                                          unsigned long long sum, uint32_t tot[3], unsigned long long* tot_sum) {
-    __shared__ uint32_t last;
-    if (threadIdx.x == 0) {
-        uint32_t r = 0;
-        if (lo != 0xFFFFFFFFu) r |= atomicMin(&slot->lo, lo);
-        if (hi != 0u) r |= atomicMax(&slot->hi, hi);
-        if (flag) r |= atomicOr(&slot->flag, flag);
-        if (sum) r |= uint32_t(atomicAdd(&slot->sum, sum));
-        // the folds have returned, so they are performed before the ticket
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const uint32_t t = atomicInc(&slot->ticket, gridDim.x - 1) + (r & 0u);
-        last = t == gridDim.x - 1 ? 1u : 0u;
-        if (last) {
-            tot[0] = atomicExch(&slot->lo, 0xFFFFFFFFu);
-            tot[1] = atomicExch(&slot->hi, 0u);
-            tot[2] = atomicExch(&slot->flag, 0u);
-            *tot_sum = atomicExch(&slot->sum, 0ull);
-        }
-    }
-    __syncthreads();
-    return last != 0u;
+// Pass flags (internal.hpp kPassFlagWords): block 0 resets the set the next
+// call uses; a workgroup raises this call's deferred / bad-header words with
+// one atomic each, skipped once another workgroup has raised them.
+__device__ __forceinline__ void pass_flags_reset(uint32_t* f) {
+    if (blockIdx.x == 0 && threadIdx.x < kPassFlagWords) f[threadIdx.x] = (threadIdx.x & ~1u) == 6u ? ~0u : 0u;
+}
+__device__ __forceinline__ void pass_flag_raise(uint32_t* f, uint32_t v) {
+    if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != v) atomicOr(f, v);
 }
 
 // SHA-1 compressions of a len-byte message (FIPS 180-4 padding: + 0x80 + 8 B)
@@ -1363,7 +1344,9 @@ struct CrcBE {
 __global__ __launch_bounds__(kBlock, NKV_VERIFY_WAVES) void k_leaf_verify(
     const uint8_t* __restrict__ stream, uint64_t stream_len, const uint64_t* __restrict__ rec_off, uint64_t n,
     int policy, uint64_t* __restrict__ voff, uint64_t* __restrict__ vlen, uint8_t* __restrict__ nodes,
-    uint32_t* __restrict__ crc_out, unsigned long long* __restrict__ stats, uint32_t* __restrict__ part) {
+    uint32_t* __restrict__ crc_out, unsigned long long* __restrict__ stats, uint32_t* __restrict__ part,
+    uint32_t* __restrict__ flags, uint32_t* __restrict__ flags_next) {
+    if (flags) pass_flags_reset(flags_next);
     // ONE LDS object (a second one can cost the DMA loop its waits): four
     // 4 KiB wave stages, the 4 KiB of byte-swapped word tables (CrcBE), then
     // T[0] for the bytewise steps: 21 KiB, seven workgroups per CU
@@ -1477,19 +1460,23 @@ __global__ __launch_bounds__(kBlock, NKV_VERIFY_WAVES) void k_leaf_verify(
             atomicMin(stats + 1, (unsigned long long)t);
         }
     }
-    if (part) {  // one partial per workgroup, through the (now idle) stage LDS
+    if (part || flags) {  // one partial per workgroup, through the (now idle) stage LDS
         const bool wdefer = any && !hash;
-        uint32_t* flags = reinterpret_cast<uint32_t*>(smem);
+        uint32_t* wf = reinterpret_cast<uint32_t*>(smem);
         __syncthreads();
-        if (lane == 0) flags[threadIdx.x >> 6] = wdefer ? 1u : 0u;
+        if (lane == 0) wf[threadIdx.x >> 6] = wdefer ? 1u : 0u;
         __syncthreads();
         if (threadIdx.x == 0) {
             uint32_t f = 0u;
 #pragma unroll
-            for (int k = 0; k < kBlock / 64; ++k) f |= flags[k];
-            part[3 * blockIdx.x] = 0u;
-            part[3 * blockIdx.x + 1] = f ? 0xFFFFFFFFu : 0u;
-            part[3 * blockIdx.x + 2] = 0u;
+            for (int k = 0; k < kBlock / 64; ++k) f |= wf[k];
+            if (flags) {
+                if (f) pass_flag_raise(flags + 1, 0xFFFFFFFFu);
+            } else {
+                part[3 * blockIdx.x] = 0u;
+                part[3 * blockIdx.x + 1] = f ? 0xFFFFFFFFu : 0u;
+                part[3 * blockIdx.x + 2] = 0u;
+            }
         }
     }
 }
@@ -1506,7 +1493,7 @@ __global__ __launch_bounds__(kBlock, NKV_VERIFY_WAVES) void k_leaf_verify(
 // group.  Every wave exits once its end meets the other one.
 //
 // The other waves only take groups whose longest chain is at most split
-// blocks (group index >= q[2], found by k_queue_split): long groups all go
+// blocks (group index >= q[2], set by the sort's queue_header): long groups all go
 // longest-first to the one raised-priority wave per SIMD, so the batch ends on
 // short groups instead of on a medium one pulled late from the short end.
 //
@@ -1543,7 +1530,7 @@ __global__ __launch_bounds__(64, queue_ring_slots<LOAD>() == 4 ? 2 : (queue_ring
     slot = __builtin_amdgcn_readfirstlane(slot);
     const bool front = slot == 0;
     if (front) __builtin_amdgcn_s_setprio(3);
-    // k_queue_split's partials: the first group short enough for the
+    // queue_header's results: the first group short enough for the
     // non-priority waves, and the batch's work; a throughput-bound batch (work
     // at least twice what the longest chain keeps every SIMD busy for) lets
     // every wave take any group
@@ -1753,6 +1740,44 @@ __device__ __forceinline__ uint32_t len_bucket_desc(uint64_t len) {
     return kLenBuckets - 1u - k;
 }
 
+// Smallest compression count of a bucket (exact below 256 compressions).
+__device__ __forceinline__ uint64_t bucket_compressions(uint32_t bucket) {
+    const uint32_t k = kLenBuckets - 1u - bucket;
+    if (k < 256u) return k;
+    const uint32_t e = 8u + (k - 256u) / 16u;
+    return uint64_t(16u + (k - 256u) % 16u) << (e - 4u);
+}
+
+// The work queue's header from the sorted order's bucket starts (start[b] =
+// first sorted position of bucket b, total = values sorted), by one workgroup,
+// so no separate launch sets the queue up: tickets 0; q[2] = the first group
+// (64 sorted values, longest first) whose first value is short, i.e. has at
+// most split + 1 compressions (0xFFFFFFFF if none); q[4..5] = the batch's work,
+// the sum over groups of their first value's compressions (each bucket's
+// smallest count: exact below 256 compressions, within 1/16 above -- it only
+// feeds k_leaf_queue's throughput-bound test).
+__device__ void queue_header(const uint32_t* start, uint32_t total, const QueueInit& qi) {
+    uint32_t first = 0xFFFFFFFFu, none_hi = 0u, none_fl = 0u;
+    unsigned long long work = 0;
+    for (uint32_t b = threadIdx.x; b < kLenBuckets; b += kBlock) {
+        const uint64_t s0 = start[b], s1 = b + 1u < kLenBuckets ? start[b + 1] : total;
+        const uint64_t comp = bucket_compressions(b);
+        work += (((s1 + 63) >> 6) - ((s0 + 63) >> 6)) * comp;  // groups whose first value is in the bucket
+        if (s1 > s0 && comp <= uint64_t(qi.split) + 1u) first = min(first, uint32_t(s0));
+    }
+    block_fold(first, none_hi, none_fl, work);
+    if (threadIdx.x == 0) {
+        uint32_t* q = qi.q;
+        q[0] = 0u;
+        q[1] = 0u;
+        q[2] = first == 0xFFFFFFFFu ? first : uint32_t((uint64_t(first) + 63) >> 6);
+        q[3] = 0u;
+        reinterpret_cast<unsigned long long*>(q)[2] = work;
+        q[6] = 0u;
+        q[7] = 0u;
+    }
+}
+
 // Two-launch form: k_len_hist_alloc reserves each (bucket, tile) run inside
 // its bucket with one device atomic per nonzero bucket (bucket totals at the
 // head of the scratch), and k_len_scatter_alloc scans the 640 totals itself,
@@ -1763,10 +1788,15 @@ __device__ __forceinline__ uint32_t len_bucket_desc(uint64_t len) {
 constexpr uint32_t kSortHead = 1024;  // [0, 640) bucket totals, [640] ticket
 __global__ __launch_bounds__(kBlock) void k_len_hist_alloc(const uint64_t* __restrict__ len, uint64_t n,
                                                             uint32_t* __restrict__ scratch, uint32_t tiles,
-                                                            Gate gate) {
+                                                            Gate gate, QueueInit qi, CopyWords cw) {
     __shared__ uint32_t h[kLenBuckets];
+    if (blockIdx.x == 0 && threadIdx.x < cw.n) cw.dst[threadIdx.x] = cw.src[threadIdx.x];
     if (!gate.open()) return;
     for (uint32_t i = threadIdx.x; i < kLenBuckets; i += kBlock) h[i] = 0u;
+    if (qi.q)  // the work queue's per-SIMD arrivals and claim flags (its header: k_len_scatter_alloc)
+        for (uint64_t i = kQueueHeader + uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < qi.nq;
+             i += uint64_t(tiles) * kBlock)
+            qi.q[i] = 0u;
     __syncthreads();
     const uint64_t base = uint64_t(blockIdx.x) * kSortTile;
     uint32_t bk[kSortItems];
@@ -1788,9 +1818,10 @@ __global__ __launch_bounds__(kBlock) void k_len_hist_alloc(const uint64_t* __res
 
 __global__ __launch_bounds__(kBlock) void k_len_scatter_alloc(const uint64_t* __restrict__ len, uint64_t n,
                                                                uint32_t* __restrict__ scratch, uint32_t tiles,
-                                                               uint32_t* __restrict__ perm, Gate gate) {
+                                                               uint32_t* __restrict__ perm, Gate gate,
+                                                               QueueInit qi) {
     __shared__ uint32_t cur[kLenBuckets];
-    __shared__ uint32_t last;
+    __shared__ uint32_t last, total;
     if (!gate.open()) return;
     if (threadIdx.x < 64) {  // exclusive scan of the bucket totals, 64 at a time
         const int lane = threadIdx.x;
@@ -1806,8 +1837,10 @@ __global__ __launch_bounds__(kBlock) void k_len_scatter_alloc(const uint64_t* __
             cur[c0 + lane] = carry + x - v;
             carry += uint32_t(__shfl(int(x), 63));
         }
+        if (lane == 0) total = carry;
     }
     __syncthreads();
+    if (qi.q && blockIdx.x == 0) queue_header(cur, total, qi);
     const uint32_t* hist = scratch + kSortHead;
     for (uint32_t i = threadIdx.x; i < kLenBuckets; i += kBlock) cur[i] += hist[uint64_t(i) * tiles + blockIdx.x];
     __syncthreads();  // every read of the totals is done
@@ -1975,8 +2008,9 @@ __global__ __launch_bounds__(kBlock) void k_locate_fold(const uint32_t* __restri
 __global__ __launch_bounds__(kBlock, kLeafWavesPerSimd) void k_leaf_records(
     const uint8_t* __restrict__ stream, uint64_t stream_len, const uint64_t* __restrict__ rec_off, uint64_t n,
     int policy, uint64_t* __restrict__ voff, uint64_t* __restrict__ vlen, uint8_t* __restrict__ nodes,
-    uint32_t* __restrict__ part) {
+    uint32_t* __restrict__ part, uint32_t* __restrict__ flags, uint32_t* __restrict__ flags_next) {
     __shared__ __attribute__((aligned(16))) uint8_t smem[kBlock * 80];
+    if (flags) pass_flags_reset(flags_next);
     const uint64_t t = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
     const bool live = t < n;
     uint64_t o = 0, l = 0;
@@ -2031,17 +2065,22 @@ __global__ __launch_bounds__(kBlock, kLeafWavesPerSimd) void k_leaf_records(
     // one partial per workgroup, folded through the (now idle) stage LDS: a
     // block_fold of its own would cost LDS, i.e. a workgroup per CU
     const int wv = threadIdx.x >> 6;
-    uint32_t* flags = reinterpret_cast<uint32_t*>(smem);
+    uint32_t* wf = reinterpret_cast<uint32_t*>(smem);
     __syncthreads();  // every wave is done with its stage
-    if ((threadIdx.x & 63) == 0) flags[wv] = (wdefer ? 2u : 0u) | (wbad ? 1u : 0u);
+    if ((threadIdx.x & 63) == 0) wf[wv] = (wdefer ? 2u : 0u) | (wbad ? 1u : 0u);
     __syncthreads();
     if (threadIdx.x == 0) {
         uint32_t f = 0u;
 #pragma unroll
-        for (int k = 0; k < kBlock / 64; ++k) f |= flags[k];
-        part[3 * blockIdx.x] = 0u;
-        part[3 * blockIdx.x + 1] = (f & 2u) ? 0xFFFFFFFFu : 0u;
-        part[3 * blockIdx.x + 2] = f & 1u;
+        for (int k = 0; k < kBlock / 64; ++k) f |= wf[k];
+        if (flags) {  // the pass flags (no fold launch)
+            if (f & 2u) pass_flag_raise(flags + 1, 0xFFFFFFFFu);
+            if (f & 1u) pass_flag_raise(flags + 2, 1u);
+        } else {
+            part[3 * blockIdx.x] = 0u;
+            part[3 * blockIdx.x + 1] = (f & 2u) ? 0xFFFFFFFFu : 0u;
+            part[3 * blockIdx.x + 2] = f & 1u;
+        }
     }
 }
 
@@ -2165,58 +2204,23 @@ hipError_t launch_leaf_offsets(const uint8_t* base, const uint64_t* off, const u
 
 hipError_t launch_leaf_verify(const uint8_t* stream, uint64_t stream_len, const uint64_t* rec_off, uint64_t n,
                               int policy, uint64_t* voff, uint64_t* vlen, uint8_t* nodes, uint32_t* crc_out,
-                              unsigned long long* stats, unsigned int* range, uint32_t* part, hipStream_t s) {
+                              unsigned long long* stats, unsigned int* range, uint32_t* part, hipStream_t s,
+                              uint32_t* flags, uint32_t* flags_next) {
     const unsigned nb = grid_for(n);
+    if (policy == 0) flags = nullptr;
     hipLaunchKernelGGL(k_leaf_verify, dim3(nb), dim3(kBlock), 0, s, stream, stream_len, rec_off, n, policy, voff,
-                       vlen, nodes, crc_out, stats, policy == 0 ? nullptr : part);
-    if (policy != 0) hipLaunchKernelGGL(k_locate_fold, dim3(1), dim3(kBlock), 0, s, part, nb, nullptr, range);
+                       vlen, nodes, crc_out, flags ? reinterpret_cast<unsigned long long*>(flags + 4) : stats,
+                       (policy == 0 || flags) ? nullptr : part, flags, flags_next);
+    if (policy != 0 && !flags)
+        hipLaunchKernelGGL(k_locate_fold, dim3(1), dim3(kBlock), 0, s, part, nb, nullptr, range);
     return hipGetLastError();
-}
-
-// The queue's state for k_leaf_queue, over all groups in parallel: every block
-// zeroes its share of the per-SIMD arrivals and claim flags; the header is
-// written by the grid's last block (grid_fold): tickets 0, q[2] = first group
-// (length-sorted, longest first) whose first value has at most split full
-// blocks (0xFFFFFFFF if none), q[4..5] = the batch's work, the sum over groups
-// of their first value's compressions.  k_leaf_queue decides from them.
-__global__ __launch_bounds__(kBlock) void k_queue_split(const uint64_t* __restrict__ len,
-                                                     const uint32_t* __restrict__ perm, uint32_t ngroups,
-                                                     uint32_t split, uint32_t* __restrict__ q, uint64_t nq,
-                                                     SyncSlot* __restrict__ sync, Gate gate) {
-    if (!gate.open()) return;
-    const uint64_t stride = uint64_t(gridDim.x) * kBlock;
-    for (uint64_t i = kQueueHeader + uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < nq; i += stride) q[i] = 0u;
-    unsigned long long w = 0;
-    uint32_t b = 0xFFFFFFFFu, hi = 0u, none = 0u;
-    for (uint32_t g = blockIdx.x * kBlock + threadIdx.x; g < ngroups; g += gridDim.x * kBlock) {
-        const uint64_t l = len[perm[uint64_t(g) * 64]];
-        w += compressions(l);
-        if ((l >> 6) <= split && g < b) b = g;
-    }
-    block_fold(b, hi, none, w);
-    uint32_t tot[3];
-    unsigned long long work;
-    if (grid_fold(sync, b, 0u, 0u, w, tot, &work) && threadIdx.x == 0) {
-        q[0] = 0u;
-        q[1] = 0u;
-        q[2] = tot[0];
-        q[3] = 0u;
-        reinterpret_cast<unsigned long long*>(q)[2] = work;
-        q[6] = 0u;
-        q[7] = 0u;
-    }
 }
 
 hipError_t launch_leaf_queue(const uint8_t* base, const uint64_t* off, const uint64_t* len,
                              const uint32_t* perm, uint64_t n, bool aligned, int ring, uint32_t* q,
-                             uint32_t simds, uint32_t waves_per_simd, uint32_t split, uint8_t* nodes,
-                             SyncSlot* sync, hipStream_t s, Gate gate) {
+                             uint32_t simds, uint32_t waves_per_simd, uint8_t* nodes, hipStream_t s, Gate gate) {
     const uint32_t ngroups = uint32_t((n + 63) / 64);
     const uint32_t waves = simds * waves_per_simd;
-    const uint64_t nq = queue_words(n);
-    const uint32_t sblocks = uint32_t(std::min<uint64_t>((nq + kBlock - 1) / kBlock, 256u));
-    hipLaunchKernelGGL(k_queue_split, dim3(sblocks), dim3(kBlock), 0, s, len, perm, ngroups, split, q, nq, sync,
-                       gate);
     if (ring == 14)
         hipLaunchKernelGGL(k_leaf_queue<13>, dim3(waves), dim3(64), 0, s, base, off, len, perm, n, ngroups, simds, q, nodes, gate);
     else if (ring == 13)
@@ -2310,11 +2314,13 @@ hipError_t launch_locate(const uint8_t* stream, uint64_t stream_len, const uint6
 
 hipError_t launch_leaf_records(const uint8_t* stream, uint64_t stream_len, const uint64_t* rec_off, uint64_t n,
                                int policy, uint64_t* voff, uint64_t* vlen, uint8_t* nodes, unsigned int* err,
-                               unsigned int* range, uint32_t* part, hipStream_t s) {
+                               unsigned int* range, uint32_t* part, hipStream_t s, uint32_t* flags,
+                               uint32_t* flags_next) {
     const unsigned nb = grid_for(n);
+    if (policy == 0) flags = nullptr;
     hipLaunchKernelGGL(k_leaf_records, dim3(nb), dim3(kBlock), 0, s, stream, stream_len, rec_off, n, policy, voff,
-                       vlen, nodes, part);
-    hipLaunchKernelGGL(k_locate_fold, dim3(1), dim3(kBlock), 0, s, part, nb, err, range);
+                       vlen, nodes, part, flags, flags_next);
+    if (!flags) hipLaunchKernelGGL(k_locate_fold, dim3(1), dim3(kBlock), 0, s, part, nb, err, range);
     return hipGetLastError();
 }
 
@@ -2423,13 +2429,13 @@ uint64_t sort_head_words() { return kSortHead; }
 // scratch: sort_hist_words(n) u32 whose first sort_head_words() are zero
 // (the two-launch form keeps them zero between calls)
 hipError_t sort_by_length_desc(const uint64_t* len, uint64_t n, uint32_t* perm, uint32_t* scratch, hipStream_t s,
-                               Gate gate) {
+                               Gate gate, QueueInit qi, CopyWords cw) {
     const uint64_t tiles = (n + kSortTile - 1) / kSortTile;
     if (tiles == 0) return hipSuccess;
     hipLaunchKernelGGL(k_len_hist_alloc, dim3(uint32_t(tiles)), dim3(kBlock), 0, s, len, n, scratch,
-                       uint32_t(tiles), gate);
+                       uint32_t(tiles), gate, qi, cw);
     hipLaunchKernelGGL(k_len_scatter_alloc, dim3(uint32_t(tiles)), dim3(kBlock), 0, s, len, n, scratch,
-                       uint32_t(tiles), perm, gate);
+                       uint32_t(tiles), perm, gate, qi);
     return hipGetLastError();
 }
 
