@@ -169,3 +169,58 @@ def test_verify_matches_separate_calls(nkv, oracle):
     assert np.array_equal(nodes, d_nodes.cpu().numpy().reshape(-1, 20))
     assert np.array_equal(crc, d_crc.cpu().numpy().view(np.uint32))
     assert stats == d_stats.cpu().numpy().view(np.uint64).tolist() == [1, 777, 0]
+
+
+def test_pass_flag_sets_alternate(nkv, oracle):
+    """The records entries keep their deferred-pass flags in two per-context
+    sets used by alternate calls, each call resetting the other set: a sequence
+    of verify and plain records calls on one context, good / corrupted / bad
+    header / ragged (deferred) / small (all sorted) tables in an order that puts
+    every case on both sets, each checked against the oracle."""
+    import hashlib
+    torch = _torch()
+    _lib, ctx = nkv
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    L = _lib.lib()
+    cases = {}
+    buf, off = _sstable(5000, ks=16, vs=1000, oracle=oracle)
+    cases["good"] = (buf, off, _want(oracle, buf, off), 0)
+    bad = buf.copy()
+    for i in (3, 700, 4999):
+        bad[int(off[i]) + 30 + 16 + 5] ^= 0x40  # value byte: stored Crc mismatch
+    cases["crc"] = (bad, off, _want(oracle, bad, off), 0)
+    hdr = buf.copy()
+    j = 1234
+    hdr[int(off[j]) + 22:int(off[j]) + 30] = np.frombuffer(np.uint64(1 << 40).tobytes(), np.uint8)
+    leaves = oracle.leaf_hashes(buf, off + 46, np.full(off.size, 1000, np.uint64), threads=8)
+    leaves[j] = np.frombuffer(hashlib.sha1(b"").digest(), np.uint8)
+    cases["header"] = (hdr, off, None, 1, oracle.tree_from_digests(leaves))
+    rng = np.random.default_rng(77)
+    rbuf, roff = _stream(rng, 5000, vmax=9000)
+    rbuf[int(roff[10])] ^= 0x01
+    cases["ragged"] = (rbuf, roff, _want(oracle, rbuf, roff), 0)
+    sbuf, soff = _stream(rng, 3000, vmax=5000)
+    cases["small"] = (sbuf, soff, _want(oracle, sbuf, soff), 0)
+    order = ["good", "header", "good", "ragged", "crc", "good", "small", "header", "ragged", "good", "good",
+             "crc", "header", "small", "good"]
+    for step, name in enumerate(order):
+        case = cases[name]
+        buf_, off_, want, herr = case[:4]
+        n = off_.size
+        if step % 3 == 2:  # a plain records call between the verify calls
+            d_buf, d_off = _dev(torch, buf_), _dev(torch, off_)
+            d_nodes = torch.zeros(L.nkv_total_nodes(n) * 20, dtype=torch.uint8, device="cuda")
+            d_err = torch.full((1,), 7, dtype=torch.int32, device="cuda")
+            _lib.check(L.nkv_tree_from_records_dev(ctx.h, d_buf.data_ptr(), buf_.size, d_off.data_ptr(), n,
+                                                   d_nodes.data_ptr(), d_err.data_ptr()))
+            torch.cuda.synchronize()
+            assert int(d_err.item()) == herr, (step, name)
+            w_nodes = case[4] if want is None else want[0]
+            assert np.array_equal(d_nodes.cpu().numpy().reshape(-1, 20), w_nodes), (step, name)
+            continue
+        got = _run(torch, L, _lib, ctx, buf_, off_, want_crc=want is not None)
+        if want is None:
+            assert np.array_equal(got[0], case[4]), (step, name)
+            assert got[2] == [0, 2**64 - 1, 1], (step, name)
+        else:
+            _check(got, want, n)
