@@ -91,6 +91,9 @@ def parse():
     ap.add_argument("--verify", action="store_true", help="check the root against the C oracle")
     ap.add_argument("--dist", action="store_true",
                     help="join the RCCL group and all-gather the roots even at world size 1 (exercises the N > 1 path on one GPU)")
+    ap.add_argument("--gather", choices=["batch", "step"], default="batch",
+                    help="root all-gather with N > 1 (or --dist): one collective per timed loop (batch) or one "
+                         "per table, pipelined behind the next table (step)")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="do not record per-kernel HIP events inside the timed loop")
     return ap.parse_args()
@@ -193,6 +196,43 @@ class RootGather:
 
     def last_roots(self):
         return self.outs[self.i % 2]
+
+
+class BatchedRootGather:
+    """The roots of a whole run of tables in one collective: each step copies
+    its 20-byte root (on the compute stream, behind the tree) into the next
+    slot, and drain() all-gathers the filled slots at once (world x k x 20 B),
+    so a timed loop of K tables issues one RCCL call instead of K (SURVEY.md
+    section 8e: the gather follows the builds; fewer, larger collectives).
+    Every gather still completes inside the timed region (drain before the
+    closing barrier).  dist None: one rank, nothing to gather."""
+
+    def __init__(self, nodes, world, dist=None, cap=256):
+        self.dist, self.nodes, self.world, self.cap = dist, nodes, world, max(1, cap)
+        self.slots = nodes.new_empty(self.cap * 20)
+        self.out = nodes.new_empty(world * self.cap * 20)
+        self.k = 0
+        self.last = None
+
+    def begin(self):
+        return self.nodes
+
+    def end(self, nodes):
+        if self.dist:
+            if self.k == self.cap:
+                self.drain()
+            self.slots[20 * self.k:20 * (self.k + 1)].copy_(nodes[-20:])
+            self.k += 1
+
+    def drain(self):
+        if self.dist and self.k:
+            out = self.out[:self.world * self.k * 20]
+            self.dist.all_gather_into_tensor(out, self.slots[:self.k * 20])
+            self.last = out.view(self.world, self.k, 20)[:, self.k - 1].reshape(-1)
+            self.k = 0
+
+    def last_roots(self):
+        return self.last
 
 
 def main():
@@ -311,14 +351,19 @@ def main():
             _lib.check(L.nkv_tree_from_values_dev(ctx.h, data.data_ptr(), d_off.data_ptr(), d_len.data_ptr(),
                                                   n, nodes.data_ptr()))
 
-    # C1, the root gather, overlapped with the next
-    # table: step i builds into bufs[i % 2] and all-gathers that buffer's root
-    # asynchronously on RCCL's stream while step i + 1 hashes into the other
-    # buffer; step i + 2 first waits for gather i (long done: a 20-byte
-    # all-gather against a 1.2 ms table) before it rewrites bufs[i % 2].
-    # Every gather still completes inside the timed region (the final
-    # synchronize waits for it).
-    rg = RootGather(nodes, roots, dist if (use_dist and not one_tree) else None)
+    # C1, the root gather.  Default (--gather batch):
+    # every table's root is kept and all of them are all-gathered in one call
+    # at the end of the loop (BatchedRootGather).  --gather step: one gather
+    # per table, overlapped with the next: step i builds into bufs[i % 2] and
+    # all-gathers that buffer's root asynchronously on RCCL's stream while
+    # step i + 1 hashes into the other buffer; step i + 2 first waits for
+    # gather i before it rewrites bufs[i % 2].  Either way every gather
+    # completes inside the timed region (the final synchronize waits for it).
+    gdist = dist if (use_dist and not one_tree) else None
+    if args.gather == "step":
+        rg = RootGather(nodes, roots, gdist)
+    else:
+        rg = BatchedRootGather(nodes, world, gdist, cap=max(args.steps, args.warmup, 8))
 
     def step():
         nonlocal nodes
@@ -471,7 +516,9 @@ def main():
                 "value_bytes": vlen if not mixed else "64..65536 (mean %.0f)" % (nbytes / n),
                 "parallelism": (f"1 tree split over {world} ranks" + (" + RCCL all_gather of sub-roots" if world > 1 else ""))
                                if one_tree else
-                               f"{world} independent tables" + (" + RCCL all_gather of roots" if world > 1 else ""),
+                               f"{world} independent tables" + ((" + RCCL all_gather of roots, "
+                                                                 + ("one call per timed loop" if args.gather == "batch"
+                                                                    else "one per table")) if world > 1 else ""),
             },
             "roofline": {
                 "bound": "hbm",

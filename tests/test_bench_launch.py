@@ -123,3 +123,47 @@ def test_rccl_root_gather_on_gpu():
     assert line["n_gpus"] == 1 and line["steps"] == 4
     assert line["root_gather_ok"] is True
     assert line["verified_vs_oracle"] is True
+
+
+def _batched_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    nodes = torch.zeros(100, dtype=torch.uint8)
+    rg = bench.BatchedRootGather(nodes, world, dist, cap=3)
+    seen = []
+    for i in range(7):  # cap 3: drains itself before the 4th and 7th slot
+        buf = rg.begin()
+        buf[-20:] = (rank * 16 + i) % 256
+        rg.end(buf)
+        if i in (2, 5):
+            seen.append(None if rg.last is None else rg.last_roots().tolist())
+    rg.drain()
+    seen.append(rg.last_roots().tolist())
+    q.put((rank, seen, rg.k))
+    dist.destroy_process_group()
+
+
+def test_batched_root_gather_world2():
+    """BatchedRootGather over gloo, world size 2: the roots of every step are
+    kept and gathered in one call (or one per cap slots); last_roots() is every
+    rank's root of the last step gathered."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_batched_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {r: (seen, k) for r, seen, k in (q.get(timeout=120) for _ in procs)}
+    for p in procs:
+        p.join(timeout=60)
+    for r in (0, 1):
+        seen, k = res[r]
+        assert k == 0
+        # after step 2 nothing was gathered yet; step 5's check sees the drain
+        # before slot 4 (steps 0-2); the final drain has step 6
+        assert seen[0] is None
+        assert seen[1] == [2] * 20 + [18] * 20
+        assert seen[2] == [6] * 20 + [22] * 20
