@@ -198,6 +198,26 @@ class RootGather:
         return self.outs[self.i % 2]
 
 
+def preroll(step, drain, sync, seconds, dist=None, flag=None) -> int:
+    """Untimed steps, in chunks of 8, until every rank has run them for
+    `seconds`; returns the count, which is the same on every rank (the ranks
+    agree after each chunk through a MIN all-reduce of flag(done))."""
+    steps, t0 = 0, time.perf_counter()
+    while True:
+        for _ in range(8):
+            step()
+        steps += 8
+        drain()
+        sync()
+        done = time.perf_counter() - t0 >= seconds
+        if dist is not None:
+            f = flag(1 if done else 0)
+            dist.all_reduce(f, op=dist.ReduceOp.MIN)
+            done = int(f.item()) == 1
+        if done:
+            return steps
+
+
 class BatchedRootGather:
     """The roots of a whole run of tables in one collective: each step copies
     its 20-byte root (on the compute stream, behind the tree) into the next
@@ -377,15 +397,13 @@ def main():
     # after ~30 ms of back-to-back launches ("The clock"),
     # so run steps for at least PREROLL_S before the caller's warmup steps.
     torch.cuda.synchronize()
-    preroll_steps, t_pre = 0, time.perf_counter()
-    while time.perf_counter() - t_pre < args.preroll_s or preroll_steps < 1:
-        step()
-        preroll_steps += 1
-        if preroll_steps % 8 == 0:
-            drain()
-            torch.cuda.synchronize()
-    drain()
-    torch.cuda.synchronize()
+    # Steps go in chunks of 8 and, with several ranks, every rank runs the same
+    # number of them (the gathers and the one_tree collectives are matched by
+    # order, so a rank that ran one step more would wait forever): after each
+    # chunk the ranks agree to stop only once every one of them has pre-rolled
+    # for PREROLL_S.
+    preroll_steps = preroll(step, drain, torch.cuda.synchronize, args.preroll_s, dist if use_dist else None,
+                            lambda v: torch.tensor([v], dtype=torch.int32, device="cuda"))
     if records and (int(d_err.item()) != 0 or (verify_crc and int(d_stats[2].item()) != 0)):
         # a malformed synthetic stream would time empty hashes
         raise SystemExit("bench.py: the record stream failed the header checks")

@@ -167,3 +167,39 @@ def test_batched_root_gather_world2():
         assert seen[0] is None
         assert seen[1] == [2] * 20 + [18] * 20
         assert seen[2] == [6] * 20 + [22] * 20
+
+
+def _preroll_worker(rank, world, port, q):
+    import time as _t
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    count = [0]
+
+    def step():  # rank 1 steps three times slower
+        _t.sleep(0.002 * (1 + 2 * rank))
+        count[0] += 1
+
+    t0 = _t.perf_counter()
+    n = bench.preroll(step, lambda: None, lambda: None, 0.1, dist, lambda v: torch.tensor([v], dtype=torch.int32))
+    q.put((rank, n, count[0], _t.perf_counter() - t0))
+    dist.destroy_process_group()
+
+
+def test_preroll_same_step_count_on_every_rank():
+    """The time-based pre-roll must run the same number of steps on every rank
+    (collectives inside a step are matched by order): gloo world 2, one rank
+    three times slower; both stop together, after each ran >= 0.1 s."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_preroll_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {r: (n, c, dt) for r, n, c, dt in (q.get(timeout=120) for _ in procs)}
+    for p in procs:
+        p.join(timeout=60)
+    assert res[0][0] == res[1][0] == res[0][1] == res[1][1]
+    assert res[0][0] % 8 == 0 and min(res[0][2], res[1][2]) >= 0.1
