@@ -489,7 +489,10 @@ def main():
         traffic, traffic_bounds = None, None
         # PMC-measured HBM bytes of this config's leaf kernel (separate rocprofv3
         # passes: tools/pmc_sizes.sh for cfg2, tools/pmc_config.sh for the others)
-        pmc_name = {"sstable4k": "pmc_traffic.json", "records": "pmc_traffic_records.json",
+        # cfg2: the default 128-byte register runs (LOAD 4) or the LDS-DMA stage (--leaf-load 1)
+        cfg2_pmc = {0: "pmc_traffic_cfg2_runs.json", 4: "pmc_traffic_cfg2_runs.json",
+                    1: "pmc_traffic.json"}.get(args.leaf_load)
+        pmc_name = {"sstable4k": cfg2_pmc, "records": "pmc_traffic_records.json",
                     "mixed": "pmc_traffic_mixed.json", "records_verify": "pmc_traffic_records_verify.json"}.get(args.config)
         pmc_path = os.path.join(ROOT, "profiles", pmc_name) if pmc_name else None
         if pmc_path and os.path.exists(pmc_path):
@@ -547,7 +550,9 @@ def main():
                            ("leaf phase: k_locate + k_leaf<offsets, aligned-segment stage> (input order)"
                             if args.records_fused == 0 else
                             "leaf phase: k_leaf_records (header parse + aligned-segment stage, input order)")) if records else
-                          "k_leaf<strided, LDS-DMA> (leaf SHA-1, level 0)",
+                          ("k_leaf<strided, LDS-DMA stage> (leaf SHA-1, level 0)" if args.leaf_load == 1 else
+                           "k_leaf<strided, 128-byte register runs> (leaf SHA-1, level 0)" if args.leaf_load in (0, 4)
+                           else f"k_leaf<strided, load path {args.leaf_load}> (leaf SHA-1, level 0)"),
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

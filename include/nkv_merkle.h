@@ -94,7 +94,8 @@ int nkv_ctx_sync(nkv_ctx *ctx);
 /* Tuning knobs (defaults are the measured-best settings). */
 #define NKV_OPT_LEAF_LOAD 1 /* leaf-kernel load path for 16-byte aligned values:
                                1 = LDS-DMA stage, 2 = direct loads, 3 = direct non-temporal,
-                               4 / 5 = direct loads in 128 / 256-byte runs per lane,
+                               4 (the default) / 5 = direct loads in 128 / 256-byte runs
+                               per lane (1 and 4 take 11 for unaligned values),
                                9 / 10 = line-pair / 80-byte-window LDS-DMA stage for values
                                that are not 64-byte aligned (waves of equal full-block
                                counts; other waves as 1); 11 (the default for values that

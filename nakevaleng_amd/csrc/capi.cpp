@@ -98,7 +98,7 @@ struct nkv_ctx {
     int device = 0;
     hipStream_t own = nullptr;
     hipStream_t stream = nullptr;
-    int leaf_load = 1;  // NKV_OPT_LEAF_LOAD
+    int leaf_load = 4;  // NKV_OPT_LEAF_LOAD
     int bucket = 2;     // NKV_OPT_BUCKET
     int deep = 3;       // NKV_OPT_DEEP_PREFETCH (2, 3 = work-queue kernel)
     uint32_t simds = 1024;  // SIMDs on the device (CUs x 4)

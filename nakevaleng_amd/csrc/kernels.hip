@@ -1157,8 +1157,11 @@ __device__ __forceinline__ void sha1_blocks_any(uint8_t* wbuf, const uint8_t* p,
 // use plus its launch.
 // LOAD: 0 = any alignment (register funnel); 1 = 16-byte aligned, LDS-DMA
 // stage; 2 = aligned, direct loads; 3 = aligned, direct non-temporal loads.
+#ifndef NKV_RUNS_WAVES
+#define NKV_RUNS_WAVES 4  // waves per SIMD of the run-load paths (LOAD 4, 5)
+#endif
 template <int MODE, int LOAD>
-__global__ __launch_bounds__(kBlock, (LOAD == 6 || LOAD == 7) ? 2 : ((LOAD == 4 || LOAD == 5) ? 4 : (LOAD == 9 ? 5 : kLeafWavesPerSimd))) void k_leaf(const uint8_t* __restrict__ base,
+__global__ __launch_bounds__(kBlock, (LOAD == 6 || LOAD == 7) ? 2 : ((LOAD == 4 || LOAD == 5) ? NKV_RUNS_WAVES : (LOAD == 9 ? 5 : kLeafWavesPerSimd))) void k_leaf(const uint8_t* __restrict__ base,
                                                   const uint64_t* __restrict__ off,
                                                   const uint64_t* __restrict__ len, uint64_t stride,
                                                   uint64_t L, const uint32_t* __restrict__ perm,
@@ -2185,10 +2188,12 @@ static void leaf_dispatch(int load, const uint8_t* base, const uint64_t* off, co
 hipError_t launch_leaf_strided(const uint8_t* base, uint64_t stride, uint64_t L, uint64_t n, int load,
                                uint8_t* nodes, hipStream_t s) {
     const bool al = ((reinterpret_cast<uintptr_t>(base) | stride) & 15) == 0;
-    // LDS-DMA serves any alignment (direct loads need 16 B).  Default: the
-    // segment stage (LOAD 11) for waves whose values share their offset mod 64,
-    // else the 80-byte window stage (LOAD 10), else the value-relative stream
-    if (!al && load != 9 && load != 10 && load != 11) load = load == 1 ? 11 : 0;
+    // Aligned values: 128-byte runs into registers (LOAD 4, the default) or the
+    // LDS-DMA stage (1).  Unaligned ones (direct loads need 16 B; LDS-DMA serves
+    // any alignment): the segment stage (LOAD 11) for waves whose values share
+    // their offset mod 64, else the 80-byte window stage (LOAD 10), else the
+    // value-relative stream
+    if (!al && load != 9 && load != 10 && load != 11) load = (load == 1 || load == 4) ? 11 : 0;
     leaf_dispatch<0>(load, base, nullptr, nullptr, stride, L, nullptr, n, nodes, s, Gate{});
     return hipGetLastError();
 }
@@ -2197,7 +2202,7 @@ hipError_t launch_leaf_offsets(const uint8_t* base, const uint64_t* off, const u
                                const uint32_t* perm, uint64_t n, bool aligned, int load, uint8_t* nodes,
                                hipStream_t s, bool deep, Gate gate) {
     if (perm && deep) load = aligned ? 6 : 7;  // ragged, length-sorted: deep prefetch
-    else if (!aligned && load != 9 && load != 10 && load != 11) load = load == 1 ? 11 : 0;  // as launch_leaf_strided
+    else if (!aligned && load != 9 && load != 10 && load != 11) load = (load == 1 || load == 4) ? 11 : 0;  // as launch_leaf_strided
     leaf_dispatch<1>(load, base, off, len, 0, 0, perm, n, nodes, s, gate);
     return hipGetLastError();
 }

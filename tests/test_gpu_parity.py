@@ -117,7 +117,7 @@ def test_mixed_sizes_log_uniform(nkv, oracle, load):
                                               n, d_nodes.data_ptr()))
         torch.cuda.synchronize()
     finally:
-        ctx.set_option(_lib.NKV_OPT_LEAF_LOAD, 1)
+        ctx.set_option(_lib.NKV_OPT_LEAF_LOAD, 4)  # the default
     want = oracle.tree_from_digests(oracle.leaf_hashes(data, off, lens, threads=8))
     assert np.array_equal(d_nodes.cpu().numpy().reshape(-1, 20), want)
     # aligned copy of the same values (host API path packs at 16 B)
@@ -288,7 +288,7 @@ def test_strided_every_load_path(nkv, oracle, load):
         _lib.check(L.nkv_tree_from_strided_dev(ctx.h, d.data_ptr(), vlen, vlen, n, d_nodes.data_ptr()))
         torch.cuda.synchronize()
     finally:
-        ctx.set_option(_lib.NKV_OPT_LEAF_LOAD, 1)
+        ctx.set_option(_lib.NKV_OPT_LEAF_LOAD, 4)  # the default
     host = oracle.splitmix64_bytes(n * vlen, SEED)
     want = oracle.tree_from_digests(oracle.leaf_hashes_strided(host, vlen, vlen, n, threads=8))
     assert np.array_equal(d_nodes.cpu().numpy().reshape(-1, 20), want)
@@ -420,7 +420,7 @@ def test_line_pair_stage_uniform(nkv, oracle, load, shift, n, vlen, rec):
                                                d_nodes2.data_ptr()))
         torch.cuda.synchronize()
     finally:
-        ctx.set_option(_lib.NKV_OPT_LEAF_LOAD, 1)
+        ctx.set_option(_lib.NKV_OPT_LEAF_LOAD, 4)  # the default
     assert np.array_equal(d_nodes.cpu().numpy().reshape(-1, 20), want)
     assert np.array_equal(d_nodes2.cpu().numpy().reshape(-1, 20), want)
 
@@ -452,7 +452,7 @@ def test_line_pair_stage_ragged_falls_back(nkv, oracle, load, spread):
                                               n, d_nodes.data_ptr()))
         torch.cuda.synchronize()
     finally:
-        ctx.set_option(_lib.NKV_OPT_LEAF_LOAD, 1)
+        ctx.set_option(_lib.NKV_OPT_LEAF_LOAD, 4)  # the default
         ctx.set_option(_lib.NKV_OPT_BUCKET, 2)
     assert np.array_equal(d_nodes.cpu().numpy().reshape(-1, 20), want)
 
@@ -485,6 +485,6 @@ def test_shift_stage_uniform_offset_ragged_lengths(nkv, oracle, shift, maxlen):
                                               n, d_nodes.data_ptr()))
         torch.cuda.synchronize()
     finally:
-        ctx.set_option(_lib.NKV_OPT_LEAF_LOAD, 1)
+        ctx.set_option(_lib.NKV_OPT_LEAF_LOAD, 4)  # the default
         ctx.set_option(_lib.NKV_OPT_BUCKET, 2)
     assert np.array_equal(d_nodes.cpu().numpy().reshape(-1, 20), want)
