@@ -102,7 +102,8 @@ int nkv_ctx_sync(nkv_ctx *ctx);
                                are not 16-byte aligned) = waves whose values share one
                                offset mod 64 stream aligned 64-byte segments (LDS-DMA,
                                or register loads when block counts differ) and shift
-                               them in registers, other waves as 10 */
+                               them in registers, other waves as 10; 12 = 128-byte runs
+                               into registers from each value's own (any) address */
 #define NKV_OPT_BUCKET 2    /* ragged values (nkv_tree_from_values*, nkv_tree_from_records*):
                                1 = hash in length-sorted order (work queue); 0 = in input
                                order; 2 (default) = auto: input order when the full-block

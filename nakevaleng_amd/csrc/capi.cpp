@@ -545,7 +545,7 @@ int nkv_ctx_set_option(nkv_ctx* c, int key, int64_t value) try {
     TRY(bind(c));
     switch (key) {
         case NKV_OPT_LEAF_LOAD:
-            if (value < 1 || value > 11 || value == 6 || value == 7 || value == 8) return NKV_ERR_INVALID;
+            if (value < 1 || value > 12 || value == 6 || value == 7 || value == 8) return NKV_ERR_INVALID;
             c->leaf_load = int(value);
             return NKV_OK;
         case NKV_OPT_BUCKET:

@@ -1161,7 +1161,7 @@ __device__ __forceinline__ void sha1_blocks_any(uint8_t* wbuf, const uint8_t* p,
 #define NKV_RUNS_WAVES 4  // waves per SIMD of the run-load paths (LOAD 4, 5)
 #endif
 template <int MODE, int LOAD>
-__global__ __launch_bounds__(kBlock, (LOAD == 6 || LOAD == 7) ? 2 : ((LOAD == 4 || LOAD == 5) ? NKV_RUNS_WAVES : (LOAD == 9 ? 5 : kLeafWavesPerSimd))) void k_leaf(const uint8_t* __restrict__ base,
+__global__ __launch_bounds__(kBlock, (LOAD == 6 || LOAD == 7) ? 2 : ((LOAD == 4 || LOAD == 5 || LOAD == 12) ? NKV_RUNS_WAVES : (LOAD == 9 ? 5 : kLeafWavesPerSimd))) void k_leaf(const uint8_t* __restrict__ base,
                                                   const uint64_t* __restrict__ off,
                                                   const uint64_t* __restrict__ len, uint64_t stride,
                                                   uint64_t L, const uint32_t* __restrict__ perm,
@@ -1192,16 +1192,16 @@ __global__ __launch_bounds__(kBlock, (LOAD == 6 || LOAD == 7) ? 2 : ((LOAD == 4 
             ln = len[leaf];
         }
     }
-    if (LOAD >= 2 && LOAD <= 7) {
+    if ((LOAD >= 2 && LOAD <= 7) || LOAD == 12) {
         sha1_init(h);
         if (live) {
             if (LOAD == 2) sha1_blocks_direct<false>(p, uint32_t(ln >> 6), h);
             else if (LOAD == 3) sha1_blocks_direct<true>(p, uint32_t(ln >> 6), h);
-            else if (LOAD == 4) sha1_blocks_runs<2>(p, uint32_t(ln >> 6), h);
+            else if (LOAD == 4 || LOAD == 12) sha1_blocks_runs<2>(p, uint32_t(ln >> 6), h);
             else if (LOAD == 5) sha1_blocks_runs<4>(p, uint32_t(ln >> 6), h);
             else if (LOAD == 6) sha1_blocks_deep<true, 4>(p, uint32_t(ln >> 6), h);
             else sha1_blocks_deep<false, 4>(p, uint32_t(ln >> 6), h);
-            if (LOAD == 7) sha1_tail<false>(p, ln, h);
+            if (LOAD == 7 || LOAD == 12) sha1_tail<false>(p, ln, h);
             else sha1_tail<true>(p, ln, h);
             store_digest(nodes, leaf, h);
         }
@@ -2008,7 +2008,10 @@ __global__ __launch_bounds__(kBlock) void k_locate_fold(const uint32_t* __restri
 // which k_locate_fold turns into err and a range whose wide Gate opens the
 // sorted pass only when something was deferred.  A header outside the
 // stream flags bad and hashes the empty value (as k_locate).
-__global__ __launch_bounds__(kBlock, kLeafWavesPerSimd) void k_leaf_records(
+#ifndef NKV_RECORDS_RUNS
+#define NKV_RECORDS_RUNS 0  // k_leaf_records hashes narrow waves from 128-byte register runs at each value's own address
+#endif
+__global__ __launch_bounds__(kBlock, NKV_RECORDS_RUNS ? NKV_RUNS_WAVES : kLeafWavesPerSimd) void k_leaf_records(
     const uint8_t* __restrict__ stream, uint64_t stream_len, const uint64_t* __restrict__ rec_off, uint64_t n,
     int policy, uint64_t* __restrict__ voff, uint64_t* __restrict__ vlen, uint8_t* __restrict__ nodes,
     uint32_t* __restrict__ part, uint32_t* __restrict__ flags, uint32_t* __restrict__ flags_next) {
@@ -2049,7 +2052,8 @@ __global__ __launch_bounds__(kBlock, kLeafWavesPerSimd) void k_leaf_records(
         const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
         uint32_t h[5];
         sha1_init(h);
-        sha1_blocks_any(smem + 5120 * wave, stream + o, live, live ? b32 : 0u, h);
+        if (NKV_RECORDS_RUNS) sha1_blocks_runs<2>(stream + o, live ? b32 : 0u, h);
+        else sha1_blocks_any(smem + 5120 * wave, stream + o, live, live ? b32 : 0u, h);
         // reload the value's place (written above by this lane) rather than
         // keeping it, or its addresses, live through the stage
         asm volatile("" ::: "memory");
@@ -2181,6 +2185,7 @@ static void leaf_dispatch(int load, const uint8_t* base, const uint64_t* off, co
         case 9: leaf_kernel<MODE, 9>(base, off, len, stride, L, perm, n, nodes, s, g); break;
         case 10: leaf_kernel<MODE, 10>(base, off, len, stride, L, perm, n, nodes, s, g); break;
         case 11: leaf_kernel<MODE, 11>(base, off, len, stride, L, perm, n, nodes, s, g); break;
+        case 12: leaf_kernel<MODE, 12>(base, off, len, stride, L, perm, n, nodes, s, g); break;
         default: leaf_kernel<MODE, 0>(base, off, len, stride, L, perm, n, nodes, s, g); break;
     }
 }
@@ -2193,7 +2198,7 @@ hipError_t launch_leaf_strided(const uint8_t* base, uint64_t stride, uint64_t L,
     // any alignment): the segment stage (LOAD 11) for waves whose values share
     // their offset mod 64, else the 80-byte window stage (LOAD 10), else the
     // value-relative stream
-    if (!al && load != 9 && load != 10 && load != 11) load = (load == 1 || load == 4) ? 11 : 0;
+    if (!al && load != 9 && load != 10 && load != 11 && load != 12) load = (load == 1 || load == 4) ? 11 : 0;
     leaf_dispatch<0>(load, base, nullptr, nullptr, stride, L, nullptr, n, nodes, s, Gate{});
     return hipGetLastError();
 }
@@ -2202,7 +2207,8 @@ hipError_t launch_leaf_offsets(const uint8_t* base, const uint64_t* off, const u
                                const uint32_t* perm, uint64_t n, bool aligned, int load, uint8_t* nodes,
                                hipStream_t s, bool deep, Gate gate) {
     if (perm && deep) load = aligned ? 6 : 7;  // ragged, length-sorted: deep prefetch
-    else if (!aligned && load != 9 && load != 10 && load != 11) load = (load == 1 || load == 4) ? 11 : 0;  // as launch_leaf_strided
+    else if (!aligned && load != 9 && load != 10 && load != 11 && load != 12)
+        load = (load == 1 || load == 4) ? 11 : 0;  // as launch_leaf_strided
     leaf_dispatch<1>(load, base, off, len, 0, 0, perm, n, nodes, s, gate);
     return hipGetLastError();
 }

@@ -27,7 +27,7 @@ ENTRIES = ["values_dev", "values_host", "strided_dev", "records_dev", "records_h
 
 def _options(rng, _lib):
     return {
-        _lib.NKV_OPT_LEAF_LOAD: int(rng.choice([1, 2, 3, 4, 5, 9, 10, 11])),
+        _lib.NKV_OPT_LEAF_LOAD: int(rng.choice([1, 2, 3, 4, 5, 9, 10, 11, 12])),
         _lib.NKV_OPT_BUCKET: int(rng.integers(0, 3)),
         _lib.NKV_OPT_DEEP_PREFETCH: int(rng.integers(0, 4)),
         _lib.NKV_OPT_QUEUE_RING: int(rng.choice([2, 3, 4, 12, 13, 14])),

@@ -95,7 +95,7 @@ def test_leaf_hash_mixed_wave_alignment(nkv, oracle, bucket):
     assert np.array_equal(got, want)
 
 
-@pytest.mark.parametrize("load", [1, 2, 4, 5])
+@pytest.mark.parametrize("load", [1, 2, 4, 5, 12])
 def test_mixed_sizes_log_uniform(nkv, oracle, load):
     """BASELINE configs[2] shape at reduced count: log-uniform 64 B - 64 KiB values,
     packed back to back (unaligned), every load path."""
@@ -393,7 +393,7 @@ def test_bucket_modes_narrow_and_wide(nkv, oracle, bucket, spread):
     assert np.array_equal(d_nodes.cpu().numpy().reshape(-1, 20), want)
 
 
-@pytest.mark.parametrize("load", [9, 10, 11])
+@pytest.mark.parametrize("load", [9, 10, 11, 12])
 @pytest.mark.parametrize("shift", [0, 1, 2, 15, 16, 17, 46, 48, 63])
 @pytest.mark.parametrize("n,vlen,rec", [(1, 4050, 4096), (63, 4050, 4096), (3001, 4050, 4096), (777, 327, 400),
                                         (300, 63, 128), (257, 64, 130), (130, 1024, 1100)])
@@ -425,7 +425,7 @@ def test_line_pair_stage_uniform(nkv, oracle, load, shift, n, vlen, rec):
     assert np.array_equal(d_nodes2.cpu().numpy().reshape(-1, 20), want)
 
 
-@pytest.mark.parametrize("load", [9, 10, 11])
+@pytest.mark.parametrize("load", [9, 10, 11, 12])
 @pytest.mark.parametrize("spread", [1, 64, 3000])
 def test_line_pair_stage_ragged_falls_back(nkv, oracle, load, spread):
     """LOAD 9 in input order over values whose full-block counts differ inside a wave: those waves take

@@ -13,3 +13,9 @@ for i in 1 2 3; do
 done
 bash tools/pmc_config.sh cfg2_runs || exit 1
 python3 tools/pmc_traffic_cfg.py cfg2_runs "void nkv::k_leaf<0, 4>" 4294967296 1048576 || exit 1
+# records: the segment stage (product) vs 128-byte register runs at each value's own address (experiment library)
+for i in 1 2 3; do
+  for lib in nakevaleng_amd/libnkvmerkle.so tools/libnkvmerkle_rruns.so; do
+    NKV_LIB=$lib timeout -k 10 120 python bench.py --config records --no-cpu-baseline --verify 2>/dev/null | python -c "import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); print('[records $lib]', d['value'], d['ms_per_step'], d['kernel_ms'], d.get('verified_vs_oracle'))" || exit 1
+  done
+done
