@@ -994,7 +994,10 @@ __device__ __forceinline__ void load_seg(const uint4* s, uint32_t r[16]) {
     }
 }
 
-template <class Hook = NoRaw>
+// LINES: whole 128-byte lines into registers when the values' segments start
+// lines (the caller's kernel must afford ~86 VGPRs: k_leaf_records runs 5
+// waves per SIMD); else the LDS-DMA stage or 64-byte register segments.
+template <class Hook = NoRaw, bool LINES = false>
 __device__ __forceinline__ bool sha1_blocks_shift(uint8_t* wbuf, const uint8_t* p, bool live, uint32_t my_nfull,
                                                   uint32_t h[5], Hook hook = Hook{}) {
     const uint32_t o = live ? uint32_t(reinterpret_cast<uintptr_t>(p) & 63u) : 0u;
@@ -1006,7 +1009,47 @@ __device__ __forceinline__ bool sha1_blocks_shift(uint8_t* wbuf, const uint8_t* 
     const uint32_t q = o0 >> 2;
     const uint32_t sel = be_sel(o0 & 3u);
     uint32_t a[16], b[16], w[16];
-    if (wbuf && __all(!live || my_nfull == nmax)) {
+#ifndef NKV_SHIFT_REGS
+#define NKV_SHIFT_REGS 0  // experiment builds: segments straight into registers, no LDS-DMA stage
+#endif
+    // Whole 128-byte lines into registers: when every live value's segment 0
+    // starts a line and the block counts are equal, each lane loads its aligned
+    // lines (two segments, eight 16-byte loads) once, no LDS.  Three segment
+    // sets rotate over four blocks: block k takes segments k and k + 1.  Every
+    // line loaded holds a needed segment, so no load leaves the value's pages.
+    if (LINES && __all(!live || my_nfull == nmax) &&
+        __all(!live || ((reinterpret_cast<uintptr_t>(p) - o) & 64u) == 0u)) {
+        const uint4* seg = reinterpret_cast<const uint4*>(live ? p - o : p);
+        uint32_t c[16];
+        auto line = [&](uint32_t sg, uint32_t x[16], uint32_t y[16]) {
+            if (live) {
+                load_seg(seg + 4 * sg, x);
+                load_seg(seg + 4 * (sg + 1), y);
+            }
+        };
+        auto block = [&](const uint32_t lo[16], const uint32_t hi[16]) {
+            funnel_u(q, lo, hi, sel, w);
+            if (live) {
+                hook.be(w);
+                sha1_compress(h, w);
+            }
+            asm volatile("" ::: "memory");  // the next line's loads stay after this compress
+        };
+        line(0u, a, b);
+        for (uint32_t k = 0; k < nmax; k += 4) {
+            block(a, b);  // segments k, k + 1
+            if (k + 1 >= nmax) break;
+            line(k + 2, a, c);
+            block(b, a);  // k + 1, k + 2
+            if (k + 2 >= nmax) break;
+            block(a, c);  // k + 2, k + 3
+            if (k + 3 >= nmax) break;
+            line(k + 4, a, b);
+            block(c, a);  // k + 3, k + 4
+        }
+        return true;
+    }
+    if (!NKV_SHIFT_REGS && wbuf && __all(!live || my_nfull == nmax)) {
         // Equal block counts: the segments go HBM -> LDS by LDS-DMA, one segment
         // of lookahead, in k_leaf's aligned stage layout (value j's segment at
         // wbuf + 64 j, chunks XOR-swizzled; sha1_blocks_lds), then into the
@@ -1124,9 +1167,10 @@ __device__ __forceinline__ bool sha1_blocks_shift(uint8_t* wbuf, const uint8_t* 
 // 5 KiB of LDS): the segment stage when the values share their offset mod 64,
 // else the 80-byte window stage when their full-block counts are equal, else
 // the value-relative stream.  k_leaf's LOAD 11 for MODE 1 and k_leaf_records.
+template <bool LINES = false>
 __device__ __forceinline__ void sha1_blocks_any(uint8_t* wbuf, const uint8_t* p, bool live, uint32_t my_nfull,
                                                 uint32_t h[5]) {
-    if (sha1_blocks_shift(wbuf, p, live, my_nfull, h)) return;
+    if (sha1_blocks_shift<NoRaw, LINES>(wbuf, p, live, my_nfull, h)) return;
     if (sha1_blocks_pair(true, wbuf, p, live, my_nfull, h)) return;
     const int lane = threadIdx.x & 63;
     const uint32_t q = (uint32_t(lane) & 3u) ^ ((uint32_t(lane) >> 4) & 3u);
@@ -2011,7 +2055,13 @@ __global__ __launch_bounds__(kBlock) void k_locate_fold(const uint32_t* __restri
 #ifndef NKV_RECORDS_RUNS
 #define NKV_RECORDS_RUNS 0  // k_leaf_records hashes narrow waves from 128-byte register runs at each value's own address
 #endif
-__global__ __launch_bounds__(kBlock, NKV_RECORDS_RUNS ? NKV_RUNS_WAVES : kLeafWavesPerSimd) void k_leaf_records(
+#ifndef NKV_RECORDS_LINES
+#define NKV_RECORDS_LINES 1  // narrow waves of line-aligned records: whole 128-byte lines into registers
+#endif
+#ifndef NKV_RECORDS_WAVES
+#define NKV_RECORDS_WAVES (NKV_RECORDS_LINES ? 5 : kLeafWavesPerSimd)  // the line path takes ~86 VGPRs
+#endif
+__global__ __launch_bounds__(kBlock, NKV_RECORDS_RUNS ? NKV_RUNS_WAVES : NKV_RECORDS_WAVES) void k_leaf_records(
     const uint8_t* __restrict__ stream, uint64_t stream_len, const uint64_t* __restrict__ rec_off, uint64_t n,
     int policy, uint64_t* __restrict__ voff, uint64_t* __restrict__ vlen, uint8_t* __restrict__ nodes,
     uint32_t* __restrict__ part, uint32_t* __restrict__ flags, uint32_t* __restrict__ flags_next) {
@@ -2053,7 +2103,7 @@ __global__ __launch_bounds__(kBlock, NKV_RECORDS_RUNS ? NKV_RUNS_WAVES : kLeafWa
         uint32_t h[5];
         sha1_init(h);
         if (NKV_RECORDS_RUNS) sha1_blocks_runs<2>(stream + o, live ? b32 : 0u, h);
-        else sha1_blocks_any(smem + 5120 * wave, stream + o, live, live ? b32 : 0u, h);
+        else sha1_blocks_any<NKV_RECORDS_LINES != 0>(smem + 5120 * wave, stream + o, live, live ? b32 : 0u, h);
         // reload the value's place (written above by this lane) rather than
         // keeping it, or its addresses, live through the stage
         asm volatile("" ::: "memory");
