@@ -1385,6 +1385,9 @@ struct CrcBE {
 // voff / vlen for the length-sorted leaf pass; a hashed value's voff becomes
 // kDone.  Each workgroup leaves (0, deferred ? ~0 : 0, 0) in part, folded by
 // k_locate_fold into the range whose wide Gate opens the sorted pass.
+#ifndef NKV_VERIFY_LINES
+#define NKV_VERIFY_LINES 0  // whole 128-byte lines into registers for line-aligned records (as k_leaf_records)
+#endif
 #ifndef NKV_VERIFY_WAVES
 #define NKV_VERIFY_WAVES 7
 #endif
@@ -1480,7 +1483,8 @@ __global__ __launch_bounds__(kBlock, NKV_VERIFY_WAVES) void k_leaf_verify(
         };
         // records of one size share their offset mod 64: each line once
         // through the segment stage (LOAD 11); else the value-relative stream
-        if (!sha1_blocks_shift(wbuf, p, live, my_nfull, h, hook)) sha1_blocks_lds(wbuf, whi, my_nfull, issue, h, hook);
+        if (!sha1_blocks_shift<decltype(hook), NKV_VERIFY_LINES != 0>(wbuf, p, live, my_nfull, h, hook))
+            sha1_blocks_lds(wbuf, whi, my_nfull, issue, h, hook);
         if (live) {
             sha1_tail<false>(p, ln, h, hook);  // the tail's checksum from the same loads
             store_digest(nodes, t, h);
