@@ -1386,10 +1386,10 @@ struct CrcBE {
 // kDone.  Each workgroup leaves (0, deferred ? ~0 : 0, 0) in part, folded by
 // k_locate_fold into the range whose wide Gate opens the sorted pass.
 #ifndef NKV_VERIFY_LINES
-#define NKV_VERIFY_LINES 0  // whole 128-byte lines into registers for line-aligned records (as k_leaf_records)
+#define NKV_VERIFY_LINES 1  // whole 128-byte lines into registers for line-aligned records (as k_leaf_records)
 #endif
 #ifndef NKV_VERIFY_WAVES
-#define NKV_VERIFY_WAVES 7
+#define NKV_VERIFY_WAVES (NKV_VERIFY_LINES ? 4 : 7)  // the line path with the CRC state takes ~105 VGPRs
 #endif
 __global__ __launch_bounds__(kBlock, NKV_VERIFY_WAVES) void k_leaf_verify(
     const uint8_t* __restrict__ stream, uint64_t stream_len, const uint64_t* __restrict__ rec_off, uint64_t n,
