@@ -545,11 +545,11 @@ def main():
                 "bound": "hbm",
                 "kernel": ("leaf phase: length sort + ragged leaf SHA-1 (%s)" % LEAF_KERNEL.get(args.deep, "default"))
                           if mixed else
-                          ("leaf phase: k_leaf_verify (header parse + record CRC + leaf SHA-1, input order)"
+                          ("leaf phase: k_leaf_verify (header parse + record CRC + leaf SHA-1 from whole 128-byte lines in registers, input order)"
                            if verify_crc else
                            ("leaf phase: k_locate + k_leaf<offsets, aligned-segment stage> (input order)"
                             if args.records_fused == 0 else
-                            "leaf phase: k_leaf_records (header parse + aligned-segment stage, input order)")) if records else
+                            "leaf phase: k_leaf_records (header parse + whole 128-byte lines into registers, input order)")) if records else
                           ("k_leaf<strided, LDS-DMA stage> (leaf SHA-1, level 0)" if args.leaf_load == 1 else
                            "k_leaf<strided, 128-byte register runs> (leaf SHA-1, level 0)" if args.leaf_load in (0, 4)
                            else f"k_leaf<strided, load path {args.leaf_load}> (leaf SHA-1, level 0)"),
