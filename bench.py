@@ -28,10 +28,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.
 # Measured compute ceiling of the per-lane SHA-1 (no memory traffic, 8 waves/SIMD,
 # 2.37-2.39 GHz): tools/sha1_rate.hip -> profiles/r01_sha1_compute_rate.txt.
 SHA1_VALU_CEILING_GBS = 4100.0
-# The same ceiling at the shader clock this workload sustains while streaming
-# random bytes from HBM (2.04 GHz against 2.37 GHz from L2/registers, board power
-# limit; tools/pattern_power.hip -> profiles/r01_clock_power.txt).
-STREAMING_CLOCK_RATIO = 2.04 / 2.37
+# (The LDS-DMA loop streamed random bytes at ~2.04 GHz under the board power
+# limit, profiles/r01_clock_power.txt; the register-load loop that replaced it
+# runs faster than that clock allows, so no fixed streaming-clock ceiling is
+# reported.)
 # k_leaf_verify's block loop issues ~711 VALU per 64-B block (SHA-1's 614 plus
 # 97 for the CRC's byte indices and three-input XORs; ISA count, DESIGN.md
 # K1v) against ~618.5 for the plain leaf kernel, so its compute ceiling is the
@@ -564,8 +564,6 @@ def main():
                 "traffic_bounds": traffic_bounds,  # RDREQ x 64 .. x 128 B (profiles/pmc_traffic.json)
                 "valu_ceiling": round(valu_ceiling, 1),
                 "valu_frac": round(achieved / valu_ceiling, 4),
-                "valu_ceiling_at_streaming_clock": round(valu_ceiling * STREAMING_CLOCK_RATIO, 1),
-                "valu_frac_at_streaming_clock": round(achieved / (valu_ceiling * STREAMING_CLOCK_RATIO), 4),
             },
             "kernel_ms": {"leaf": round(leaf_ms, 4), "tree_reduce": round(reduce_ms, 4),
                           "bfs_image": round(bfs_ms, 4)},
