@@ -224,3 +224,31 @@ def test_pass_flag_sets_alternate(nkv, oracle):
             assert got[2] == [0, 2**64 - 1, 1], (step, name)
         else:
             _check(got, want, n)
+
+
+@pytest.mark.parametrize("rec,ks", [(4096, 16), (1024, 16), (1024, 50), (256, 0), (384, 7), (192, 16), (4096, 97)])
+def test_line_register_path_records(nkv, oracle, rec, ks):
+    """Records whose segment 0 starts a 128-byte line (rec a multiple of 128)
+    take the whole-line register path in k_leaf_records and k_leaf_verify;
+    rec = 192 mixes line parities inside a wave (the segment stage instead).
+    The last record ends at the end of the stream.  Both entries against the
+    oracle, a few stored Crcs corrupted."""
+    torch = _torch()
+    _lib, ctx = nkv
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    L = _lib.lib()
+    n = 5000
+    buf, off = _sstable(n, ks=ks, vs=rec - 30 - ks, oracle=oracle)
+    assert buf.size == n * rec
+    for i in (0, 777, n - 1):
+        buf[int(off[i]) + 30 + ks] ^= 0x01  # first value byte
+    want = _want(oracle, buf, off)
+    _check(_run(torch, L, _lib, ctx, buf, off), want, n)
+    d_buf, d_off = _dev(torch, buf), _dev(torch, off)
+    d_nodes = torch.zeros(L.nkv_total_nodes(n) * 20, dtype=torch.uint8, device="cuda")
+    d_err = torch.full((1,), 7, dtype=torch.int32, device="cuda")
+    _lib.check(L.nkv_tree_from_records_dev(ctx.h, d_buf.data_ptr(), buf.size, d_off.data_ptr(), n,
+                                           d_nodes.data_ptr(), d_err.data_ptr()))
+    torch.cuda.synchronize()
+    assert int(d_err.item()) == 0
+    assert np.array_equal(d_nodes.cpu().numpy().reshape(-1, 20), want[0])
