@@ -25,24 +25,22 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md (chip table)
-# Measured compute ceiling of the per-lane SHA-1 (no memory traffic, 8 waves/SIMD,
-# 2.37-2.39 GHz): tools/sha1_rate.hip -> profiles/r01_sha1_compute_rate.txt.
-SHA1_VALU_CEILING_GBS = 4100.0
-# (The LDS-DMA loop streamed random bytes at ~2.04 GHz under the board power
-# limit, profiles/r01_clock_power.txt; the register-load loop that replaced it
-# runs faster than that clock allows, so no fixed streaming-clock ceiling is
-# reported.)
-# k_leaf_verify's block loop issues ~711 VALU per 64-B block (SHA-1's 614 plus
-# 97 for the CRC's byte indices and three-input XORs; ISA count, DESIGN.md
-# K1v) against ~618.5 for the plain leaf kernel, so its compute ceiling is the
-# SHA-1 one scaled by that ratio.
-VERIFY_VALU_RATIO = 618.5 / 711.0
+# The VALU-issue ceiling of the leaf kernel at the shader clock its waves
+# actually ran at in the timed loop (the clock probe, sclk_mhz): every SIMD
+# issuing one VALU instruction per VALU_CYCLES cycles (the half-rate ops
+# v_add3 / v_alignbit / v_perm set the cadence, profiles/r01_valu_rate.txt),
+# VALU_PER_WAVE_BLOCK instructions per wave per 64-byte block (PMC
+# SQ_INSTS_VALU per launch / wave-blocks), 4096 bytes per
+# wave-block (64 lanes x 64 B):
+#   ceiling = SIMDS x f / (VALU_PER_WAVE_BLOCK x VALU_CYCLES) x 4096 B.
+SIMDS = 1024  # 256 CUs x 4
+VALU_CYCLES = 4.0
+VALU_PER_WAVE_BLOCK = {"leaf": 618.5, "verify": 711.0}
+SHA1_VALU_CEILING_GBS = 4100.0  # fallback without a clock reading: tools/sha1_rate.hip at 2.37 GHz
 SEED = 0x6E616B65
 SEED_MIXED = 0x6E616B66
 
 
-LEAF_KERNEL = {-1: "library default", 0: "k_leaf, one-block lookahead", 1: "k_leaf, deep register prefetch",
-               2: "k_leaf_queue, deep register prefetch", 3: "k_leaf_queue, LDS chunk ring"}
 
 
 def mixed_lengths(target_bytes: int, seed: int):
@@ -65,21 +63,35 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", choices=["sstable4k", "mixed", "records", "records_verify", "one_tree"],
+    ap.add_argument("--config", choices=["sstable4k", "mixed", "records", "records_verify", "one_tree", "runs4",
+                                         "api_flush"],
                     default="sstable4k",
                     help="sstable4k = BASELINE configs[1] (the metric); mixed = configs[2]; records = the "
                          "compaction form: 1 Mi serialized 4 KiB records in a Data table, values located "
                          "from the record headers and hashed in place; records_verify = the same plus every "
-                         "record's Crc checked (nkv_tree_verify_records_dev)")
+                         "record's Crc checked (nkv_tree_verify_records_dev); runs4 = configs[3] per GPU: "
+                         "lsm_run_max = 4 tables of 1 Mi x 4 KiB per step (sstable4k with --tables 4); "
+                         "api_flush = the host-inclusive flush through the C++ Go-API mirror: NewLeaf x n "
+                         "from host memory, New, Root, Serialize to a fresh file (tools/api_flush.cpp)")
+    ap.add_argument("--api-cycles", type=int, default=4, help="api_flush: flushes per mode (the first allocates "
+                                                              "the pinned arena)")
+    ap.add_argument("--tables", type=int, default=0,
+                    help="tables per step and GPU (0: 4 for runs4, else 1); more than one goes through "
+                         "nkv_trees_dev, spread over --table-lanes streams")
+    ap.add_argument("--table-lanes", type=int, default=0,
+                    help="NKV_OPT_TABLE_LANES (0 = library default 2; 1 = the tables one after another on one stream)")
+    ap.add_argument("--backend", choices=["torch", "capi"], default="torch",
+                    help="torch: one process per GPU (torch.distributed over RCCL); capi: one process over all "
+                         "--gpus through the library's group (nkv_group_*: a context per GPU, ncclCommInitAll, "
+                         "the roots all-gathered by the library)")
+    ap.add_argument("--no-clock", action="store_true", help="no shader-clock probe in the timed loop")
     ap.add_argument("--mixed-bytes", type=int, default=4 << 30, help="payload of the mixed config")
     ap.add_argument("--no-bucket", action="store_true", help="hash ragged values in input order (--bucket 0)")
     ap.add_argument("--bucket", type=int, default=-1, help="NKV_OPT_BUCKET override (0 input order, 1 sorted, 2 auto)")
-    ap.add_argument("--leaf-load", type=int, default=0, help="NKV_OPT_LEAF_LOAD override (0 = library default)")
-    ap.add_argument("--deep", type=int, default=-1,
-                    help="NKV_OPT_DEEP_PREFETCH override for ragged batches (-1 = library default)")
-    ap.add_argument("--queue-split", type=int, default=-1, help="NKV_OPT_QUEUE_SPLIT override")
-    ap.add_argument("--queue-waves", type=int, default=0, help="NKV_OPT_QUEUE_WAVES override")
-    ap.add_argument("--queue-ring", type=int, default=0, help="NKV_OPT_QUEUE_RING override (2, 3, 4)")
+    ap.add_argument("--leaf-load", type=int, default=0,
+                    help="NKV_OPT_LEAF_LOAD override (0 = library default 4: 128-byte register runs for aligned "
+                         "values; 11: the staged paths for every value)")
+    ap.add_argument("--queue-waves", type=int, default=0, help="NKV_OPT_QUEUE_WAVES override (1..3)")
     ap.add_argument("--records-fused", type=int, default=-1, help="NKV_OPT_RECORDS_FUSED override (0, 1)")
     ap.add_argument("--leaves", type=int, default=1 << 20)
     ap.add_argument("--key-bytes", type=int, default=16, help="records configs: KeySize (the Value starts at +30+key)")
@@ -220,9 +232,9 @@ def preroll(step, drain, sync, seconds, dist=None, flag=None) -> int:
 
 class BatchedRootGather:
     """The roots of a whole run of tables in one collective: each step copies
-    its 20-byte root (on the compute stream, behind the tree) into the next
-    slot, and drain() all-gathers the filled slots at once (world x k x 20 B),
-    so a timed loop of K tables issues one RCCL call instead of K (SURVEY.md
+    its tables' 20-byte roots (on the compute stream, behind the trees) into the
+    next slots, and drain() all-gathers the filled slots at once (world x k x 20
+    B), so a timed loop of K steps issues one RCCL call instead of K (SURVEY.md
     section 8e: the gather follows the builds; fewer, larger collectives).
     Every gather still completes inside the timed region (drain before the
     closing barrier).  dist None: one rank, nothing to gather."""
@@ -237,28 +249,240 @@ class BatchedRootGather:
     def begin(self):
         return self.nodes
 
-    def end(self, nodes):
+    def end(self, nodes, more=()):
+        """Queue the roots of this step's tables (nodes first, then `more`)."""
         if self.dist:
-            if self.k == self.cap:
+            group = (nodes,) + tuple(more)
+            if self.k + len(group) > self.cap:
                 self.drain()
-            self.slots[20 * self.k:20 * (self.k + 1)].copy_(nodes[-20:])
-            self.k += 1
+            self.first = self.k  # slot of this step's first table
+            for nb in group:
+                self.slots[20 * self.k:20 * (self.k + 1)].copy_(nb[-20:])
+                self.k += 1
 
     def drain(self):
         if self.dist and self.k:
             out = self.out[:self.world * self.k * 20]
             self.dist.all_gather_into_tensor(out, self.slots[:self.k * 20])
-            self.last = out.view(self.world, self.k, 20)[:, self.k - 1].reshape(-1)
+            # every rank's root of the latest step's first table
+            self.last = out.view(self.world, self.k, 20)[:, self.first].reshape(-1)
             self.k = 0
 
     def last_roots(self):
         return self.last
 
 
+TABLE_SEED_STEP = 7919  # table t of a step uses seed + rank + t * TABLE_SEED_STEP (t = 0: the single-table seeds)
+
+
+def build_tables(args, torch, _lib, L, ctx, rank, T, device="cuda"):
+    """T independent tables of the config's shape, resident in HBM on `device`.
+    Each is a dict: nodes (device tensor), table (NkvTable for nkv_trees_dev),
+    single() (the single-table entry on ctx), want() (the oracle root, host),
+    plus its buffers."""
+    import numpy as np
+    tabs = []
+    for t in range(T):
+        seed_t = t * TABLE_SEED_STEP
+        tab = {}
+        if args.config in ("records", "records_verify"):
+            n, rb, ks = args.leaves, args.value_bytes, args.key_bytes
+            vlen = rb - 30 - ks  # record.go:191-199: 30-B header, the key, the rest is the Value
+            stream_len = n * rb
+            data = torch.empty(stream_len, dtype=torch.uint8, device=device)
+            _lib.check(L.nkv_fill_splitmix64_dev(ctx.h, data.data_ptr(), stream_len, SEED + rank + seed_t))
+            v = data.view(n, rb)
+            v[:, 14:22] = torch.from_numpy(np.frombuffer(np.uint64(ks).tobytes(), np.uint8).copy()).to(device)
+            v[:, 22:30] = torch.from_numpy(np.frombuffer(np.uint64(vlen).tobytes(), np.uint8).copy()).to(device)
+            d_roff = torch.arange(n, dtype=torch.int64, device=device) * rb
+            nodes = torch.empty(L.nkv_total_nodes(n) * 20, dtype=torch.uint8, device=device)
+            d_err = torch.zeros(1, dtype=torch.int32, device=device)
+            tab.update(data=data, d_roff=d_roff, nodes=nodes, d_err=d_err, n=n, vlen=vlen, nbytes=n * vlen,
+                       stream_len=stream_len, rb=rb, ks=ks)
+            if args.config == "records_verify":  # store each record's right checksum (computed on the device once)
+                d_crc = torch.empty(n, dtype=torch.int32, device=device)
+                d_stats = torch.zeros(3, dtype=torch.int64, device=device)
+                _lib.check(L.nkv_record_crc_dev(ctx.h, data.data_ptr(), stream_len, d_roff.data_ptr(), n,
+                                                d_crc.data_ptr(), d_stats.data_ptr()))
+                v[:, 0:4] = d_crc.view(torch.uint8).view(n, 4)
+                tab.update(d_stats=d_stats)
+                tab["table"] = _lib.table(_lib.NKV_TABLE_VERIFY, nodes.data_ptr(), n, base=data.data_ptr(),
+                                          base_len=stream_len, off=d_roff.data_ptr(), stats=d_stats.data_ptr())
+
+                def single(tab=tab):
+                    _lib.check(L.nkv_tree_verify_records_dev(ctx.h, tab["data"].data_ptr(), tab["stream_len"],
+                                                             tab["d_roff"].data_ptr(), tab["n"],
+                                                             tab["nodes"].data_ptr(), None,
+                                                             tab["d_stats"].data_ptr()))
+            else:
+                tab["table"] = _lib.table(_lib.NKV_TABLE_RECORDS, nodes.data_ptr(), n, base=data.data_ptr(),
+                                          base_len=stream_len, off=d_roff.data_ptr(), err=d_err.data_ptr())
+
+                def single(tab=tab):
+                    _lib.check(L.nkv_tree_from_records_dev(ctx.h, tab["data"].data_ptr(), tab["stream_len"],
+                                                           tab["d_roff"].data_ptr(), tab["n"],
+                                                           tab["nodes"].data_ptr(), tab["d_err"].data_ptr()))
+
+            def want(tab=tab):
+                from oracle import oracle_c as oc
+                host = tab["data"].cpu().numpy()
+                voff = np.arange(tab["n"], dtype=np.uint64) * tab["rb"] + 30 + tab["ks"]
+                return oc.tree_from_digests(oc.leaf_hashes(host, voff, np.full(tab["n"], tab["vlen"], np.uint64),
+                                                           threads=16))[-1].tobytes().hex()
+        elif args.config == "mixed":
+            lens_h, off_h = mixed_lengths(args.mixed_bytes, SEED_MIXED + rank + seed_t)
+            n = len(lens_h)
+            nbytes = int(lens_h.sum())
+            data = torch.empty(nbytes, dtype=torch.uint8, device=device)
+            _lib.check(L.nkv_fill_splitmix64_dev(ctx.h, data.data_ptr(), nbytes, SEED_MIXED + rank + seed_t))
+            d_off = torch.from_numpy(off_h.view(np.int64)).to(device)
+            d_len = torch.from_numpy(lens_h.view(np.int64)).to(device)
+            nodes = torch.empty(L.nkv_total_nodes(n) * 20, dtype=torch.uint8, device=device)
+            tab.update(data=data, d_off=d_off, d_len=d_len, nodes=nodes, n=n, vlen=None, nbytes=nbytes,
+                       lens_h=lens_h, off_h=off_h, seed=SEED_MIXED + rank + seed_t)
+            tab["table"] = _lib.table(_lib.NKV_TABLE_VALUES, nodes.data_ptr(), n, base=data.data_ptr(),
+                                      off=d_off.data_ptr(), lens=d_len.data_ptr())
+
+            def single(tab=tab):
+                _lib.check(L.nkv_tree_from_values_dev(ctx.h, tab["data"].data_ptr(), tab["d_off"].data_ptr(),
+                                                      tab["d_len"].data_ptr(), tab["n"], tab["nodes"].data_ptr()))
+
+            def want(tab=tab):
+                from oracle import oracle_c as oc
+                host = oc.splitmix64_bytes(tab["nbytes"], tab["seed"])
+                return oc.tree_from_digests(oc.leaf_hashes(host, tab["off_h"], tab["lens_h"],
+                                                           threads=16))[-1].tobytes().hex()
+        else:  # sstable4k, runs4, one_tree: n values of vlen bytes at base + i vlen
+            n, vlen = args.leaves, args.value_bytes
+            nbytes = n * vlen
+            data = torch.empty(nbytes, dtype=torch.uint8, device=device)
+            _lib.check(L.nkv_fill_splitmix64_dev(ctx.h, data.data_ptr(), nbytes, SEED + rank + seed_t))
+            nodes = torch.empty(L.nkv_total_nodes(n) * 20, dtype=torch.uint8, device=device)
+            tab.update(data=data, nodes=nodes, n=n, vlen=vlen, nbytes=nbytes, seed=SEED + rank + seed_t)
+            tab["table"] = _lib.table(_lib.NKV_TABLE_STRIDED, nodes.data_ptr(), n, base=data.data_ptr(),
+                                      stride=vlen, length=vlen)
+
+            def single(tab=tab):
+                _lib.check(L.nkv_tree_from_strided_dev(ctx.h, tab["data"].data_ptr(), tab["vlen"], tab["vlen"],
+                                                       tab["n"], tab["nodes"].data_ptr()))
+
+            def want(tab=tab):
+                from oracle import oracle_c as oc
+                host = oc.splitmix64_bytes(tab["nbytes"], tab["seed"])
+                return oc.tree_from_digests(oc.leaf_hashes_strided(host, tab["vlen"], tab["vlen"], tab["n"],
+                                                                   threads=16))[-1].tobytes().hex()
+        tab["single"], tab["want"] = single, want
+        tabs.append(tab)
+    return tabs
+
+
+def valu_ceiling(mhz, verify):
+    """GB/s the leaf kernel would reach issuing one VALU per VALU_CYCLES on every
+    SIMD at the measured clock (None without a clock reading)."""
+    if not mhz:
+        return None
+    per = VALU_PER_WAVE_BLOCK["verify" if verify else "leaf"]
+    return SIMDS * mhz * 1e6 / (per * VALU_CYCLES) * 4096 / 1e9
+
+
+def pmc_traffic(args, n, vlen, nbytes):
+    """PMC-measured HBM bytes of this config's leaf kernel, per launch (separate
+    rocprofv3 passes: tools/pmc_sizes.sh for cfg2, tools/pmc_config.sh for the others)."""
+    cfg2_pmc = {0: "pmc_traffic_cfg2_runs.json", 4: "pmc_traffic_cfg2_runs.json",
+                1: "pmc_traffic.json"}.get(args.leaf_load)
+    pmc_name = {"sstable4k": cfg2_pmc, "runs4": cfg2_pmc, "records": "pmc_traffic_records.json",
+                "mixed": "pmc_traffic_mixed.json", "records_verify": "pmc_traffic_records_verify.json"}.get(args.config)
+    pmc_path = os.path.join(ROOT, "profiles", pmc_name) if pmc_name else None
+    if pmc_path and os.path.exists(pmc_path):
+        with open(pmc_path) as f:
+            pmc = json.load(f)
+        same = pmc.get("leaves") == n and (pmc.get("value_bytes") in (None, vlen)) and \
+            pmc.get("algorithmic_bytes_per_launch") in (None, nbytes)
+        if same:
+            return pmc.get("hbm_bytes_per_launch"), pmc.get("hbm_read_bytes_bounds_per_launch")
+    return None, None
+
+
+def set_options(args, _lib, ctx):
+    if args.leaf_load:
+        ctx.set_option(_lib.NKV_OPT_LEAF_LOAD, args.leaf_load)
+    if args.queue_split >= 0:
+        ctx.set_option(_lib.NKV_OPT_QUEUE_SPLIT, args.queue_split)
+    if args.queue_waves:
+        ctx.set_option(_lib.NKV_OPT_QUEUE_WAVES, args.queue_waves)
+    if args.records_fused >= 0:
+        ctx.set_option(_lib.NKV_OPT_RECORDS_FUSED, args.records_fused)
+    if args.no_bucket:
+        ctx.set_option(_lib.NKV_OPT_BUCKET, 0)
+    elif args.bucket >= 0:
+        ctx.set_option(_lib.NKV_OPT_BUCKET, args.bucket)
+    if args.table_lanes:
+        ctx.set_option(_lib.NKV_OPT_TABLE_LANES, args.table_lanes)
+
+
+def workload_text(args, n, vlen, nbytes, world, T, rb=None, ks=None):
+    mixed = args.config == "mixed"
+    records = args.config in ("records", "records_verify")
+    if args.config == "runs4" or T > 1:
+        head = (f"BASELINE configs[3] per GPU: lsm_run_max = {T} runs per compaction, " if args.config == "runs4"
+                else f"{T} tables per step, ")
+    else:
+        head = ""
+    if mixed:
+        body = ("BASELINE configs[2]: mixed 64 B - 64 KiB log-uniform values packed back to back, "
+                + ("input order" if args.no_bucket else "length-bucketed"))
+    elif records:
+        body = (f"compaction form: {n} serialized {rb}-B records ({ks}-B key, {vlen}-B value) in a "
+                "Data table in HBM; values located from the headers and hashed in place, full tree"
+                + ("; every record's Crc (Key ++ Value) checked in the same pass"
+                   if args.config == "records_verify" else ""))
+    elif args.config == "one_tree":
+        body = (f"one tree over {world} GPU(s): {n} x {vlen} B values per rank, each rank builds the "
+                "levels of its aligned leaf range, sub-roots all-gathered, top levels on rank 0")
+    else:
+        body = (("BASELINE configs[1]: single SSTable flush, 1 Mi x 4 KiB values, "
+                 if (n, vlen) == (1 << 20, 4096) and T == 1 else
+                 "BASELINE configs[4] per-GPU table (8 Mi x 4 KiB values), "
+                 if (n, vlen) == (8 << 20, 4096) else
+                 f"tables of {n} x {vlen} B values, ")
+                + "leaf SHA-1 + full tree reduce (one table per GPU; roots all-gathered over RCCL when N>1)")
+    return head + body
+
+
+def kernel_text(args, T):
+    mixed = args.config == "mixed"
+    records = args.config in ("records", "records_verify")
+    if mixed:
+        k = "leaf phase: length sort + ragged leaf SHA-1 (k_leaf_queue: work queue, LDS ring)"
+    elif args.config == "records_verify":
+        k = ("leaf phase: k_leaf_verify (header parse + record CRC + leaf SHA-1 from whole 128-byte lines in "
+             "registers, input order)")
+    elif records:
+        k = ("leaf phase: k_locate + k_leaf<offsets, aligned-segment stage> (input order)"
+             if args.records_fused == 0 else
+             "leaf phase: k_leaf_records (header parse + whole 128-byte lines into registers, input order)")
+    else:
+        k = ("k_leaf<strided, LDS-DMA stage> (leaf SHA-1, level 0)" if args.leaf_load == 1 else
+             "k_leaf<strided, 128-byte register runs> (leaf SHA-1, level 0)" if args.leaf_load in (0, 4)
+             else f"k_leaf<strided, load path {args.leaf_load}> (leaf SHA-1, level 0)")
+    if T > 1:
+        k += f"; {T} tables per step over {args.table_lanes or 2} streams (per-table event spans overlap)"
+    return k
+
+
 def main():
     args = parse()
     if args.config in ("records", "records_verify") and args.value_bytes <= 30 + args.key_bytes:
         raise SystemExit("bench.py: --value-bytes (the record size) must exceed the 30-B header + --key-bytes")
+    T = args.tables or (4 if args.config == "runs4" else 1)
+    if args.config == "one_tree" and T != 1:
+        raise SystemExit("bench.py: --config one_tree builds one tree per step (--tables 1)")
+    if args.gather == "step" and T != 1:
+        raise SystemExit("bench.py: --gather step gathers one table per step (--tables 1)")
+    if args.backend == "capi":
+        return main_capi(args, T)
+    if args.config == "api_flush":
+        return main_api_flush(args)
     rc = ensure_ranks(args, sys.argv[1:])
     if rc is not None:
         sys.exit(rc)
@@ -287,89 +511,33 @@ def main():
     ctx = _lib.Context(dev)
     stream = torch.cuda.current_stream()
     ctx.set_stream(stream.cuda_stream)
+    set_options(args, _lib, ctx)
 
-    if args.leaf_load:
-        ctx.set_option(_lib.NKV_OPT_LEAF_LOAD, args.leaf_load)
-    if args.deep >= 0:
-        ctx.set_option(_lib.NKV_OPT_DEEP_PREFETCH, args.deep)
-    if args.queue_split >= 0:
-        ctx.set_option(_lib.NKV_OPT_QUEUE_SPLIT, args.queue_split)
-    if args.queue_waves:
-        ctx.set_option(_lib.NKV_OPT_QUEUE_WAVES, args.queue_waves)
-    if args.queue_ring:
-        ctx.set_option(_lib.NKV_OPT_QUEUE_RING, args.queue_ring)
-    if args.records_fused >= 0:
-        ctx.set_option(_lib.NKV_OPT_RECORDS_FUSED, args.records_fused)
-    if args.no_bucket:
-        ctx.set_option(_lib.NKV_OPT_BUCKET, 0)
-    elif args.bucket >= 0:
-        ctx.set_option(_lib.NKV_OPT_BUCKET, args.bucket)
     roots = torch.empty(world * 20, dtype=torch.uint8, device="cuda")
     mixed = args.config == "mixed"
     one_tree = args.config == "one_tree"
     records = args.config in ("records", "records_verify")
     verify_crc = args.config == "records_verify"
-    if records:
-        import numpy as np
-        n, rb = args.leaves, args.value_bytes
-        ks = args.key_bytes
-        vlen = rb - 30 - ks  # record.go:191-199 header 30 B, 16-B key, the rest is the Value
-        stream_len = n * rb
-        data = torch.empty(stream_len, dtype=torch.uint8, device="cuda")
-        _lib.check(L.nkv_fill_splitmix64_dev(ctx.h, data.data_ptr(), stream_len, SEED + rank))
-        v = data.view(n, rb)
-        v[:, 14:22] = torch.from_numpy(np.frombuffer(np.uint64(ks).tobytes(), np.uint8).copy()).cuda()
-        v[:, 22:30] = torch.from_numpy(np.frombuffer(np.uint64(vlen).tobytes(), np.uint8).copy()).cuda()
-        d_roff = torch.arange(n, dtype=torch.int64, device="cuda") * rb
-        d_err = torch.zeros(1, dtype=torch.int32, device="cuda")
-        nbytes = n * vlen  # payload: the hashed Values
-        nodes = torch.empty(L.nkv_total_nodes(n) * 20, dtype=torch.uint8, device="cuda")
-        if verify_crc:  # store each record's right checksum (computed on the device once)
-            d_crc = torch.empty(n, dtype=torch.int32, device="cuda")
-            d_stats = torch.zeros(3, dtype=torch.int64, device="cuda")
-            _lib.check(L.nkv_record_crc_dev(ctx.h, data.data_ptr(), stream_len, d_roff.data_ptr(), n,
-                                            d_crc.data_ptr(), d_stats.data_ptr()))
-            v[:, 0:4] = d_crc.view(torch.uint8).view(n, 4)
+    tabs = build_tables(args, torch, _lib, L, ctx, rank, T)
+    t0_ = tabs[0]
+    n, vlen, nodes = t0_["n"], t0_["vlen"], t0_["nodes"]
+    nbytes = sum(t["nbytes"] for t in tabs)  # payload per step on this GPU
+    arr = (_lib.NkvTable * T)(*[t["table"] for t in tabs])
 
-            def tree():
-                _lib.check(L.nkv_tree_verify_records_dev(ctx.h, data.data_ptr(), stream_len, d_roff.data_ptr(), n,
-                                                         nodes.data_ptr(), None, d_stats.data_ptr()))
-        else:
-            def tree():
-                _lib.check(L.nkv_tree_from_records_dev(ctx.h, data.data_ptr(), stream_len, d_roff.data_ptr(), n,
-                                                       nodes.data_ptr(), d_err.data_ptr()))
-    elif not mixed:
-        n, vlen = args.leaves, args.value_bytes
-        nbytes = n * vlen
-        data = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
-        _lib.check(L.nkv_fill_splitmix64_dev(ctx.h, data.data_ptr(), nbytes, SEED + rank))
-        nodes = torch.empty(L.nkv_total_nodes(n) * 20, dtype=torch.uint8, device="cuda")
+    if one_tree:  # one tree over every rank's leaves (rank r holds leaves [r n, (r+1) n))
+        from nakevaleng_amd import sharded_tree
+        if n & (n - 1):
+            raise SystemExit("--config one_tree needs a power-of-two --leaves (ranges aligned to 2^k)")
+        ops = sharded_tree.DeviceOps(dev, ctx=ctx)
+        data = t0_["data"]
 
         def tree():
-            _lib.check(L.nkv_tree_from_strided_dev(ctx.h, data.data_ptr(), vlen, vlen, n, nodes.data_ptr()))
-
-        if one_tree:  # one tree over every rank's leaves (rank r holds leaves [r n, (r+1) n))
-            from nakevaleng_amd import sharded_tree
-            if n & (n - 1):
-                raise SystemExit("--config one_tree needs a power-of-two --leaves (ranges aligned to 2^k)")
-            ops = sharded_tree.DeviceOps(dev, ctx=ctx)
-
-            def tree():
-                nodes[-20:] = sharded_tree.sharded_root((data, vlen, vlen), n * world, ops=ops, host_root=False)
+            nodes[-20:] = sharded_tree.sharded_root((data, vlen, vlen), n * world, ops=ops, host_root=False)
+    elif T == 1:
+        tree = t0_["single"]
     else:
-        import numpy as np
-        lens_h, off_h = mixed_lengths(args.mixed_bytes, SEED_MIXED + rank)
-        n, vlen = len(lens_h), None
-        nbytes = int(lens_h.sum())
-        data = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
-        _lib.check(L.nkv_fill_splitmix64_dev(ctx.h, data.data_ptr(), nbytes, SEED_MIXED + rank))
-        d_off = torch.from_numpy(off_h.view(np.int64)).cuda()
-        d_len = torch.from_numpy(lens_h.view(np.int64)).cuda()
-        nodes = torch.empty(L.nkv_total_nodes(n) * 20, dtype=torch.uint8, device="cuda")
-
         def tree():
-            _lib.check(L.nkv_tree_from_values_dev(ctx.h, data.data_ptr(), d_off.data_ptr(), d_len.data_ptr(),
-                                                  n, nodes.data_ptr()))
+            _lib.check(L.nkv_trees_dev(ctx.h, arr, T), "nkv_trees_dev")
 
     # C1, the root gather.  Default (--gather batch):
     # every table's root is kept and all of them are all-gathered in one call
@@ -383,13 +551,16 @@ def main():
     if args.gather == "step":
         rg = RootGather(nodes, roots, gdist)
     else:
-        rg = BatchedRootGather(nodes, world, gdist, cap=max(args.steps, args.warmup, 8))
+        rg = BatchedRootGather(nodes, world, gdist, cap=T * max(args.steps, args.warmup, 8))
+    more = tuple(t["nodes"] for t in tabs[1:])
 
     def step():
         nonlocal nodes
         nodes = rg.begin()
+        if args.gather == "step":
+            t0_["nodes"] = nodes
         tree()
-        rg.end(nodes)
+        rg.end(nodes, more) if args.gather != "step" else rg.end(nodes)
 
     drain = rg.drain
 
@@ -404,7 +575,8 @@ def main():
     # for PREROLL_S.
     preroll_steps = preroll(step, drain, torch.cuda.synchronize, args.preroll_s, dist if use_dist else None,
                             lambda v: torch.tensor([v], dtype=torch.int32, device="cuda"))
-    if records and (int(d_err.item()) != 0 or (verify_crc and int(d_stats[2].item()) != 0)):
+    if records and any(int(t["d_err"].item()) != 0 or (verify_crc and int(t["d_stats"][2].item()) != 0)
+                       for t in tabs):
         # a malformed synthetic stream would time empty hashes
         raise SystemExit("bench.py: the record stream failed the header checks")
     for _ in range(args.warmup):
@@ -414,7 +586,7 @@ def main():
     if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
-    ctx.set_timing(not args.no_kernel_timing)
+    ctx.set_timing(not args.no_kernel_timing, clock=not args.no_clock)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -424,6 +596,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    sclk, clock_waves = ctx.clock() if not args.no_clock else (None, 0)
     calls, leaf_ms_tot, reduce_ms_tot = ctx.timing_summary()
     ctx.set_timing(False)
     if calls == 0:  # kernel split measured in a separate loop of the same steps
@@ -461,48 +634,29 @@ def main():
     if args.verify and rank == 0:
         import numpy as np
         from oracle import oracle_c as oc
-        if mixed:
-            host = oc.splitmix64_bytes(nbytes, SEED_MIXED)
-            want = oc.tree_from_digests(oc.leaf_hashes(host, off_h, lens_h, threads=16))
-        elif records:
-            host = data.cpu().numpy()
-            voff = np.arange(n, dtype=np.uint64) * rb + 30 + ks
-            want = oc.tree_from_digests(oc.leaf_hashes(host, voff, np.full(n, vlen, np.uint64), threads=16))
-            assert int(d_err.item()) == 0
+        if records:
+            assert all(int(t["d_err"].item()) == 0 for t in tabs)
             if verify_crc:
-                assert d_stats.cpu().tolist() == [0, -1, 0], d_stats.cpu().tolist()
-        else:
-            host = np.concatenate([oc.splitmix64_bytes(nbytes, SEED + r) for r in range(world if one_tree else 1)])
+                assert all(t["d_stats"].cpu().tolist() == [0, -1, 0] for t in tabs), "a stored Crc failed"
+        if one_tree:
+            host = np.concatenate([oc.splitmix64_bytes(n * vlen, SEED + r) for r in range(world)])
             want = oc.tree_from_digests(oc.leaf_hashes_strided(host, vlen, vlen, len(host) // vlen, threads=16))
-        verified = want[-1].tobytes().hex() == root
-        del host
+            verified = want[-1].tobytes().hex() == root
+            del host
+        else:
+            verified = all(t["want"]() == t["nodes"][-20:].cpu().numpy().tobytes().hex() for t in tabs)
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "sstable4k":
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config in ("sstable4k", "runs4"):
         cpu = cpu_baseline(min(args.cpu_sample_leaves, n), vlen)
 
     if rank == 0:
         total_bytes = nbytes * world * args.steps
         value = total_bytes / elapsed / 2**30
-        achieved = nbytes / (leaf_ms * 1e-3) / 1e9  # algorithmic payload bytes per K1 launch
-        valu_ceiling = SHA1_VALU_CEILING_GBS * (VERIFY_VALU_RATIO if verify_crc else 1.0)
-        traffic, traffic_bounds = None, None
-        # PMC-measured HBM bytes of this config's leaf kernel (separate rocprofv3
-        # passes: tools/pmc_sizes.sh for cfg2, tools/pmc_config.sh for the others)
-        # cfg2: the default 128-byte register runs (LOAD 4) or the LDS-DMA stage (--leaf-load 1)
-        cfg2_pmc = {0: "pmc_traffic_cfg2_runs.json", 4: "pmc_traffic_cfg2_runs.json",
-                    1: "pmc_traffic.json"}.get(args.leaf_load)
-        pmc_name = {"sstable4k": cfg2_pmc, "records": "pmc_traffic_records.json",
-                    "mixed": "pmc_traffic_mixed.json", "records_verify": "pmc_traffic_records_verify.json"}.get(args.config)
-        pmc_path = os.path.join(ROOT, "profiles", pmc_name) if pmc_name else None
-        if pmc_path and os.path.exists(pmc_path):
-            with open(pmc_path) as f:
-                pmc = json.load(f)
-            same = pmc.get("leaves") == n and (pmc.get("value_bytes") in (None, vlen)) and \
-                pmc.get("algorithmic_bytes_per_launch") in (None, nbytes)
-            if same:
-                traffic = pmc.get("hbm_bytes_per_launch")
-                traffic_bounds = pmc.get("hbm_read_bytes_bounds_per_launch")
+        table_bytes = t0_["nbytes"]
+        achieved = table_bytes / (leaf_ms * 1e-3) / 1e9  # algorithmic payload bytes per K1 launch
+        ceiling = valu_ceiling(sclk, verify_crc)
+        traffic, traffic_bounds = pmc_traffic(args, n, vlen, table_bytes)
         out = {
             "metric": "GiB/s Merkle leaf-hash + tree-reduce over device-resident record blocks",
             "value": round(value, 2),
@@ -516,43 +670,23 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u32",
-            "data": f"synthetic: splitmix64 bytes (seed {SEED_MIXED if mixed else SEED:#x} + rank) generated in HBM",
+            "data": f"synthetic: splitmix64 bytes (seed {SEED_MIXED if mixed else SEED:#x} + rank"
+                    + (f" + {TABLE_SEED_STEP} t for table t" if T > 1 else "") + ") generated in HBM",
             "config": {
-                "workload": ("BASELINE configs[2]: mixed 64 B - 64 KiB log-uniform values packed back to back, "
-                             + ("input order" if args.no_bucket else "length-bucketed")) if mixed else
-                            (f"compaction form: {n} serialized {rb}-B records ({ks}-B key, {vlen}-B value) in a "
-                             "Data table in HBM; values located from the headers and hashed in place, full tree"
-                             + ("; every record's Crc (Key ++ Value) checked in the same pass" if verify_crc else ""))
-                            if records else
-                            (f"one tree over {world} GPU(s): {n} x {vlen} B values per rank, each rank builds the "
-                             "levels of its aligned leaf range, sub-roots all-gathered, top levels on every rank")
-                            if one_tree else
-                            ("BASELINE configs[1]: single SSTable flush, 1 Mi x 4 KiB values, "
-                             if (n, vlen) == (1 << 20, 4096) else
-                             "BASELINE configs[4] per-GPU table (8 Mi x 4 KiB values), "
-                             if (n, vlen) == (8 << 20, 4096) else
-                             f"single SSTable flush, {n} x {vlen} B values, ")
-                            + "leaf SHA-1 + full tree reduce (one table per GPU; roots all-gathered over RCCL when N>1)",
-                "leaves_per_gpu": n,
-                "value_bytes": vlen if not mixed else "64..65536 (mean %.0f)" % (nbytes / n),
+                "workload": workload_text(args, n, vlen, table_bytes, world, T, t0_.get("rb"), t0_.get("ks")),
+                "leaves_per_gpu": n * T,
+                "tables_per_gpu": T,
+                "value_bytes": vlen if not mixed else "64..65536 (mean %.0f)" % (table_bytes / n),
                 "parallelism": (f"1 tree split over {world} ranks" + (" + RCCL all_gather of sub-roots" if world > 1 else ""))
                                if one_tree else
-                               f"{world} independent tables" + ((" + RCCL all_gather of roots, "
-                                                                 + ("one call per timed loop" if args.gather == "batch"
-                                                                    else "one per table")) if world > 1 else ""),
+                               f"{world * T} independent tables" + ((" + RCCL all_gather of roots, "
+                                                                     + ("one call per timed loop" if args.gather == "batch"
+                                                                        else "one per table")) if world > 1 else ""),
             },
+            "sclk_mhz": round(sclk, 1) if sclk else None,
             "roofline": {
                 "bound": "hbm",
-                "kernel": ("leaf phase: length sort + ragged leaf SHA-1 (%s)" % LEAF_KERNEL.get(args.deep, "default"))
-                          if mixed else
-                          ("leaf phase: k_leaf_verify (header parse + record CRC + leaf SHA-1 from whole 128-byte lines in registers, input order)"
-                           if verify_crc else
-                           ("leaf phase: k_locate + k_leaf<offsets, aligned-segment stage> (input order)"
-                            if args.records_fused == 0 else
-                            "leaf phase: k_leaf_records (header parse + whole 128-byte lines into registers, input order)")) if records else
-                          ("k_leaf<strided, LDS-DMA stage> (leaf SHA-1, level 0)" if args.leaf_load == 1 else
-                           "k_leaf<strided, 128-byte register runs> (leaf SHA-1, level 0)" if args.leaf_load in (0, 4)
-                           else f"k_leaf<strided, load path {args.leaf_load}> (leaf SHA-1, level 0)"),
+                "kernel": kernel_text(args, T),
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -562,11 +696,17 @@ def main():
                 "step_frac": round(nbytes / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
                 "traffic_bounds": traffic_bounds,  # RDREQ x 64 .. x 128 B (profiles/pmc_traffic.json)
-                "valu_ceiling": round(valu_ceiling, 1),
-                "valu_frac": round(achieved / valu_ceiling, 4),
+                # VALU-issue ceiling at the measured clock (sclk_mhz) and the
+                # fraction of it the leaf kernel reached
+                "valu_ceiling": round(ceiling, 1) if ceiling else SHA1_VALU_CEILING_GBS,
+                "valu_ceiling_basis": (f"{SIMDS} SIMDs x {sclk:.0f} MHz / ({VALU_PER_WAVE_BLOCK['verify' if verify_crc else 'leaf']}"
+                                       f" VALU per wave-block x {VALU_CYCLES:g} cycles) x 4096 B") if ceiling else
+                                      "tools/sha1_rate.hip at 2.37 GHz (no clock reading)",
+                "valu_frac": round(achieved / (ceiling or SHA1_VALU_CEILING_GBS), 4),
             },
             "kernel_ms": {"leaf": round(leaf_ms, 4), "tree_reduce": round(reduce_ms, 4),
                           "bfs_image": round(bfs_ms, 4)},
+            "clock_probe_waves": clock_waves,
             "root": root,
             "cpu_baseline": cpu,
         }
@@ -579,6 +719,209 @@ def main():
     if use_dist:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def main_api_flush(args):
+    """--config api_flush: the Merkle step of one memtable flush as the unchanged
+    caller runs it (sstable.makeMetadata, core/sstable/sstable.go:58-74), through
+    the C++ mirror of the Go API: NewLeaf per value from host memory into the
+    pinned arena (the settled 32 MiB chunks streamed to HBM during the loop),
+    New (the device call + the pointer tree), Root.String(), Serialize to a fresh
+    file.  Runs tools/api_flush.cpp with streaming on, then off; the first cycle
+    of each allocates the arena, the steady state is the best later cycle."""
+    import subprocess
+    import tempfile
+    from nakevaleng_amd import build as nb
+    exe = nb.build_api_flush()
+    n, vlen = args.leaves, args.value_bytes
+    runs = {}
+    with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
+        for mode in (1, 0):
+            out = subprocess.run([exe, str(n), str(vlen), str(max(2, args.api_cycles)), td, str(mode), hex(SEED)],
+                                 capture_output=True, text=True, timeout=900)
+            if out.returncode != 0:
+                raise SystemExit(f"api_flush failed: {out.stderr[-2000:]}")
+            runs[mode] = [json.loads(x) for x in out.stdout.splitlines() if x.startswith("{")]
+    best = {m: max(r[1:], key=lambda c: c["gib_s"]) for m, r in runs.items()}
+    root = best[1]["root"]
+    verified = None
+    if args.verify:
+        from oracle import oracle_c as oc
+        host = oc.splitmix64_bytes(n * vlen, SEED)
+        want = oc.tree_from_digests(oc.leaf_hashes_strided(host, vlen, vlen, n, threads=16))[-1].tobytes().hex()
+        verified = all(c["root"] == want for r in runs.values() for c in r)
+    b, nb0 = best[1], best[0]
+    out = {
+        "metric": "GiB/s host-inclusive Merkle step of one SSTable flush through the Go-API mirror "
+                  "(NewLeaf x n from host memory, New, Root, Serialize)",
+        "value": b["gib_s"],
+        "unit": "GiB/s",
+        "n_gpus": 1,
+        "steps": len(runs[1]),
+        "higher_is_better": True,
+        "dtype": "u32",
+        "data": f"synthetic: splitmix64 bytes (seed {SEED:#x}) in host memory (the memtable's values)",
+        "config": {"workload": f"memtable flush: {n} x {vlen} B values, sstable.go:58-74 call sequence",
+                   "leaves": n, "value_bytes": vlen},
+        "breakdown_ms": {k: b[k] for k in ("newleaf_ms", "new_call_ms", "upload_ms", "kernels_ms", "download_ms",
+                                           "materialize_ms", "root_ms", "walk_ms", "write_ms", "total_ms")},
+        "streaming_off": {"gib_s": nb0["gib_s"], "total_ms": nb0["total_ms"], "newleaf_ms": nb0["newleaf_ms"],
+                          "new_call_ms": nb0["new_call_ms"], "upload_ms": nb0["upload_ms"],
+                          # the whole payload in one DMA straight from the pinned arena
+                          "dma_gbps": round(n * vlen / (nb0["upload_ms"] * 1e-3) / 1e9, 2)
+                          if nb0["upload_ms"] > 0 else None},
+        "cycles": runs,
+        "root": root,
+    }
+    if verified is not None:
+        out["verified_vs_oracle"] = verified
+    print(json.dumps(out), flush=True)
+
+
+def main_capi(args, T):
+    """--backend capi: ONE process drives every GPU through the library's group
+    (SURVEY.md 8e process model: nkv_group_create = a context per GPU +
+    ncclCommInitAll).  A step builds T tables per GPU (nkv_group_trees_dev:
+    table t on member t % N, the tables of a member over its streams) and
+    all-gathers every root over RCCL inside the library; one_tree builds one
+    tree split over the GPUs (nkv_group_tree_dev).  Inputs are resident in each
+    GPU's HBM before timing starts; the timed region ends with every member
+    synchronized."""
+    if os.environ.get("WORLD_SIZE", "1") != "1":
+        raise SystemExit("bench.py: --backend capi is one process for all GPUs (no launcher)")
+    import numpy as np
+    import torch
+    from nakevaleng_amd import build as nb
+    nb.build()
+    from nakevaleng_amd import _lib
+    L = _lib.lib()
+    N = args.gpus
+    if torch.cuda.device_count() < N:
+        raise SystemExit(f"bench.py: --gpus {N} but {torch.cuda.device_count()} device(s) visible")
+    grp = _lib.Group(list(range(N)))
+    ctxs = []
+    for m in range(N):
+        c = grp.ctx(m)  # the member's context (owned by the group)
+        set_options(args, _lib, c)
+        ctxs.append(c)
+    one_tree = args.config == "one_tree"
+    per = []  # per member: its tables
+    for m in range(N):
+        with torch.cuda.device(m):
+            # inputs are written on torch's stream (fills through the member's
+            # context on that stream too); the member's own stream then waits
+            # for them (nkv_ctx_use_own_stream orders the hand-over)
+            ctxs[m].set_stream(torch.cuda.current_stream(m).cuda_stream)
+            per.append(build_tables(args, torch, _lib, L, ctxs[m], m, T, device=f"cuda:{m}"))
+            ctxs[m].set_stream(_lib._OWN)
+    for m in range(N):
+        torch.cuda.synchronize(m)
+        _lib.check(L.nkv_ctx_sync(ctxs[m].h))
+    n, vlen = per[0][0]["n"], per[0][0]["vlen"]
+    nbytes = sum(t["nbytes"] for tabs in per for t in tabs)  # payload per step, all GPUs
+    if one_tree:
+        if n & (n - 1):
+            raise SystemExit("--config one_tree needs a power-of-two --leaves (ranges aligned to 2^k)")
+        parts = (_lib.NkvTable * N)(*[per[m][0]["table"] for m in range(N)])
+        d_root = torch.zeros(20, dtype=torch.uint8, device="cuda:0")
+
+        def step():
+            _lib.check(L.nkv_group_tree_dev(grp.h, parts, n * N, d_root.data_ptr(), None), "nkv_group_tree_dev")
+    else:
+        order = [per[t % N][t // N] for t in range(N * T)]  # table t on member t % N
+        arr = (_lib.NkvTable * (N * T))(*[t["table"] for t in order])
+
+        def step():
+            _lib.check(L.nkv_group_trees_dev(grp.h, arr, N * T, None), "nkv_group_trees_dev")
+
+    t_pre, preroll_steps = time.perf_counter(), 0
+    while preroll_steps < 8 or time.perf_counter() - t_pre < args.preroll_s:
+        step()
+        preroll_steps += 1
+        if preroll_steps % 8 == 0:
+            grp.sync()
+    for _ in range(args.warmup):
+        step()
+    grp.sync()
+    ctxs[0].set_timing(not args.no_kernel_timing, clock=not args.no_clock)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    grp.sync()
+    elapsed = time.perf_counter() - t0
+    sclk, clock_waves = ctxs[0].clock() if not args.no_clock else (None, 0)
+    calls, leaf_ms_tot, _ = ctxs[0].timing_summary()
+    ctxs[0].set_timing(False)
+    # the gathered roots of the last step, checked against each table's own nodes
+    if one_tree:
+        root = d_root.cpu().numpy().tobytes().hex()
+        gathered_ok = None
+    else:
+        roots = np.zeros(20 * N * T, np.uint8)
+        _lib.check(L.nkv_group_trees_dev(grp.h, arr, N * T, _lib.p8(roots)))
+        gathered_ok = all(roots[20 * t:20 * t + 20].tobytes() == order[t]["nodes"][-20:].cpu().numpy().tobytes()
+                          for t in range(N * T))
+        root = per[0][0]["nodes"][-20:].cpu().numpy().tobytes().hex()
+    verified = None
+    if args.verify:
+        if one_tree:
+            from oracle import oracle_c as oc
+            host = np.concatenate([oc.splitmix64_bytes(n * vlen, SEED + r) for r in range(N)])
+            verified = oc.tree_from_digests(oc.leaf_hashes_strided(host, vlen, vlen, n * N,
+                                                                   threads=16))[-1].tobytes().hex() == root
+        else:
+            verified = all(t["want"]() == t["nodes"][-20:].cpu().numpy().tobytes().hex() for t in order)
+    leaf_ms = leaf_ms_tot / max(calls, 1)
+    table_bytes = per[0][0]["nbytes"]
+    achieved = table_bytes / (leaf_ms * 1e-3) / 1e9 if calls else None
+    ceiling = valu_ceiling(sclk, args.config == "records_verify")
+    out = {
+        "metric": "GiB/s Merkle leaf-hash + tree-reduce over device-resident record blocks",
+        "value": round(nbytes * args.steps / elapsed / 2**30, 2),
+        "unit": "GiB/s",
+        "n_gpus": N,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "preroll_steps": preroll_steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": f"synthetic: splitmix64 bytes generated in each GPU's HBM",
+        "backend": f"capi group: one process, {N} context(s), transport "
+                   + ("RCCL" if grp.transport == _lib.NKV_TRANSPORT_RCCL else "copy"),
+        "config": {
+            "workload": workload_text(args, n, vlen, table_bytes, N, T, per[0][0].get("rb"), per[0][0].get("ks")),
+            "leaves_per_gpu": n * T,
+            "tables_per_gpu": T,
+            "value_bytes": vlen,
+            "parallelism": (f"1 tree split over {N} GPU(s), sub-roots all-gathered by the library" if one_tree else
+                            f"{N * T} independent tables, every root all-gathered by the library each step"),
+        },
+        "sclk_mhz": round(sclk, 1) if sclk else None,
+        "roofline": {
+            "bound": "hbm",
+            "kernel": kernel_text(args, T) + " (member 0)",
+            "achieved": round(achieved, 1) if achieved else None,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+            "step_frac": round(nbytes / N / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 4),
+            "valu_ceiling": round(ceiling, 1) if ceiling else None,
+            "valu_frac": round(achieved / ceiling, 4) if (ceiling and achieved) else None,
+        },
+        "kernel_ms": {"leaf": round(leaf_ms, 4)},
+        "clock_probe_waves": clock_waves,
+        "root": root,
+        "cpu_baseline": None,
+    }
+    if gathered_ok is not None:
+        out["root_gather_ok"] = gathered_ok
+    if verified is not None:
+        out["verified_vs_oracle"] = verified
+    print(json.dumps(out), flush=True)
+    grp.close()
 
 
 if __name__ == "__main__":

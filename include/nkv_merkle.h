@@ -19,8 +19,10 @@
  *   MakeTableSecondaries    core/sstable/sstable.go:35-47       nkv_tree_from_values /
  *     (Merkle part) + lsmtree.merge leaf collection               nkv_tree_from_records[_dev]
  *                           core/lsmtree/lsmtree.go:146,211
- *   (*MerkleTree).Validate  ds/merkletree/merkletree.go:162-171 nkv_tree_build / nkv_tree_generic
- *                           ds/merkletree/merklenode.go:99-108    + 20-byte root compare
+ *   (*MerkleTree).Validate  ds/merkletree/merkletree.go:162-171 nkv_tree_validate (device rebuild
+ *                           ds/merkletree/merklenode.go:99-108    + 20-byte root compare)
+ *   compaction over GPUs    core/lsmtree/lsmtree.go:71-128,211  nkv_group_* (one process, one
+ *                core/sstable/sstable.go:35-47       context per GPU, RCCL)
  *   record value location   core/record/record.go:191-199       nkv_locate_values_dev
  *   bloomfilter.New sizing  ds/bloomfilter/bloomfilter.go:18-24 nkv_bloom_params
  *   makeFilter / Insert     core/sstable/sstable.go:49-56,      nkv_bloom_build /
@@ -92,34 +94,26 @@ int nkv_ctx_set_stream(nkv_ctx *ctx, void *hip_stream);
 int nkv_ctx_use_own_stream(nkv_ctx *ctx);
 int nkv_ctx_sync(nkv_ctx *ctx);
 /* Tuning knobs (defaults are the measured-best settings). */
-#define NKV_OPT_LEAF_LOAD 1 /* leaf-kernel load path for 16-byte aligned values:
-                               1 = LDS-DMA stage, 2 = direct loads, 3 = direct non-temporal,
-                               4 (the default) / 5 = direct loads in 128 / 256-byte runs
-                               per lane (1 and 4 take 11 for unaligned values),
-                               9 / 10 = line-pair / 80-byte-window LDS-DMA stage for values
-                               that are not 64-byte aligned (waves of equal full-block
-                               counts; other waves as 1); 11 (the default for values that
-                               are not 16-byte aligned) = waves whose values share one
-                               offset mod 64 stream aligned 64-byte segments (LDS-DMA,
-                               or register loads when block counts differ) and shift
-                               them in registers, other waves as 10; 12 = 128-byte runs
-                               into registers from each value's own (any) address */
+#define NKV_OPT_LEAF_LOAD 1 /* leaf-kernel load path: 4 (default) = 16-byte aligned values in
+                               128-byte runs straight into registers, others as 11; 11 =
+                               every value through the staged paths: the segment stage
+                               when a wave's values share their offset mod 64, the
+                               80-byte window stage when their full-block counts are
+                               equal, else the value-relative LDS-DMA stream.  (The
+                               load paths that lost their A/Bs in rounds 1-2 are gone.) */
 #define NKV_OPT_BUCKET 2    /* ragged values (nkv_tree_from_values*, nkv_tree_from_records*):
                                1 = hash in length-sorted order (work queue); 0 = in input
                                order; 2 (default) = auto: input order when the full-block
                                counts of a batch of >= 4096 values lie within max(1, min/16)
                                of each other, else sorted (decided on the device, no
                                read-back) */
-#define NKV_OPT_DEEP_PREFETCH 3 /* length-sorted ragged batches: 0 = one block of
-                                   lookahead; 1 = several blocks; 2 = several blocks in a
-                                   work-queue kernel that spreads the longest chains one
-                                   per SIMD; 3 (default) = the work-queue kernel with
-                                   values staged as aligned 64-B chunks through an LDS
-                                   ring */
+#define NKV_OPT_DEEP_PREFETCH 3 /* kept for ABI stability: 3 (the work-queue kernel) is the
+                                   only value accepted */
 #define NKV_OPT_QUEUE_SPLIT 4 /* work-queue kernel: groups whose longest value has at most
                                  this many 64-B blocks may go to the non-priority waves
                                  when the longest value bounds the batch (default 32) */
-#define NKV_OPT_QUEUE_WAVES 5 /* work-queue kernel (LDS ring): waves per SIMD, 1..5 (default 4) */
+#define NKV_OPT_QUEUE_WAVES 5 /* work-queue kernel: waves per SIMD, 1..3 (default 3: its
+                                 3-slot, 12 KiB LDS ring per wave) */
 #define NKV_OPT_CRC_LOAD 6    /* record checksums: bit 0 = spans staged as aligned 64-B
                                  chunks through an LDS ring (else per-lane loads); bits
                                  1-2 = LDS table copies x workgroup: 0 = 8 x 256,
@@ -136,20 +130,32 @@ int nkv_ctx_sync(nkv_ctx *ctx);
                                   staged), then set them in LDS, one workgroup per range; 1 = the
                                   same grouping by a global counting sort (hashes twice); 0 = one
                                   device atomicOr per bit */
-#define NKV_OPT_QUEUE_RING 9   /* work-queue kernel: LDS ring of aligned chunks with 2 slots
-                                  (one block of DMA lookahead), 3 / 4 = pipelined ring
-                                  with 1 / 2 blocks of lookahead; 12 / 13 / 14 = pipelined
-                                  ring of value-relative chunks (no funnel) with 2 / 3 / 4
-                                  slots (default 13).  3 and 13 allow 3 waves per SIMD, 4
-                                  and 14 two */
+#define NKV_OPT_QUEUE_RING 9   /* kept for ABI stability: 13 (the pipelined 3-slot ring of
+                                  value-relative chunks) is the only value accepted */
 #define NKV_OPT_RECORDS_FUSED 11 /* records form (nkv_tree_from_records*): 1 (default) = one
                                     launch locates each value from its header and hashes it
                                     (k_leaf_records); 0 = a separate locate pass first */
+#define NKV_OPT_TABLE_LANES 12 /* nkv_trees_dev: streams the tables of one call are spread
+                                  over (1..8, default 2), so one table's leaf kernel runs
+                                  while the previous one finishes and reduces */
 int nkv_ctx_set_option(nkv_ctx *ctx, int key, int64_t value);
-/* When enabled, the device-resident tree calls record HIP events around the
- * leaf kernel and the tree reduce on the context's stream. */
-int nkv_ctx_set_timing(nkv_ctx *ctx, int enable);
+/* Timing (nkv_ctx_set_timing flags).  NKV_TIMING_EVENTS: the tree calls record
+ * HIP events around the leaf kernel and the tree reduce on the context's
+ * stream (and, for nkv_tree_from_values, around the upload and the download).
+ * NKV_TIMING_CLOCK: every wave of the leaf kernels on the context's device
+ * adds its lifetime in shader-clock cycles and in 100 MHz ticks to a
+ * counter the context owns (nkv_ctx_clock); one context per device at a
+ * time.  0 switches both off. */
+#define NKV_TIMING_EVENTS 1
+#define NKV_TIMING_CLOCK 2
+int nkv_ctx_set_timing(nkv_ctx *ctx, int flags);
 int nkv_ctx_last_timing(nkv_ctx *ctx, float *leaf_ms, float *reduce_ms);
+/* the latest nkv_tree_from_values under NKV_TIMING_EVENTS: upload (host values ->
+ * HBM), kernels (leaf + tree), download (outputs -> host) */
+int nkv_ctx_last_host_timing(nkv_ctx *ctx, float *upload_ms, float *kernels_ms, float *download_ms);
+/* NKV_TIMING_CLOCK: the lifetime-weighted mean shader clock of the leaf-kernel
+ * waves since the flag was set, and how many waves reported (synchronizes). */
+int nkv_ctx_clock(nkv_ctx *ctx, double *mhz, uint64_t *waves);
 /* Sum over every tree call since timing was (re-)enabled: synchronizes on the
  * last call's events only, so a timed loop is not perturbed. */
 int nkv_ctx_timing_summary(nkv_ctx *ctx, int *calls, float *leaf_ms_total, float *reduce_ms_total);
@@ -161,9 +167,20 @@ uint64_t nkv_level_start(uint64_t n, int level);
 uint64_t nkv_total_nodes(uint64_t n);
 uint64_t nkv_bfs_size(uint64_t n); /* Serialize() bytes for 20-byte leaves */
 
-/* ---- pinned host arena (for the deferred-NewLeaf shim) ---- */
+/* ---- pinned host arena (for the deferred-NewLeaf shim) ----
+ * A block from nkv_host_alloc belongs to the context.  Host-buffer calls on the
+ * same context whose values all lie inside one block copy them to the device
+ * in one DMA straight from the block (no staging gather), values keeping their
+ * places (16-byte aligned places take the aligned kernel path).
+ * nkv_host_stream(block, upto): bytes [0, upto) of the block are final for the
+ * current batch; their copy to the device starts now, asynchronously, so it
+ * overlaps the caller's NewLeaf loop; the next call over the block moves only
+ * the rest.  Those bytes must not change until that call returns.  A call over
+ * the block ends the batch; an upto below the previous one starts a new batch.
+ * nkv_host_free waits for copies from the block. */
 int nkv_host_alloc(nkv_ctx *ctx, uint64_t bytes, void **out);
 int nkv_host_free(nkv_ctx *ctx, void *p);
+int nkv_host_stream(nkv_ctx *ctx, const void *block, uint64_t upto);
 
 /* ---- host-buffer API (synchronous) ---- */
 
@@ -309,6 +326,102 @@ int nkv_bloom_query_dev(nkv_ctx *ctx, const void *d_keys, const uint64_t *d_off,
                         const void *d_bits, uint8_t *d_out);
 /* synthetic input: byte j = byte (j % 8) of splitmix64(seed, j / 8) */
 int nkv_fill_splitmix64_dev(nkv_ctx *ctx, void *d_buf, uint64_t nbytes, uint64_t seed);
+
+/* ---- several tables per call (compaction's runs, consecutive flushes) ----
+ * One table of device-resident leaves, described for nkv_trees_dev /
+ * nkv_group_trees_dev (all pointers on the device that builds it). */
+typedef enum nkv_table_kind {
+    NKV_TABLE_STRIDED = 0, /* value i = base + i * stride, len bytes (nkv_tree_from_strided_dev) */
+    NKV_TABLE_VALUES = 1,  /* value i = base + off[i], lens[i] bytes (nkv_tree_from_values_dev) */
+    NKV_TABLE_RECORDS = 2, /* Data table: base = stream of base_len bytes, off = record offsets
+                              (nkv_tree_from_records_dev; err nullable) */
+    NKV_TABLE_VERIFY = 3   /* as RECORDS plus every record's Crc checked
+                              (nkv_tree_verify_records_dev; crc, stats nullable) */
+} nkv_table_kind;
+typedef struct nkv_table {
+    int kind;
+    const void *base;
+    uint64_t base_len;
+    uint64_t stride, len;
+    const uint64_t *off;
+    const uint64_t *lens;
+    uint64_t n;
+    void *nodes; /* nkv_total_nodes(n) * 20 bytes */
+    uint32_t *err;
+    uint32_t *crc;
+    uint64_t *stats;
+} nkv_table;
+/* The trees of k independent tables, asynchronous on the context's stream:
+ * the tables are spread over NKV_OPT_TABLE_LANES streams of the context's
+ * device (table t on lane t % lanes, forked from and joined back to the
+ * context's stream), so one table's leaf kernel overlaps the tail and the tree
+ * reduce of the one before.  Each table's results are those of its single-table
+ * call.  A RECORDS table with err NULL: the call synchronizes and returns
+ * NKV_ERR_INVALID if any of those tables has a header outside its stream. */
+int nkv_trees_dev(nkv_ctx *ctx, const nkv_table *tables, int k);
+
+/* ---- multi-GPU: one host process, one context per GPU ----
+ * A group is one context per listed device and one RCCL communicator over
+ * them (ncclCommInitAll).  Tables shard with no data-path exchange; the only
+ * collective is the all-gather of 20-byte roots (an RCCL group call over the
+ * members' streams).  Listing a device twice is allowed (several streams on
+ * one GPU, e.g. to rehearse the split on one card): RCCL cannot join one
+ * device twice, so such a group gathers by device-to-device copies instead
+ * (nkv_group_transport). */
+typedef struct nkv_group nkv_group;
+#define NKV_TRANSPORT_RCCL 1
+#define NKV_TRANSPORT_COPY 2
+int nkv_group_create(const int *devices, int g, nkv_group **out);
+void nkv_group_destroy(nkv_group *grp);
+int nkv_group_size(const nkv_group *grp);
+int nkv_group_transport(const nkv_group *grp);
+/* member i's context (owned by the group): options, streams, *_dev calls */
+int nkv_group_ctx(nkv_group *grp, int i, nkv_ctx **out);
+int nkv_group_sync(nkv_group *grp);
+/* d_roots[i]: 20 bytes on member i.  All-gather them: d_out[i] (nullable
+ * array, or entries) receives the g * 20 bytes on member i; roots_out
+ * (nullable host buffer, g * 20 bytes) a copy (then the call synchronizes,
+ * else it is asynchronous on the members' streams). */
+int nkv_group_roots_allgather(nkv_group *grp, const void *const *d_roots, void *const *d_out,
+                              uint8_t *roots_out);
+/* Compaction over GPUs (lsmtree.go:71-128 merges runs; one output table per
+ * GPU): table t is built on member t % g (its pointers live on that device,
+ * nkv_trees_dev there), then every table's root is all-gathered so every member
+ * holds all k roots in table order.  roots_out (host, k * 20 bytes, nullable):
+ * then the call synchronizes; else asynchronous on the members' streams. */
+int nkv_group_trees_dev(nkv_group *grp, const nkv_table *tables, int k, uint8_t *roots_out);
+/* The same from host memory (cgo: what MakeTableSecondaries holds after a
+ * merge): table t = values base[t] + off[t][i], len[t][i], on member t % g, one
+ * host thread per member; outputs as nkv_tree_from_values (each nullable). */
+typedef struct nkv_values {
+    const uint8_t *base;
+    const uint64_t *off;
+    const uint64_t *len;
+    uint64_t n;
+    uint8_t *root20;
+    uint8_t *nodes_out;
+    uint8_t *img_out;
+} nkv_values;
+int nkv_group_trees_from_values(nkv_group *grp, const nkv_values *tables, int k);
+/* One table over the group (a single compaction's output table, lsmtree.go:106-110):
+ * padding only happens at a level's end (merkletree.go:32-34), so the tree splits
+ * at 2^k-aligned leaf ranges: member r builds levels 0..k of leaves
+ * [r * span, min(n, (r + 1) * span)), span = nkv_split_span(n, g) = 2^k, k =
+ * max(1, ceil(log2(ceil(n / g)))); a partial last range re-hashes its lone top node
+ * up to level k; the level-k nodes are all-gathered and the top levels reduced on
+ * every member.  Outputs as nkv_tree_from_values (each nullable; all host). */
+uint64_t nkv_split_span(uint64_t n, int g);
+int nkv_group_tree_from_values(nkv_group *grp, const uint8_t *base, const uint64_t *off, const uint64_t *len,
+                               uint64_t n, uint8_t *root20, uint8_t *nodes_out, uint8_t *img_out);
+/* The same over device-resident ranges: parts[r] describes member r's leaf range
+ * (a STRIDED or VALUES table on member r's device, n = its range's length, 0 for
+ * members past the last range; nodes ignored: the group keeps the levels).
+ * d_root (nullable): 20 bytes on member 0 that receive the root; root20 (host,
+ * nullable): then the call synchronizes, else it is asynchronous.
+ * nkv_group_tree_fetch then copies the latest such tree's nodes (level-major,
+ * nkv_total_nodes(n) * 20 bytes) and/or its Serialize image to the host. */
+int nkv_group_tree_dev(nkv_group *grp, const nkv_table *parts, uint64_t n, void *d_root, uint8_t *root20);
+int nkv_group_tree_fetch(nkv_group *grp, uint8_t *nodes_out, uint8_t *img_out);
 
 #ifdef __cplusplus
 }

@@ -16,18 +16,24 @@
 //   MerkleTree::Serialize           merkletree.go:67-92  (O_WRONLY|O_CREAT, no O_TRUNC)
 //   MerkleTree::Deserialize         merkletree.go:97-157 (root only, as the reference)
 //   MerkleTree::Validate            merkletree.go:162-171 + merklenode.go:99-108
+//   CompactRoots                    lsmtree.go:71-128,211 + sstable.go:35-47: the Merkle
+//                                   step of several output tables, one thread per GPU
 //
 // Errors the reference panics on are thrown as std::runtime_error.  There is
 // no CPU hashing path: without a HIP device every hashing call throws.
 #pragma once
 
+#include <array>
+#include <chrono>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
 #include <deque>
+#include <exception>
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -71,20 +77,34 @@ class Session {
         bool resolved = false;
     };
 
-    // Copies `data` into the arena; returns (batch, index).
+    // Copies `data` into the arena at a 16-byte aligned place (the leaf
+    // kernel's aligned path reads the values where they lie: the library
+    // copies the arena to the device in one DMA, nkv_merkle.h); returns
+    // (batch, index).  Every settled kStreamChunk of the arena starts its
+    // device copy at once (nkv_host_stream), so the copy overlaps the rest of
+    // the NewLeaf loop.
+    static constexpr uint64_t kStreamChunk = uint64_t(32) << 20;
     std::pair<std::shared_ptr<Batch>, uint64_t> AddLeaf(const uint8_t* data, size_t n) {
         if (!batch_ || batch_->resolved) {
             batch_ = std::make_shared<Batch>();
             batch_->epoch = ++epoch_;
             used_ = 0;
+            streamed_ = 0;
         }
-        Reserve(used_ + n);
-        if (n) std::memcpy(static_cast<uint8_t*>(arena_) + used_, data, n);
-        batch_->off.push_back(used_);
+        const uint64_t at = (used_ + 15) & ~uint64_t(15);
+        Reserve(at + n);
+        if (n) std::memcpy(static_cast<uint8_t*>(arena_) + at, data, n);
+        batch_->off.push_back(at);
         batch_->len.push_back(n);
-        used_ += n;
+        used_ = at + n;
+        if (stream_ && used_ >= streamed_ + kStreamChunk) {
+            streamed_ = used_ - used_ % kStreamChunk;
+            check(nkv_host_stream(ctx_, arena_, streamed_), "nkv_host_stream");
+        }
         return {batch_, batch_->off.size() - 1};
     }
+    // NewLeaf streams settled arena chunks ahead of New (default on)
+    void SetStreaming(bool on) { stream_ = on; }
 
     const uint8_t* arena() const { return static_cast<const uint8_t*>(arena_); }
     // nkv_host_alloc calls so far: a sealed batch's arena is reused by the next
@@ -113,11 +133,13 @@ class Session {
         }
         arena_ = p;
         cap_ = want;
+        streamed_ = 0;  // a new block: its device copy starts from byte 0
     }
 
     nkv_ctx* ctx_ = nullptr;
     void* arena_ = nullptr;
-    uint64_t cap_ = 0, used_ = 0, epoch_ = 0, allocs_ = 0;
+    uint64_t cap_ = 0, used_ = 0, epoch_ = 0, allocs_ = 0, streamed_ = 0;
+    bool stream_ = true;
     std::shared_ptr<Batch> batch_;
 };
 
@@ -277,6 +299,13 @@ class MerkleTree {  // merkletree.go:13-15
     // every digest, level-major bottom-up (as the C-ABI returns it)
     const std::vector<uint8_t>& Levels() const { return levels_; }
 
+    // where New's time went (bench.py --config api_flush): the device call
+    // (values to HBM, kernels, digests back) and the pointer-tree materialization
+    struct NewTiming {
+        double call_ms = 0, materialize_ms = 0;
+    };
+    const NewTiming& LastNewTiming() const { return timing_; }
+
     friend std::unique_ptr<MerkleTree> New(std::vector<MerkleNode> level, std::string* err);
 
    private:
@@ -352,6 +381,7 @@ class MerkleTree {  // merkletree.go:13-15
     std::deque<MerkleNode> nodes_;  // owns every node of the tree (stable addresses)
     std::vector<uint8_t> levels_;
     uint64_t n_ = 0;  // leaves New built the tree from
+    NewTiming timing_;
 };
 
 inline std::vector<std::vector<uint8_t>> Sha1Many(const std::vector<std::vector<uint8_t>>& msgs) {
@@ -380,6 +410,8 @@ inline std::unique_ptr<MerkleTree> New(std::vector<MerkleNode> level, std::strin
         if (err) *err = "cannot build Merkle Tree from 0 nodes";
         return nullptr;
     }
+    using clk = std::chrono::steady_clock;
+    const auto c0 = clk::now();
     nkv_ctx* ctx = Session::Default().ctx();
     std::unique_ptr<MerkleTree> t(new MerkleTree());
     const uint64_t total = nkv_total_nodes(n);
@@ -418,6 +450,7 @@ inline std::unique_ptr<MerkleTree> New(std::vector<MerkleNode> level, std::strin
                   "New");
         }
     }
+    const auto c1 = clk::now();
     // materialize the pointer tree: copies of the given leaves (Go copies
     // `l := level[i]`), then parents level by level with the empty pad node
     auto& pool = t->nodes_;
@@ -446,7 +479,74 @@ inline std::unique_ptr<MerkleTree> New(std::vector<MerkleNode> level, std::strin
         below.swap(cur);
     }
     t->Root = below[0];
+    t->timing_.call_ms = std::chrono::duration<double, std::milli>(c1 - c0).count();
+    t->timing_.materialize_ms = std::chrono::duration<double, std::milli>(clk::now() - c1).count();
     return t;
+}
+
+// The Merkle step of several compaction output tables (lsmtree.go:71-128 merges
+// a level's runs; MakeTableSecondaries builds each output table's tree,
+// sstable.go:35-47) over several GPUs of one process: table t goes to devices[t %
+// g], one host thread per device drives that device's context of a group
+// (nkv_group_create: one context per GPU and one RCCL communicator), and each
+// table's values are located in its serialized Data table on the device
+// (nkv_tree_from_records, record.go:191-199).  Returns the roots in table order.
+struct DataTable {
+    std::vector<uint8_t> data;       // the Data-table bytes (record.Serialize, record.go:191-199)
+    std::vector<uint64_t> rec_size;  // KeyContext.RecSize of each record (record.go:38-41)
+};
+
+class Group {  // RAII over nkv_group
+   public:
+    explicit Group(const std::vector<int>& devices) {
+        check(nkv_group_create(devices.data(), int(devices.size()), &g_), "nkv_group_create");
+    }
+    ~Group() { nkv_group_destroy(g_); }
+    Group(const Group&) = delete;
+    Group& operator=(const Group&) = delete;
+    nkv_group* get() const { return g_; }
+    int size() const { return nkv_group_size(g_); }
+    nkv_ctx* ctx(int i) const {
+        nkv_ctx* c = nullptr;
+        check(nkv_group_ctx(g_, i, &c), "nkv_group_ctx");
+        return c;
+    }
+
+   private:
+    nkv_group* g_ = nullptr;
+};
+
+inline std::vector<std::array<uint8_t, 20>> CompactRoots(Group& grp, const std::vector<DataTable>& tables) {
+    const int g = grp.size();
+    std::vector<std::array<uint8_t, 20>> roots(tables.size());
+    std::vector<std::exception_ptr> err(g);
+    auto work = [&](int m) {
+        try {
+            nkv_ctx* c = grp.ctx(m);
+            for (size_t t = size_t(m); t < tables.size(); t += size_t(g)) {
+                const DataTable& d = tables[t];
+                if (d.rec_size.empty()) throw std::runtime_error("cannot build Merkle Tree from 0 nodes");
+                check(nkv_tree_from_records(c, d.data.data(), d.data.size(), d.rec_size.data(), d.rec_size.size(),
+                                            roots[t].data(), nullptr, nullptr),
+                      "CompactRoots");
+            }
+        } catch (...) {
+            err[m] = std::current_exception();
+        }
+    };
+    std::vector<std::thread> th;
+    for (int m = 1; m < g; ++m) th.emplace_back(work, m);
+    work(0);
+    for (auto& x : th) x.join();
+    for (auto& e : err)
+        if (e) std::rethrow_exception(e);
+    return roots;
+}
+
+inline std::vector<std::array<uint8_t, 20>> CompactRoots(const std::vector<int>& devices,
+                                                         const std::vector<DataTable>& tables) {
+    Group grp(devices);
+    return CompactRoots(grp, tables);
 }
 
 }  // namespace merkletree

@@ -31,12 +31,36 @@ NKV_OPT_STAGE_CHUNK = 8
 NKV_OPT_QUEUE_RING = 9
 NKV_OPT_BLOOM_PATH = 10
 NKV_OPT_RECORDS_FUSED = 11
+NKV_OPT_TABLE_LANES = 12
+NKV_TIMING_EVENTS = 1
+NKV_TIMING_CLOCK = 2
+NKV_TABLE_STRIDED = 0
+NKV_TABLE_VALUES = 1
+NKV_TABLE_RECORDS = 2
+NKV_TABLE_VERIFY = 3
+NKV_TRANSPORT_RCCL = 1
+NKV_TRANSPORT_COPY = 2
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)
 _u64p = ctypes.POINTER(ctypes.c_uint64)
 _vp = ctypes.c_void_p
 _u64 = ctypes.c_uint64
 _int = ctypes.c_int
+
+class NkvTable(ctypes.Structure):
+    """struct nkv_table (include/nkv_merkle.h): one table of device-resident leaves."""
+    _fields_ = [("kind", _int), ("base", _vp), ("base_len", _u64), ("stride", _u64), ("len", _u64),
+                ("off", _vp), ("lens", _vp), ("n", _u64), ("nodes", _vp), ("err", _vp), ("crc", _vp),
+                ("stats", _vp)]
+
+
+class NkvValues(ctypes.Structure):
+    """struct nkv_values: one table of host values (nkv_group_trees_from_values)."""
+    _fields_ = [("base", _vp), ("off", _vp), ("len", _vp), ("n", _u64), ("root20", _vp), ("nodes_out", _vp),
+                ("img_out", _vp)]
+
+
+_tabp = ctypes.POINTER(NkvTable)
 
 # name -> (restype, argtypes); every symbol include/nkv_merkle.h declares
 SIGNATURES = {
@@ -94,6 +118,24 @@ SIGNATURES = {
     "nkv_bloom_query_dev": (_int, [_vp, _vp, _vp, _vp, _u64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                    _vp, _vp]),
     "nkv_fill_splitmix64_dev": (_int, [_vp, _vp, _u64, _u64]),
+    "nkv_ctx_clock": (_int, [_vp, ctypes.POINTER(ctypes.c_double), _u64p]),
+    "nkv_ctx_last_host_timing": (_int, [_vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float),
+                                        ctypes.POINTER(ctypes.c_float)]),
+    "nkv_host_stream": (_int, [_vp, _vp, _u64]),
+    "nkv_trees_dev": (_int, [_vp, _tabp, _int]),
+    "nkv_group_create": (_int, [ctypes.POINTER(_int), _int, ctypes.POINTER(_vp)]),
+    "nkv_group_destroy": (None, [_vp]),
+    "nkv_group_size": (_int, [_vp]),
+    "nkv_group_transport": (_int, [_vp]),
+    "nkv_group_ctx": (_int, [_vp, _int, ctypes.POINTER(_vp)]),
+    "nkv_group_sync": (_int, [_vp]),
+    "nkv_group_roots_allgather": (_int, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(_vp), _u8p]),
+    "nkv_group_trees_dev": (_int, [_vp, _tabp, _int, _u8p]),
+    "nkv_group_trees_from_values": (_int, [_vp, ctypes.POINTER(NkvValues), _int]),
+    "nkv_split_span": (_u64, [_u64, _int]),
+    "nkv_group_tree_from_values": (_int, [_vp, _u8p, _u64p, _u64p, _u64, _u8p, _u8p, _u8p]),
+    "nkv_group_tree_dev": (_int, [_vp, _tabp, _u64, _vp, _u8p]),
+    "nkv_group_tree_fetch": (_int, [_vp, _u8p, _u8p]),
 }
 
 _lib = None
@@ -164,10 +206,19 @@ class Context:
         self.h = h
         self.device = device
         self.stream = _OWN  # the context's own stream until set_stream
+        self.owned = True
+
+    @classmethod
+    def borrow(cls, handle, device: int) -> "Context":
+        """A view of a context someone else owns (a group member): close() does not destroy it."""
+        c = cls.__new__(cls)
+        c.h, c.device, c.stream, c.owned = handle, device, _OWN, False
+        return c
 
     def close(self) -> None:
         if getattr(self, "h", None):
-            lib().nkv_ctx_destroy(self.h)
+            if getattr(self, "owned", True):
+                lib().nkv_ctx_destroy(self.h)
             self.h = None
 
     def __del__(self):
@@ -212,8 +263,21 @@ class Context:
     def sync(self) -> None:
         check(lib().nkv_ctx_sync(self.h))
 
-    def set_timing(self, on: bool) -> None:
-        check(lib().nkv_ctx_set_timing(self.h, 1 if on else 0))
+    def set_timing(self, on, clock: bool = False) -> None:
+        """Events around the leaf kernel / reduce (on) and the leaf kernels' clock probe (clock)."""
+        flags = (NKV_TIMING_EVENTS if on else 0) | (NKV_TIMING_CLOCK if clock else 0)
+        check(lib().nkv_ctx_set_timing(self.h, flags))
+
+    def clock(self):
+        """(MHz, waves): lifetime-weighted shader clock of the leaf-kernel waves since set_timing(clock=True)."""
+        mhz, waves = ctypes.c_double(), _u64()
+        check(lib().nkv_ctx_clock(self.h, ctypes.byref(mhz), ctypes.byref(waves)))
+        return mhz.value, waves.value
+
+    def trees(self, tables) -> None:
+        """nkv_trees_dev over a list of NkvTable (asynchronous on the context's stream)."""
+        arr = (NkvTable * len(tables))(*tables)
+        check(lib().nkv_trees_dev(self.h, arr, len(tables)), "nkv_trees_dev")
 
     def timing_summary(self):
         """(calls, leaf_ms_total, reduce_ms_total) since set_timing(True)."""
@@ -225,6 +289,62 @@ class Context:
         a, b = ctypes.c_float(), ctypes.c_float()
         check(lib().nkv_ctx_last_timing(self.h, ctypes.byref(a), ctypes.byref(b)))
         return a.value, b.value
+
+
+def table(kind: int, nodes: int, n: int, base: int = 0, base_len: int = 0, stride: int = 0, length: int = 0,
+          off: int = 0, lens: int = 0, err: int = 0, crc: int = 0, stats: int = 0) -> NkvTable:
+    """An nkv_table from device addresses (ints, 0 = NULL)."""
+    return NkvTable(kind, base or None, base_len, stride, length, off or None, lens or None, n, nodes or None,
+                    err or None, crc or None, stats or None)
+
+
+class Group:
+    """One host process over several GPUs (nkv_group_*): a context per listed
+    device and one RCCL communicator (copy transport if a device repeats)."""
+
+    def __init__(self, devices):
+        devs = (_int * len(devices))(*devices)
+        h = _vp()
+        check(lib().nkv_group_create(devs, len(devices), ctypes.byref(h)), f"nkv_group_create({list(devices)})")
+        self.h = h
+        self.devices = list(devices)
+
+    @property
+    def size(self) -> int:
+        return lib().nkv_group_size(self.h)
+
+    @property
+    def transport(self) -> int:
+        return lib().nkv_group_transport(self.h)
+
+    def ctx_handle(self, i: int):
+        out = _vp()
+        check(lib().nkv_group_ctx(self.h, i, ctypes.byref(out)))
+        return out
+
+    def ctx(self, i: int) -> Context:
+        """Member i's context (owned by the group)."""
+        return Context.borrow(self.ctx_handle(i), self.devices[i])
+
+    def sync(self) -> None:
+        check(lib().nkv_group_sync(self.h))
+
+    def close(self) -> None:
+        if getattr(self, "h", None):
+            lib().nkv_group_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
 
 _default: dict = {}

@@ -18,18 +18,21 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 SO = os.path.join(PKG, "libnkvmerkle.so")
-SOURCES = ["kernels.hip", "crc.hip", "bloom.hip", "capi.cpp", "host_stage.cpp"]
-HEADERS = ["internal.hpp", "sha1_dev.hpp", "host_stage.hpp", "crc_dev.hpp"]
+SOURCES = ["kernels.hip", "crc.hip", "bloom.hip", "capi.cpp", "group.cpp", "host_stage.cpp"]
+HEADERS = ["internal.hpp", "context.hpp", "sha1_dev.hpp", "host_stage.hpp", "crc_dev.hpp"]
 ARCH = os.environ.get("NKV_OFFLOAD_ARCH", "gfx950")
 FLAGS = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread",
          "-Wall", "-Wno-unused-result"]
+# RCCL for the multi-GPU group (nkv_group_*: ncclCommInitAll, ncclAllGather)
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+LIBS = [f"-L{ROCM}/lib", "-lrccl"]
 _ID = re.compile(rb"nkv-src-sha256:([0-9a-f]{64})")
 
 
 def source_hash(diag: bool = False) -> str:
     """SHA-256 over the compile flags and every source/header the library is built from."""
     h = hashlib.sha256()
-    h.update(" ".join(FLAGS + (["-DNKV_DIAG"] if diag else [])).encode())
+    h.update(" ".join(FLAGS + LIBS + (["-DNKV_DIAG"] if diag else [])).encode())
     for path in [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(ROOT, "include", "nkv_merkle.h")]:
         h.update(os.path.basename(path).encode() + b"\0")
         with open(path, "rb") as f:
@@ -67,7 +70,7 @@ def build(force: bool = False, verbose: bool = False, diag: bool = False, quiet:
     cmd = [hipcc] + FLAGS + ["-I", os.path.join(ROOT, "include"), "-I", CSRC, f'-DNKV_SRC_HASH="{want}"']
     if diag:
         cmd.append("-DNKV_DIAG")
-    cmd += [os.path.join(CSRC, f) for f in SOURCES] + ["-o", tmp]
+    cmd += [os.path.join(CSRC, f) for f in SOURCES] + LIBS + ["-o", tmp]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.check_call(cmd)
@@ -79,6 +82,23 @@ def build(force: bool = False, verbose: bool = False, diag: bool = False, quiet:
     if not quiet:
         print(last_status, file=sys.stderr)
     return so
+
+
+API_FLUSH_SRC = os.path.join(ROOT, "tools", "api_flush.cpp")
+API_FLUSH = os.path.join(ROOT, "build", "api_flush")
+
+
+def build_api_flush() -> str:
+    """The end-to-end flush driver (tools/api_flush.cpp) over the C++ Go-API mirror
+    (bench.py --config api_flush); g++, linked to the in-tree library."""
+    build(quiet=True)
+    os.makedirs(os.path.dirname(API_FLUSH), exist_ok=True)
+    tmp = f"{API_FLUSH}.tmp{os.getpid()}"
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-pthread", "-I", os.path.join(ROOT, "include"),
+                           API_FLUSH_SRC, "-L", PKG, "-lnkvmerkle", "-Wl,-rpath,$ORIGIN/../nakevaleng_amd",
+                           "-o", tmp])
+    os.replace(tmp, API_FLUSH)
+    return API_FLUSH
 
 
 if __name__ == "__main__":

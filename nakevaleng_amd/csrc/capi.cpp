@@ -14,143 +14,11 @@
 #include <new>
 #include <vector>
 
-#include "host_stage.hpp"
-#include "internal.hpp"
-#include "nkv_merkle.h"
+#include "context.hpp"
 
 using namespace nkv;
 
-namespace {
-
-// ---------------------------------------------------------------------------
-// tree shape (merkletree.go:31-64): n_0 = n, n_{L+1} = ceil(n_L / 2), until a
-// level of one node that is not the leaf level.
-
-int levels_of(uint64_t n) {
-    if (n == 0) return 0;
-    int lv = 1;
-    uint64_t c = n;
-    do {
-        c = (c + 1) / 2;
-        ++lv;
-    } while (c > 1);
-    return lv;
-}
-
-uint64_t count_of(uint64_t n, int L) { return L == 0 ? n : ((n - 1) >> L) + 1; }
-
-uint64_t start_of(uint64_t n, int L) {
-    uint64_t s = 0;
-    for (int j = 0; j < L; ++j) s += count_of(n, j);
-    return s;
-}
-
-uint64_t total_of(uint64_t n) {
-    const int lv = levels_of(n);
-    uint64_t s = 0;
-    for (int j = 0; j < lv; ++j) s += count_of(n, j);
-    return s;
-}
-
-// Image layout (merkletree.go:67-92) of levels given bottom-up counts[0..nlev)
-// of 20-byte nodes stored level-major from node index 0: top level first, 21
-// bytes per node, one 0x01 pad byte after every odd level below the top.
-BfsLayout layout_of(const std::vector<uint64_t>& counts, uint64_t img_base = 0) {
-    BfsLayout lay{};
-    const int nlev = int(counts.size());
-    lay.nlev = nlev;
-    std::vector<uint64_t> start(nlev);
-    uint64_t s = 0;
-    for (int L = 0; L < nlev; ++L) {
-        start[L] = s;
-        s += counts[L];
-    }
-    uint64_t p = img_base;
-    for (int i = 0; i < nlev; ++i) {  // image order: top first
-        const int L = nlev - 1 - i;
-        lay.img_start[i] = p;
-        lay.node_start[i] = start[L];
-        lay.count[i] = counts[L];
-        p += 21 * counts[L];
-        if (L < nlev - 1 && (counts[L] & 1)) p += 1;
-    }
-    lay.total = p;
-    return lay;
-}
-
-std::vector<uint64_t> counts_of(uint64_t n) {
-    std::vector<uint64_t> c(levels_of(n));
-    for (size_t L = 0; L < c.size(); ++L) c[L] = count_of(n, int(L));
-    return c;
-}
-
-}  // namespace
-
-// ---------------------------------------------------------------------------
-// context
-
-struct DevBuf {
-    void* p = nullptr;
-    size_t cap = 0;
-};
-
-struct nkv_ctx {
-    int device = 0;
-    hipStream_t own = nullptr;
-    hipStream_t stream = nullptr;
-    int leaf_load = 4;  // NKV_OPT_LEAF_LOAD
-    int bucket = 2;     // NKV_OPT_BUCKET
-    int deep = 3;       // NKV_OPT_DEEP_PREFETCH (2, 3 = work-queue kernel)
-    uint32_t simds = 1024;  // SIMDs on the device (CUs x 4)
-    int queue_split = 32;   // NKV_OPT_QUEUE_SPLIT
-    int queue_waves = 4;    // NKV_OPT_QUEUE_WAVES
-    int queue_ring = 13;    // NKV_OPT_QUEUE_RING
-    int bloom_path = 2;     // NKV_OPT_BLOOM_PATH
-    int crc_load = 1;       // NKV_OPT_CRC_LOAD
-    int records_fused = 1;  // NKV_OPT_RECORDS_FUSED
-    bool timing = false;
-    bool timed = false;
-    // per-call event triples (leaf start, leaf end / reduce start, reduce end),
-    // the latest kTimingRing / 3 calls
-    static constexpr size_t kTimingRing = 3 * 65536;
-    std::vector<hipEvent_t> ring;
-    size_t ring_used = 0;
-    DevBuf d_data, d_off, d_len, d_nodes, d_img, d_tmp, d_err, d_aux, d_keys, d_perm, d_stmp, d_queue, d_stats,
-        d_range, d_part, d_tmp2, d_flags;
-    int flag_set = 0;  // which of the two pass-flag sets in d_flags the next records call uses
-    void* h_stage = nullptr;  // small pinned staging (offsets, lengths, stats)
-    unsigned int* h_small = nullptr;  // 64 pinned bytes for device-to-host decisions
-    size_t h_cap = 0;
-    Stager stage;  // pipelined pinned staging of bulk bytes (host_stage.hpp)
-};
-
-namespace {
-
-int st(hipError_t e) {
-    if (e == hipSuccess) return NKV_OK;
-    if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) return NKV_ERR_NOMEM;
-    return NKV_ERR_DEVICE;
-}
-
-#define TRY(x)                         \
-    do {                               \
-        int _rc = (x);                 \
-        if (_rc != NKV_OK) return _rc; \
-    } while (0)
-#define HIPTRY(x) TRY(st(x))
-// Every C-ABI entry is a function-try-block: a host allocation or thread start
-// that throws inside the library becomes a status code, never an exception
-// crossing the C boundary (cgo / ctypes callers cannot catch it).
-#define NKV_CATCH                      \
-    catch (const std::bad_alloc&) {    \
-        return NKV_ERR_NOMEM;          \
-    }                                  \
-    catch (...) {                      \
-        return NKV_ERR_DEVICE;         \
-    }
-// Largest batch: leaf indices are 32-bit in the sort and queue kernels
-// (2^31 - 1 values of 4 KiB would be 8 TiB, far beyond one GPU's HBM).
-constexpr uint64_t kMaxN = 0x7fffffffull;
+namespace nkv {
 
 int bind(nkv_ctx* c) {
     if (!c) return NKV_ERR_INVALID;
@@ -221,17 +89,84 @@ bool records_fit(const uint64_t* rec_size, uint64_t n, uint64_t stream_len) {
     return true;
 }
 
-// Pack n host values into d_data at 16-byte aligned offsets and upload their
-// packed offsets/lengths to d_off / d_len.  The bytes go through the pipelined
-// pinned stager (a pool of host threads gathers chunk k+1 while chunk k is in
-// flight); no caller pointer is kept.
-int stage_values(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint64_t* len,
-                 uint64_t n) {
+// The pinned block (nkv_host_alloc on this context) that holds every value
+// base + off[i] .. + len[i], or null; *lo / *hi: the values' extent relative
+// to the block.
+nkv_ctx::Pinned* pinned_extent(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint64_t* len,
+                               uint64_t n, uint64_t* lo, uint64_t* hi) {
+    if (c->pinned.empty() || n == 0) return nullptr;
+    uint64_t a = ~uint64_t(0), b = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        if (len[i] > (uint64_t(1) << 62) || off[i] > (uint64_t(1) << 62)) return nullptr;
+        a = std::min(a, off[i]);
+        b = std::max(b, off[i] + len[i]);
+    }
+    const uintptr_t s = reinterpret_cast<uintptr_t>(base) + a, e = reinterpret_cast<uintptr_t>(base) + b;
+    if (e < s) return nullptr;
+    for (nkv_ctx::Pinned* blk : c->pinned) {
+        const uintptr_t p = reinterpret_cast<uintptr_t>(blk->p);
+        if (s >= p && e <= p + blk->bytes) {
+            *lo = s - p;
+            *hi = e - p;
+            return blk;
+        }
+    }
+    return nullptr;
+}
+
+// Queue bytes [from, to) of a pinned block to its device mirror on the
+// context's stream (the block is library-owned memory, so the DMA may outlive
+// the call).
+int stream_block(nkv_ctx* c, nkv_ctx::Pinned* blk, uint64_t from, uint64_t to) {
+    if (to <= from) return NKV_OK;
+    if (!blk->d_arena.p) TRY(grow(blk->d_arena, blk->bytes));
+    HIPTRY(hipMemcpyAsync(static_cast<uint8_t*>(blk->d_arena.p) + from, blk->p + from, to - from,
+                          hipMemcpyHostToDevice, c->stream));
+    return NKV_OK;
+}
+
+// Move n host values to the device and upload their offsets/lengths to d_off /
+// d_len; *d_base / *aligned tell the kernels where the values are.
+//  - Values inside one pinned block of this context (the deferred-NewLeaf
+//    arena, nkv_host_alloc): one DMA straight from the block into its device
+//    mirror, minus the prefix nkv_host_stream already queued; offsets are the
+//    values' places in the block (aligned iff all are 16-byte aligned).
+//  - Anything else: packed at 16-byte aligned offsets through the pipelined
+//    pinned stager (a pool of host threads gathers chunk k+1 while chunk k is
+//    in flight).
+// No caller pointer is kept either way.
+int stage_values(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint64_t* len, uint64_t n,
+                 const uint8_t** d_base, bool* aligned) {
+    uint64_t lo = 0, hi = 0;
+    if (nkv_ctx::Pinned* blk = pinned_extent(c, base, off, len, n, &lo, &hi)) {
+        TRY(grow_host(c, 16 * n));
+        TRY(grow(c->d_off, 8 * n));
+        TRY(grow(c->d_len, 8 * n));
+        uint64_t* hoff = static_cast<uint64_t*>(c->h_stage);
+        uint64_t* hlen = hoff + n;
+        const uint64_t adj = uint64_t(base - blk->p);
+        uint64_t ormask = 0;
+        for (uint64_t i = 0; i < n; ++i) {
+            hoff[i] = adj + off[i];
+            hlen[i] = len[i];
+            ormask |= hoff[i];
+        }
+        // the prefix nkv_host_stream queued is already on its way; the rest now
+        TRY(stream_block(c, blk, std::max(lo, blk->streamed), hi));
+        blk->streamed = 0;  // this call consumes the batch: a new one streams from 0
+        HIPTRY(hipMemcpyAsync(c->d_off.p, hoff, 8 * n, hipMemcpyHostToDevice, c->stream));
+        HIPTRY(hipMemcpyAsync(c->d_len.p, hlen, 8 * n, hipMemcpyHostToDevice, c->stream));
+        *d_base = static_cast<const uint8_t*>(blk->d_arena.p);
+        *aligned = (ormask & 15) == 0;
+        return NKV_OK;
+    }
     uint64_t total = 0;
     for (uint64_t i = 0; i < n; ++i) {
         if (len[i] > (uint64_t(1) << 62) || total > (uint64_t(1) << 62)) return NKV_ERR_INVALID;
         total += align16(len[i]);
     }
+    *d_base = nullptr;
+    *aligned = true;
     TRY(grow_host(c, 16 * n));
     TRY(grow(c->d_data, total));
     TRY(grow(c->d_off, 8 * n));
@@ -248,6 +183,7 @@ int stage_values(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uin
     HIPTRY(c->stage.upload(seg, total, static_cast<uint8_t*>(c->d_data.p), c->stream));
     HIPTRY(hipMemcpyAsync(c->d_off.p, hoff, 8 * n, hipMemcpyHostToDevice, c->stream));
     HIPTRY(hipMemcpyAsync(c->d_len.p, hlen, 8 * n, hipMemcpyHostToDevice, c->stream));
+    *d_base = static_cast<const uint8_t*>(c->d_data.p);
     return NKV_OK;
 }
 
@@ -301,6 +237,17 @@ int mark(nkv_ctx* c, int which) {
     return NKV_OK;
 }
 
+// Events around a host-buffer tree call (which = 0 before the upload, 1 after
+// the outputs are back): with the three mark() events of the same call they
+// split it into upload, kernels and download (nkv_ctx_last_host_timing).
+int host_mark(nkv_ctx* c, int which) {
+    if (!c->timing) return NKV_OK;
+    if (!c->host_ev[which]) HIPTRY(hipEventCreate(&c->host_ev[which]));
+    HIPTRY(hipEventRecord(c->host_ev[which], c->stream));
+    if (which == 1) c->host_timed = c->timed;
+    return NKV_OK;
+}
+
 // Order of a ragged batch for the leaf kernel (NKV_OPT_BUCKET): input order
 // (no sort), length-sorted (work queue), or both kernels
 // launched behind a device-side Gate.  Auto mode (2) sorts batches of fewer than
@@ -350,38 +297,28 @@ int leaf_level(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint6
                bool aligned, uint8_t* nodes, int plan, Gate range, bool narrow_kernel = true,
                CopyWords cw = CopyWords{}) {
     if (plan == kInputOrder && cw.n) return NKV_ERR_INVALID;  // the copy rides on the sort
-    if (plan == kInputOrder)
-        return st(launch_leaf_offsets(base, off, len, nullptr, n, aligned, c->leaf_load, nodes, c->stream,
-                                      c->deep != 0));
+    if (plan == kInputOrder) return st(launch_leaf_offsets(base, off, len, n, aligned, c->leaf_load, nodes, c->stream));
     if (n > 0x7fffffffull) return NKV_ERR_INVALID;
     const Gate wide{range.range, plan == kGated ? 2 : 0};
     const size_t keys_cap = c->d_keys.cap;
     TRY(grow(c->d_keys, 4 * sort_hist_words(n)));
-    if (c->d_keys.cap != keys_cap)  // (re)allocated scratch: the sort's bucket totals start at zero
+    // (re)allocated scratch, or a sort cut short by an error: the sort's bucket
+    // totals must start at zero (its last workgroup leaves them zero again)
+    if (c->d_keys.cap != keys_cap || c->sort_dirty) {
         HIPTRY(hipMemsetAsync(c->d_keys.p, 0, 4 * sort_head_words(), c->stream));
+        c->sort_dirty = false;
+    }
+    c->sort_dirty = true;  // until the sort and the kernels behind it are queued
     TRY(grow(c->d_perm, 4 * n));
     uint32_t* perm = static_cast<uint32_t*>(c->d_perm.p);
-    QueueInit qi;
-    if (c->deep >= 2) {
-        TRY(grow(c->d_queue, 4 * queue_words(n)));
-        qi = QueueInit{static_cast<uint32_t*>(c->d_queue.p), queue_words(n), uint32_t(c->queue_split)};
-    }
+    TRY(grow(c->d_queue, 4 * queue_words(n)));
+    const QueueInit qi{static_cast<uint32_t*>(c->d_queue.p), queue_words(n), uint32_t(c->queue_split)};
     HIPTRY(sort_by_length_desc(len, n, perm, static_cast<uint32_t*>(c->d_keys.p), c->stream, wide, qi, cw));
-    if (c->deep >= 2) {
-        const int ring = c->deep == 3 ? c->queue_ring : 0;
-        // LDS per CU (160 KiB) holds 20 / 13 / 10 rings of 2 / 3 / 4 slots
-        const int slots = ring % 10;
-        const int max_waves = slots == 4 ? 2 : (slots == 3 ? 3 : 5);
-        const int waves = ring ? std::min(c->queue_waves, max_waves) : 2;
-        HIPTRY(launch_leaf_queue(base, off, len, perm, n, aligned, ring, static_cast<uint32_t*>(c->d_queue.p),
-                                 c->simds, uint32_t(waves), nodes, c->stream, wide));
-    } else {
-        HIPTRY(launch_leaf_offsets(base, off, len, perm, n, aligned, c->leaf_load, nodes, c->stream, c->deep != 0,
-                                   wide));
-    }
+    HIPTRY(launch_leaf_queue(base, off, len, perm, n, static_cast<uint32_t*>(c->d_queue.p), c->simds,
+                             uint32_t(c->queue_waves), nodes, c->stream, wide));
     if (plan == kGated && narrow_kernel)
-        HIPTRY(launch_leaf_offsets(base, off, len, nullptr, n, aligned, c->leaf_load, nodes, c->stream,
-                                   c->deep != 0, Gate{range.range, 1}));
+        HIPTRY(launch_leaf_offsets(base, off, len, n, aligned, c->leaf_load, nodes, c->stream, Gate{range.range, 1}));
+    c->sort_dirty = false;
     return NKV_OK;
 }
 
@@ -396,8 +333,8 @@ int leaf_level(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint6
 // host_len (nullable): the value lengths on the host, when the caller has them.
 // Every order leaves level 0 complete, so one reduce sequence follows.
 int tree_from_device_values(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint64_t* len,
-                            uint64_t n, bool aligned, uint8_t* nodes, const uint64_t* host_len = nullptr,
-                            const unsigned int* dev_range = nullptr) {
+                            uint64_t n, bool aligned, uint8_t* nodes, const uint64_t* host_len,
+                            const unsigned int* dev_range) {
     int plan = kInputOrder;
     Gate g;
     TRY(plan_of(c, len, host_len, n, &plan, &g, dev_range));
@@ -451,7 +388,7 @@ int records_tree(nkv_ctx* c, const uint8_t* stream, uint64_t stream_len, const u
     return mark(c, 2);
 }
 
-}  // namespace
+}  // namespace nkv
 
 #ifndef NKV_SRC_HASH
 #define NKV_SRC_HASH "unknown"
@@ -518,44 +455,67 @@ void nkv_ctx_destroy(nkv_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->own) (void)hipStreamSynchronize(c->own);
+    if (c->clock_probe) (void)set_clock_probe(nullptr, c->own);  // kernels must not add into freed memory
+    for (nkv_ctx* l : c->lanes) nkv_ctx_destroy(l);
+    (void)hipSetDevice(c->device);
     for (DevBuf* b : {&c->d_data, &c->d_off, &c->d_len, &c->d_nodes, &c->d_img, &c->d_tmp,
                       &c->d_err, &c->d_aux, &c->d_keys, &c->d_perm, &c->d_stmp, &c->d_queue, &c->d_stats,
-                      &c->d_range, &c->d_part, &c->d_tmp2, &c->d_flags})
+                      &c->d_range, &c->d_part, &c->d_tmp2, &c->d_flags, &c->d_clk})
         if (b->p) (void)hipFree(b->p);
+    for (nkv_ctx::Pinned* blk : c->pinned) {
+        if (blk->d_arena.p) (void)hipFree(blk->d_arena.p);
+        (void)hipHostFree(blk->p);
+        delete blk;
+    }
     if (c->h_stage) (void)hipHostFree(c->h_stage);
     if (c->h_small) (void)hipHostFree(c->h_small);
     for (hipEvent_t e : c->ring) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->join_ev) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->host_ev)
+        if (e) (void)hipEventDestroy(e);
+    if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
+    if (c->switch_ev) (void)hipEventDestroy(c->switch_ev);
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;
 }
 
+// Stream hand-over: work already queued on the old stream (an asynchronous
+// *_dev call) is ordered before anything the context queues on the new one --
+// the records entries' pass flags and the sort scratch carry state from one
+// call to the next on a context.
+static int switch_stream(nkv_ctx* c, hipStream_t s) {
+    if (s == c->stream) return NKV_OK;
+    if (!c->switch_ev) HIPTRY(hipEventCreateWithFlags(&c->switch_ev, hipEventDisableTiming));
+    HIPTRY(hipEventRecord(c->switch_ev, c->stream));
+    HIPTRY(hipStreamWaitEvent(s, c->switch_ev, 0));
+    c->stream = s;
+    return NKV_OK;
+}
+
 int nkv_ctx_set_stream(nkv_ctx* c, void* s) try {
     TRY(bind(c));
-    c->stream = static_cast<hipStream_t>(s);  // NULL = the device's null stream
-    return NKV_OK;
+    return switch_stream(c, static_cast<hipStream_t>(s));  // NULL = the device's null stream
 } NKV_CATCH
 
 int nkv_ctx_use_own_stream(nkv_ctx* c) try {
     TRY(bind(c));
-    c->stream = c->own;
-    return NKV_OK;
+    return switch_stream(c, c->own);
 } NKV_CATCH
 
 int nkv_ctx_set_option(nkv_ctx* c, int key, int64_t value) try {
     TRY(bind(c));
     switch (key) {
         case NKV_OPT_LEAF_LOAD:
-            if (value < 1 || value > 12 || value == 6 || value == 7 || value == 8) return NKV_ERR_INVALID;
+            if (value != 4 && value != 11) return NKV_ERR_INVALID;
             c->leaf_load = int(value);
             return NKV_OK;
         case NKV_OPT_BUCKET:
             if (value < 0 || value > 2) return NKV_ERR_INVALID;
             c->bucket = int(value);
             return NKV_OK;
-        case NKV_OPT_DEEP_PREFETCH:
-            if (value < 0 || value > 3) return NKV_ERR_INVALID;
-            c->deep = int(value);
-            return NKV_OK;
+        case NKV_OPT_DEEP_PREFETCH:  // the work-queue kernel is the only sorted path left
+            return value == 3 ? NKV_OK : NKV_ERR_INVALID;
         case NKV_OPT_QUEUE_SPLIT:
             if (value < 0 || value > 0xFFFFFFFFll) return NKV_ERR_INVALID;
             c->queue_split = int(std::min<int64_t>(value, 0x7FFFFFFF));
@@ -568,10 +528,8 @@ int nkv_ctx_set_option(nkv_ctx* c, int key, int64_t value) try {
             if (value < 0 || value > 2) return NKV_ERR_INVALID;
             c->bloom_path = int(value);
             return NKV_OK;
-        case NKV_OPT_QUEUE_RING:
-            if (!((value >= 2 && value <= 4) || (value >= 12 && value <= 14))) return NKV_ERR_INVALID;
-            c->queue_ring = int(value);
-            return NKV_OK;
+        case NKV_OPT_QUEUE_RING:  // the 3-slot value-relative ring is the only one left
+            return value == 13 ? NKV_OK : NKV_ERR_INVALID;
         case NKV_OPT_HOST_THREADS:
             if (value < 0 || value > 256) return NKV_ERR_INVALID;
             c->stage.want_threads = int(value);
@@ -586,8 +544,12 @@ int nkv_ctx_set_option(nkv_ctx* c, int key, int64_t value) try {
             c->records_fused = int(value);
             return NKV_OK;
         case NKV_OPT_QUEUE_WAVES:
-            if (value < 1 || value > 5) return NKV_ERR_INVALID;  // 8 KiB LDS per wave: <= 20 per CU
+            if (value < 1 || value > 3) return NKV_ERR_INVALID;  // 12 KiB ring per wave: <= 13 per CU
             c->queue_waves = int(value);
+            return NKV_OK;
+        case NKV_OPT_TABLE_LANES:
+            if (value < 1 || value > 8) return NKV_ERR_INVALID;
+            c->table_lanes = int(value);
             return NKV_OK;
         default:
             return NKV_ERR_INVALID;
@@ -601,28 +563,87 @@ int nkv_ctx_sync(nkv_ctx* c) try {
 
 int nkv_ctx_set_timing(nkv_ctx* c, int enable) try {
     TRY(bind(c));
-    c->timing = enable != 0;
+    if (enable & ~(NKV_TIMING_EVENTS | NKV_TIMING_CLOCK)) return NKV_ERR_INVALID;
+    c->timing = (enable & NKV_TIMING_EVENTS) != 0;
     c->timed = false;
     c->ring_used = 0;
+    for (nkv_ctx* l : c->lanes) {
+        l->timing = c->timing;
+        l->timed = false;
+        l->ring_used = 0;
+    }
+    if (enable & NKV_TIMING_CLOCK) {
+        TRY(grow(c->d_clk, kClockWords * sizeof(unsigned long long)));
+        HIPTRY(hipMemsetAsync(c->d_clk.p, 0, kClockWords * sizeof(unsigned long long), c->stream));
+        HIPTRY(set_clock_probe(static_cast<unsigned long long*>(c->d_clk.p), c->stream));
+        c->clock_probe = true;
+    } else if (c->clock_probe) {
+        HIPTRY(set_clock_probe(nullptr, c->stream));
+        c->clock_probe = false;
+    }
     return NKV_OK;
 } NKV_CATCH
 
-int nkv_ctx_timing_summary(nkv_ctx* c, int* calls, float* leaf_ms_total, float* reduce_ms_total) try {
+int nkv_ctx_clock(nkv_ctx* c, double* mhz, uint64_t* waves) try {
     TRY(bind(c));
-    if (!calls || !leaf_ms_total || !reduce_ms_total) return NKV_ERR_INVALID;
+    if (!mhz || !waves) return NKV_ERR_INVALID;
+    if (!c->d_clk.p) return NKV_ERR_INVALID;
+    std::vector<unsigned long long> h(kClockWords);
+    HIPTRY(hipStreamSynchronize(c->stream));
+    for (nkv_ctx* l : c->lanes) HIPTRY(hipStreamSynchronize(l->stream));
+    HIPTRY(hipMemcpy(h.data(), c->d_clk.p, kClockWords * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    // per slot: [0] shader-clock cycles, [1] 100 MHz reference ticks, summed over waves; [2] waves
+    double cyc = 0, ticks = 0;
+    uint64_t w = 0;
+    for (uint32_t s = 0; s < kClockWords; s += 32) {
+        cyc += double(h[s]);
+        ticks += double(h[s + 1]);
+        w += h[s + 2];
+    }
+    *mhz = ticks > 0 ? 100.0 * cyc / ticks : 0.0;
+    *waves = w;
+    return NKV_OK;
+} NKV_CATCH
+
+static int timing_sum(nkv_ctx* c, int* calls, double* a, double* b) {
     const size_t k = c->ring_used / 3;
     if (k) HIPTRY(hipEventSynchronize(c->ring[c->ring_used - 1]));
-    double a = 0, b = 0;
     for (size_t i = 0; i < k; ++i) {
         float x = 0.f, y = 0.f;
         HIPTRY(hipEventElapsedTime(&x, c->ring[3 * i], c->ring[3 * i + 1]));
         HIPTRY(hipEventElapsedTime(&y, c->ring[3 * i + 1], c->ring[3 * i + 2]));
-        a += x;
-        b += y;
+        *a += x;
+        *b += y;
     }
-    *calls = int(k);
+    *calls += int(k);
+    return NKV_OK;
+}
+
+int nkv_ctx_timing_summary(nkv_ctx* c, int* calls, float* leaf_ms_total, float* reduce_ms_total) try {
+    TRY(bind(c));
+    if (!calls || !leaf_ms_total || !reduce_ms_total) return NKV_ERR_INVALID;
+    int k = 0;
+    double a = 0, b = 0;
+    TRY(timing_sum(c, &k, &a, &b));
+    for (nkv_ctx* l : c->lanes) TRY(timing_sum(l, &k, &a, &b));  // nkv_trees_dev's lanes
+    *calls = k;
     *leaf_ms_total = float(a);
     *reduce_ms_total = float(b);
+    return NKV_OK;
+} NKV_CATCH
+
+int nkv_ctx_last_host_timing(nkv_ctx* c, float* upload_ms, float* kernels_ms, float* download_ms) try {
+    TRY(bind(c));
+    if (!c->host_timed || !c->timed) return NKV_ERR_INVALID;
+    hipEvent_t* ev = &c->ring[c->ring_used - 3];
+    HIPTRY(hipEventSynchronize(c->host_ev[1]));
+    float a = 0.f, b = 0.f, d = 0.f;
+    HIPTRY(hipEventElapsedTime(&a, c->host_ev[0], ev[0]));
+    HIPTRY(hipEventElapsedTime(&b, ev[0], ev[2]));
+    HIPTRY(hipEventElapsedTime(&d, ev[2], c->host_ev[1]));
+    if (upload_ms) *upload_ms = a;
+    if (kernels_ms) *kernels_ms = b;
+    if (download_ms) *download_ms = d;
     return NKV_OK;
 } NKV_CATCH
 
@@ -653,18 +674,51 @@ uint64_t nkv_bfs_size(uint64_t n) { return n == 0 ? 0 : layout_of(counts_of(n)).
 // ---- pinned arena ----
 int nkv_host_alloc(nkv_ctx* c, uint64_t bytes, void** out) try {
     if (!out) return NKV_ERR_INVALID;
+    *out = nullptr;
     TRY(bind(c));
-    if (hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) {
         (void)hipGetLastError();
-        *out = nullptr;
         return NKV_ERR_NOMEM;
     }
+    nkv_ctx::Pinned* blk = new (std::nothrow) nkv_ctx::Pinned{static_cast<uint8_t*>(p), bytes ? bytes : 1, 0, {}};
+    if (!blk) {
+        (void)hipHostFree(p);
+        return NKV_ERR_NOMEM;
+    }
+    c->pinned.push_back(blk);
+    *out = p;
     return NKV_OK;
 } NKV_CATCH
 
 int nkv_host_free(nkv_ctx* c, void* p) try {
     TRY(bind(c));
-    return p ? st(hipHostFree(p)) : NKV_OK;
+    if (!p) return NKV_OK;
+    for (size_t i = 0; i < c->pinned.size(); ++i) {
+        nkv_ctx::Pinned* blk = c->pinned[i];
+        if (blk->p != p) continue;
+        // copies from the block (nkv_host_stream, a tree call) may still be queued
+        HIPTRY(hipStreamSynchronize(c->stream));
+        if (blk->d_arena.p) (void)hipFree(blk->d_arena.p);
+        c->pinned.erase(c->pinned.begin() + long(i));
+        delete blk;
+        break;
+    }
+    return st(hipHostFree(p));
+} NKV_CATCH
+
+int nkv_host_stream(nkv_ctx* c, const void* block, uint64_t upto) try {
+    TRY(bind(c));
+    if (!block) return NKV_ERR_INVALID;
+    for (nkv_ctx::Pinned* blk : c->pinned) {
+        if (blk->p != block) continue;
+        if (upto > blk->bytes) return NKV_ERR_INVALID;
+        if (upto < blk->streamed) blk->streamed = 0;  // a new batch: its bytes replace the old ones
+        TRY(stream_block(c, blk, blk->streamed, upto));
+        blk->streamed = std::max(blk->streamed, upto);
+        return NKV_OK;
+    }
+    return NKV_ERR_INVALID;  // not a block nkv_host_alloc returned on this context
 } NKV_CATCH
 
 // ---- host-buffer API ----
@@ -674,11 +728,13 @@ int nkv_leaf_hash(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const ui
     if (n > kMaxN) return NKV_ERR_INVALID;
     if (n == 0) return NKV_OK;
     if (!base || !off || !len || !out20) return NKV_ERR_INVALID;
-    TRY(stage_values(c, base, off, len, n));
+    const uint8_t* d_base = nullptr;
+    bool aligned = true;
+    TRY(stage_values(c, base, off, len, n, &d_base, &aligned));
     TRY(grow(c->d_nodes, 20 * n));
     uint8_t* nodes = static_cast<uint8_t*>(c->d_nodes.p);
-    TRY(leaf_level(c, static_cast<const uint8_t*>(c->d_data.p), static_cast<const uint64_t*>(c->d_off.p),
-                   static_cast<const uint64_t*>(c->d_len.p), n, true, nodes, len));
+    TRY(leaf_level(c, d_base, static_cast<const uint64_t*>(c->d_off.p), static_cast<const uint64_t*>(c->d_len.p), n,
+                   aligned, nodes, len));
     HIPTRY(c->stage.download(out20, nodes, 20 * n, c->stream));
     return st(hipStreamSynchronize(c->stream));
 } NKV_CATCH
@@ -702,13 +758,16 @@ int nkv_tree_from_values(nkv_ctx* c, const uint8_t* base, const uint64_t* off, c
     if (n > kMaxN) return NKV_ERR_INVALID;
     if (n == 0) return NKV_ERR_EMPTY;
     if (!base || !off || !len) return NKV_ERR_INVALID;
-    TRY(stage_values(c, base, off, len, n));
+    TRY(host_mark(c, 0));
+    const uint8_t* d_base = nullptr;
+    bool aligned = true;
+    TRY(stage_values(c, base, off, len, n, &d_base, &aligned));
     TRY(grow(c->d_nodes, 20 * total_of(n)));
     uint8_t* nodes = static_cast<uint8_t*>(c->d_nodes.p);
-    TRY(tree_from_device_values(c, static_cast<const uint8_t*>(c->d_data.p),
-                                static_cast<const uint64_t*>(c->d_off.p),
-                                static_cast<const uint64_t*>(c->d_len.p), n, true, nodes, len));
-    return finish_tree(c, nodes, n, root20, nodes_out, img_out);
+    TRY(tree_from_device_values(c, d_base, static_cast<const uint64_t*>(c->d_off.p),
+                                static_cast<const uint64_t*>(c->d_len.p), n, aligned, nodes, len));
+    TRY(finish_tree(c, nodes, n, root20, nodes_out, img_out));
+    return host_mark(c, 1);
 } NKV_CATCH
 
 uint64_t nkv_generic_bfs_size(const uint64_t* len, uint64_t n) {
@@ -748,12 +807,14 @@ int nkv_tree_generic(nkv_ctx* c, const uint8_t* data, const uint64_t* off, const
             p += len[2 * i + 1];
         }
     }
-    TRY(stage_values(c, tmp.data(), moff.data(), mlen.data(), n1));
+    const uint8_t* d_base = nullptr;
+    bool aligned = true;
+    TRY(stage_values(c, tmp.data(), moff.data(), mlen.data(), n1, &d_base, &aligned));
     const uint64_t up_total = n1 == 1 ? 1 : total_of(n1);
     TRY(grow(c->d_nodes, 20 * up_total));
     uint8_t* up = static_cast<uint8_t*>(c->d_nodes.p);
-    TRY(leaf_level(c, static_cast<const uint8_t*>(c->d_data.p), static_cast<const uint64_t*>(c->d_off.p),
-                   static_cast<const uint64_t*>(c->d_len.p), n1, true, up, mlen.data()));
+    TRY(leaf_level(c, d_base, static_cast<const uint64_t*>(c->d_off.p), static_cast<const uint64_t*>(c->d_len.p), n1,
+                   aligned, up, mlen.data()));
     if (n1 > 1) HIPTRY(launch_reduce(up, n1, 0, levels_of(n1) - 1, c->stream));
     if (upper_out) HIPTRY(c->stage.download(upper_out, up, 20 * up_total, c->stream));
     if (root20)

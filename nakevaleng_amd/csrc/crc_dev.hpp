@@ -59,29 +59,18 @@ __device__ __forceinline__ uint32_t crc_x_last(uint32_t x, const uint32_t* tab) 
            crc_lut<C>(tab, 0, x >> 24);
 }
 
-// 16 little-endian words (one 64-byte block) in x form; NKV_CRC_WORD_STEP
-// builds the plain word steps instead (A/B only)
+// 16 little-endian words (one 64-byte block) in x form
 template <int C>
 __device__ __forceinline__ uint32_t crc_block16(uint32_t crc, const uint32_t w[16], const uint32_t* tab) {
-#ifdef NKV_CRC_WORD_STEP
-#pragma unroll
-    for (int i = 0; i < 16; ++i) crc = crc_word<C>(crc, w[i], tab);
-    return crc;
-#else
     uint32_t x = crc ^ w[0];
 #pragma unroll
     for (int i = 1; i < 16; ++i) x = crc_x_next<C>(x, w[i], tab);
     return crc_x_last<C>(x, tab);
-#endif
 }
 
 template <int C>
 __device__ __forceinline__ uint32_t crc_quad(uint32_t crc, uint4 v, const uint32_t* tab) {
-#ifdef NKV_CRC_WORD_STEP
-    return crc_word<C>(crc_word<C>(crc_word<C>(crc_word<C>(crc, v.x, tab), v.y, tab), v.z, tab), v.w, tab);
-#else
     return crc_x_last<C>(crc_x_next<C>(crc_x_next<C>(crc_x_next<C>(crc ^ v.x, v.y, tab), v.z, tab), v.w, tab), tab);
-#endif
 }
 
 template <int C>

@@ -7,23 +7,14 @@ namespace nkv {
 
 constexpr int kBlock = 256;       // threads per workgroup = leaves per K1 block
 constexpr int kSlabLevels = 8;    // log2(kBlock): levels one k_reduce workgroup builds
-#ifndef NKV_REDUCE2_MIN
-#define NKV_REDUCE2_MIN 524288
-#endif
 // levels of at least this many nodes are reduced two at a time at full lane
 // use (k_reduce2) before the slabs take over (launch_reduce)
-constexpr uint64_t kReduce2Min = NKV_REDUCE2_MIN;
-#ifndef NKV_REDUCE_WIDE_MIN
-#define NKV_REDUCE_WIDE_MIN 65536
-#endif
+constexpr uint64_t kReduce2Min = 524288;
 // levels of at least this many nodes (and at least 12 below the top) take the
 // bottom-twelve-levels launch (k_reduce_wide) first
-constexpr uint64_t kReduceWideMin = NKV_REDUCE_WIDE_MIN;
+constexpr uint64_t kReduceWideMin = 65536;
 constexpr int kMaxLevels = 64;
-#ifndef NKV_LEAF_WAVES
-#define NKV_LEAF_WAVES 8
-#endif
-constexpr int kLeafWavesPerSimd = NKV_LEAF_WAVES;  // 8 waves/SIMD <=> <= 64 VGPRs
+constexpr int kLeafWavesPerSimd = 8;  // 8 waves/SIMD <=> <= 64 VGPRs
 
 // Device-side choice between two leaf kernels launched back to back (no host
 // read-back): range = the batch's (min, max) full-block counts from
@@ -68,16 +59,15 @@ struct BfsLayout {
     uint64_t count[kMaxLevels];       // real nodes in the level
 };
 
-// load: leaf-kernel load path (1 LDS-DMA, 2 direct, 3 direct non-temporal, 4 / 5
-// direct 128 / 256-B runs); direct loads need 16-byte aligned values, so
-// unaligned batches take LDS-DMA from the values' own addresses (8) for load 1
-// and the register funnel (0) otherwise.
+// load: leaf-kernel load path (NKV_OPT_LEAF_LOAD): 4 = 128-byte register runs
+// for 16-byte aligned values (unaligned ones take 11), 11 = the staged paths
+// (segment stage, 80-byte window stage, value-relative LDS-DMA stream) for any.
 // Level 0 (the leaf digests) only; launch_reduce builds the levels above.
 hipError_t launch_leaf_strided(const uint8_t* base, uint64_t stride, uint64_t L, uint64_t n, int load,
                                uint8_t* nodes, hipStream_t s);
-hipError_t launch_leaf_offsets(const uint8_t* base, const uint64_t* off, const uint64_t* len,
-                               const uint32_t* perm, uint64_t n, bool aligned, int load, uint8_t* nodes,
-                               hipStream_t s, bool deep = true, Gate gate = Gate{});
+// In input order (the length-sorted order goes through launch_leaf_queue).
+hipError_t launch_leaf_offsets(const uint8_t* base, const uint64_t* off, const uint64_t* len, uint64_t n,
+                               bool aligned, int load, uint8_t* nodes, hipStream_t s, Gate gate = Gate{});
 // The work queue's state (queue_words(n) u32 at q), set up by the length sort
 // that precedes the queue kernel (sort_by_length_desc with a QueueInit): split
 // = longest chain (compressions - 1) of a group the non-priority waves take
@@ -89,13 +79,11 @@ struct QueueInit {
     uint32_t split = 0;
 };
 // Ragged batch through the work-queue leaf kernel (perm = length-sorted order,
-// longest first; q set up by the sort).  ring: 0 = register prefetch, 2 = LDS
-// chunk ring, 3 / 4 = pipelined ring of 3 / 4 slots, 12 / 13 / 14 = pipelined
-// ring of value-relative chunks with 2 / 3 / 4 slots.
-hipError_t launch_leaf_queue(const uint8_t* base, const uint64_t* off, const uint64_t* len,
-                             const uint32_t* perm, uint64_t n, bool aligned, int ring, uint32_t* q,
-                             uint32_t simds, uint32_t waves_per_simd, uint8_t* nodes, hipStream_t s,
-                             Gate gate = Gate{});
+// longest first; q set up by the sort), values staged through a pipelined LDS
+// ring of value-relative chunks; waves_per_simd: 1..3.
+hipError_t launch_leaf_queue(const uint8_t* base, const uint64_t* off, const uint64_t* len, const uint32_t* perm,
+                             uint64_t n, uint32_t* q, uint32_t simds, uint32_t waves_per_simd, uint8_t* nodes,
+                             hipStream_t s, Gate gate = Gate{});
 hipError_t launch_reduce(uint8_t* nodes, uint64_t n, int from_level, int top, hipStream_t s, Gate gate = Gate{});
 hipError_t launch_bfs_image(const uint8_t* nodes, const BfsLayout& lay, uint8_t* img,
                             hipStream_t s);
@@ -174,6 +162,11 @@ hipError_t launch_bloom_staged(int mode, const uint8_t* base, const uint64_t* of
                                uint64_t stream_len, uint64_t n, uint32_t m, uint32_t k, uint32_t seed0,
                                uint32_t* bits, unsigned int* err, uint32_t* scratch, hipStream_t s);
 hipError_t launch_fill(uint8_t* buf, uint64_t nbytes, uint64_t seed, hipStream_t s);
+// Clock probe of the leaf kernels on the current device (NKV_TIMING_CLOCK):
+// p = kClockWords u64 (8 slots of 32: shader-clock cycles, 100 MHz ticks, waves;
+// zeroed by the caller) or nullptr to switch it off.
+constexpr uint32_t kClockWords = 8 * 32;
+hipError_t set_clock_probe(unsigned long long* p, hipStream_t s);
 // out[0] / out[1] = min / max of len[i] / 64 over the batch (2 u32 on the
 // device); part: scratch of locate_part_words(n) u32
 hipError_t launch_len_range(const uint64_t* len, uint64_t n, unsigned int* out, uint32_t* part, hipStream_t s);

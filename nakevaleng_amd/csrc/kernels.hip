@@ -45,6 +45,40 @@ __device__ unsigned long long* g_diag = nullptr;
     } while (0)
 #endif
 
+// Clock probe (NKV_TIMING_CLOCK; bench.py's sclk_mhz).  Each wave of a leaf
+// kernel adds its lifetime in shader-clock cycles (s_memtime) and in 100 MHz
+// reference ticks (s_memrealtime) to slot[0] / slot[1] and counts itself in
+// slot[2] (slot = g_clk + 32 (workgroup % 8)); the host divides the sums: the
+// shader clock the kernel's waves ran at, weighted by their lifetimes.  Off
+// (g_clk null) it costs one uniform load.
+__device__ unsigned long long* g_clk = nullptr;
+struct ClockProbe {
+    unsigned long long* p;
+    uint64_t c0 = 0, r0 = 0;
+    __device__ __forceinline__ ClockProbe() : p(g_clk) {
+        if (p) {
+            c0 = __builtin_amdgcn_s_memtime();
+            r0 = __builtin_amdgcn_s_memrealtime();
+        }
+    }
+    __device__ __forceinline__ void end() const {
+        if (p) {
+            const uint64_t c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+            if ((threadIdx.x & 63) == 0) {  // 8 slots on their own 256-B lines: little contention
+                unsigned long long* q = p + 32 * (blockIdx.x & 7);
+                atomicAdd(q, (unsigned long long)(c1 - c0));
+                atomicAdd(q + 1, (unsigned long long)(r1 - r0));
+                atomicAdd(q + 2, 1ull);
+            }
+        }
+    }
+};
+
+hipError_t set_clock_probe(unsigned long long* p, hipStream_t s) {
+    (void)s;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_clk), &p, sizeof(p));
+}
+
 // KeySize and ValueSize (header bytes 14..29, record.go:191-199) of the
 // record at p, from two or three aligned 8-byte loads and a funnel shift
 // instead of sixteen byte loads (one line request per lane per load rather
@@ -252,43 +286,6 @@ struct NoRaw;
 template <bool ALIGNED, class Hook = NoRaw>
 __device__ __forceinline__ void sha1_tail(const uint8_t* p, uint64_t len, uint32_t h[5], Hook hook = Hook{});
 
-// Whole message in registers: full blocks with a one-block register prefetch
-// (aligned) or the 80-byte funnel window (unaligned), then the padding blocks.
-template <bool ALIGNED>
-__device__ __forceinline__ void sha1_value(const uint8_t* p, uint64_t len, uint32_t h[5]) {
-    sha1_init(h);
-    const uint64_t nfull = len >> 6;
-    uint32_t w[16];
-    const bool aligned = ALIGNED || __all((reinterpret_cast<uintptr_t>(p) & 15) == 0);
-    if (aligned) {
-        const uint4* q = reinterpret_cast<const uint4*>(p);
-        uint4 c[4];
-        if (nfull > 0) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) c[i] = q[i];
-        }
-        for (uint64_t b = 0; b < nfull; ++b) {
-            be16_from_raw(c, w);
-            if (b + 1 < nfull) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) c[i] = q[4 * (b + 1) + i];
-            }
-            sha1_compress(h, w);
-        }
-    } else {
-        // one-window register prefetch (the loads of block b+1 overlap block b)
-        const uint32_t s = uint32_t(reinterpret_cast<uintptr_t>(p) & 15);
-        uint32_t d[20];
-        if (nfull > 0) load_window(p, 64u, d);
-        for (uint64_t b = 0; b < nfull; ++b) {
-            be16_funnel(d, s, w);
-            if (b + 1 < nfull) load_window(p + 64 * (b + 1), 64u, d);
-            sha1_compress(h, w);
-        }
-    }
-    sha1_tail<ALIGNED>(p, len, h);
-}
-
 // The 1-2 padding blocks: rem = len % 64 value bytes, 0x80, zeros, 64-bit
 // big-endian bit length (FIPS 180-4 5.1.1).  h holds the state after the full
 // blocks.
@@ -450,26 +447,6 @@ __device__ __forceinline__ void sha1_blocks_lds(const uint8_t* wbuf, uint32_t nm
     }
 }
 
-// Full blocks straight from HBM into registers, 4 x global_load_dwordx4 per
-// block and lane (no LDS stage, no prefetch: the other resident waves cover
-// the load latency).  NT: non-temporal loads (read-once data).
-template <bool NT>
-__device__ __forceinline__ void sha1_blocks_direct(const uint8_t* p, uint32_t nfull, uint32_t h[5]) {
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-    const u32x4* q = reinterpret_cast<const u32x4*>(p);
-    uint32_t w[16];
-    for (uint32_t b = 0; b < nfull; ++b) {
-        uint4 c[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const u32x4 v = NT ? __builtin_nontemporal_load(q + 4 * b + i) : q[4 * b + i];
-            c[i] = make_uint4(v.x, v.y, v.z, v.w);
-        }
-        be16_from_raw(c, w);
-        sha1_compress(h, w);
-    }
-}
-
 // Full blocks in runs of S blocks: each lane loads S*64 contiguous bytes of its
 // value (4S x global_load_dwordx4) before compressing them, so every request
 // stream touches a DRAM page for a longer run.
@@ -497,132 +474,6 @@ __device__ __forceinline__ void sha1_blocks_runs(const uint8_t* p, uint32_t nful
     }
 }
 
-// Deep register prefetch for ragged batches: a long value is one chain of
-// dependent compressions, and while its wave runs nearly alone (the short waves
-// have finished) one block of lookahead cannot cover HBM latency under load.
-// D windows are in flight; the loop is unrolled by D so every buffer index is
-// static.  Aligned: 4 chunks per window; unaligned: 5 chunks + v_perm funnel.
-template <bool ALIGNED, int D>
-__device__ __forceinline__ void sha1_blocks_deep(const uint8_t* p, uint32_t nfull, uint32_t h[5]) {
-    constexpr int C = ALIGNED ? 4 : 5;
-    const uint32_t s = ALIGNED ? 0u : uint32_t(reinterpret_cast<uintptr_t>(p) & 15);
-    const uint4* q0 = reinterpret_cast<const uint4*>(p - s);
-    uint4 buf[D][C];
-    auto load = [&](int slot, uint32_t b) {
-#pragma unroll
-        for (int c = 0; c < C; ++c)
-            buf[slot][c] = (c < 4 || s > 0) ? q0[4 * b + c] : make_uint4(0u, 0u, 0u, 0u);
-    };
-    auto use = [&](int slot, uint32_t w[16]) {
-        if (ALIGNED) {
-            be16_from_raw(buf[slot], w);
-        } else {
-            uint32_t d[20];
-#pragma unroll
-            for (int c = 0; c < 5; ++c) {
-                d[4 * c] = buf[slot][c].x;
-                d[4 * c + 1] = buf[slot][c].y;
-                d[4 * c + 2] = buf[slot][c].z;
-                d[4 * c + 3] = buf[slot][c].w;
-            }
-            be16_funnel(d, s, w);
-        }
-    };
-#pragma unroll
-    for (int i = 0; i < D; ++i)
-        if (uint32_t(i) < nfull) load(i, uint32_t(i));
-    uint32_t b = 0;
-    for (; b + D <= nfull; b += D) {
-#pragma unroll
-        for (int i = 0; i < D; ++i) {
-            uint32_t w[16];
-            use(i, w);
-            if (b + i + D < nfull) load(i, b + i + D);
-            sha1_compress(h, w);
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < D - 1; ++i) {
-        if (b + i < nfull) {
-            uint32_t w[16];
-            use(i, w);
-            sha1_compress(h, w);
-        }
-    }
-}
-
-// Ragged values of any alignment through a wave-private LDS ring of aligned
-// 64-B chunks (two 4 KiB slots; chunk c of every value in slot c & 1).  DMA
-// role as in the LOAD 1 path: wave-instruction k moves one chunk of values
-// 16k .. 16k+15, 64 contiguous bytes each, so one instruction touches 16
-// segments instead of 64 scattered 16-B pieces.  Block b of a value at byte
-// offset o = p & 63 spans chunks b and b+1: the lane reads the five quads
-// holding bytes [o, o + 64) and funnels them by o & 15.  Chunk b+2 goes into
-// block b's slot once its reads are done, so one block of compute (and the
-// other resident waves) covers the DMA.  Only chunks holding full-block bytes
-// are fetched: an aligned 64-B chunk with one valid byte lies in that byte's
-// page, so nothing outside the value's pages is read.
-__device__ __forceinline__ void sha1_blocks_ring(uint8_t* wbuf, const uint8_t* p, uint32_t my_nfull,
-                                                 uint32_t h[5]) {
-    const int lane = threadIdx.x & 63;
-    const uint32_t o = uint32_t(reinterpret_cast<uintptr_t>(p)) & 63u;
-    const uint32_t nch = my_nfull ? my_nfull + (o != 0u) : 0u;
-    const uint32_t dq = (uint32_t(lane) & 3u) ^ ((uint32_t(lane) >> 4) & 3u);
-    const uint8_t* src[4];
-    uint32_t nc[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int j = 16 * k + (lane >> 2);
-        const uint64_t aj = uint64_t(__shfl(int64_t(reinterpret_cast<uintptr_t>(p - o)), j));
-        src[k] = reinterpret_cast<const uint8_t*>(aj) + 16 * dq;
-        nc[k] = uint32_t(__shfl(int(nch), j));
-    }
-    const uint32_t nmax = wave_max_u32(my_nfull);
-    if (nmax == 0) return;
-    auto issue = [&](uint32_t c) {
-        uint8_t* dst = wbuf + 4096 * (c & 1u);
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if (c < nc[k]) __builtin_amdgcn_global_load_lds(src[k] + 64ull * c, dst + 1024 * k, 16, 0, 0);
-    };
-    // byte offset in wbuf of quad i of the window for an even block; an odd
-    // block swaps the slots (bit 12)
-    const uint32_t swz = (uint32_t(lane) >> 2) & 3u;
-    uint32_t ro[5];
-#pragma unroll
-    for (int i = 0; i < 5; ++i) {
-        const uint32_t qi = (o >> 4) + uint32_t(i);
-        ro[i] = (qi >> 2) * 4096u + 64u * uint32_t(lane) + 16u * ((qi & 3u) ^ swz);
-    }
-    const uint32_t s = o & 15u;
-    issue(0u);
-    issue(1u);
-    for (uint32_t b = 0; b < nmax; ++b) {
-        const uint32_t flip = (b & 1u) << 12;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // chunks b, b+1 landed (explicit, see sha1_blocks_lds)
-        uint32_t d[20];
-#pragma unroll
-        for (int i = 0; i < 5; ++i) {
-            const uint4 c = *reinterpret_cast<const uint4*>(wbuf + (ro[i] ^ flip));
-            d[4 * i] = c.x;
-            d[4 * i + 1] = c.y;
-            d[4 * i + 2] = c.z;
-            d[4 * i + 3] = c.w;
-        }
-        uint32_t w[16];
-        be16_funnel(d, s, w);
-        if (b + 2 <= nmax) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot reads done before refill
-            issue(b + 2);
-        }
-        if (b < my_nfull) sha1_compress(h, w);
-    }
-}
-
-// Source of the DMA lanes whose value has no chunk c: every ring issue then
-// moves exactly four wave-instructions, so vmcnt counts are static.
-__device__ __attribute__((aligned(64))) uint8_t g_ring_dummy[64];
-
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ u32x4 ds_read_b128_asm(uint32_t addr) {
@@ -635,104 +486,6 @@ __device__ __forceinline__ u32x4 ds_read_b128_off(uint32_t addr) {
     u32x4 v;
     asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF) : "memory");
     return v;
-}
-
-// The ring above with R >= 3 slots and explicit waits, software-pipelined:
-// while block b is compressed, the DMA of chunk b+R and the LDS reads of window
-// b+1 are in flight, and chunk b+2 (read for window b+1) was issued R-2
-// blocks earlier.  The compiler's own waits would be vmcnt(0) before every LDS
-// read (it cannot tell ring slots apart), so the window reads are inline asm
-// and the waits are explicit:
-//   - vmcnt(4 (R-2)) before reading window b+1: chunks b+1, b+2 landed, the
-//     R-2 younger chunks (b+3 .. b+R, four wave-instructions each) may fly;
-//   - lgkmcnt(0) after block b's compression, carried through window b+1's
-//     registers (in/out asm operands, so no copy of them is scheduled before
-//     the wait), which also frees chunk b+1's slot for the next issue.
-// Every issue moves four wave-instructions (lanes past their value read
-// g_ring_dummy), and the ring drains (vmcnt(0)) before the slots are reused.
-template <int R>
-__device__ __forceinline__ void sha1_blocks_ring_pipe(uint8_t* wbuf, const uint8_t* p, uint32_t my_nfull,
-                                                      uint32_t h[5]) {
-    static_assert(R >= 3 && R <= 4, "ring depth");
-    const int lane = threadIdx.x & 63;
-    const uint32_t o = uint32_t(reinterpret_cast<uintptr_t>(p)) & 63u;
-    const uint32_t nch = my_nfull ? my_nfull + (o != 0u) : 0u;
-    const uint32_t dq = (uint32_t(lane) & 3u) ^ ((uint32_t(lane) >> 4) & 3u);
-    const uint8_t* src[4];
-    uint32_t nc[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int j = 16 * k + (lane >> 2);
-        const uint64_t aj = uint64_t(__shfl(int64_t(reinterpret_cast<uintptr_t>(p - o)), j));
-        src[k] = reinterpret_cast<const uint8_t*>(aj) + 16 * dq;
-        nc[k] = uint32_t(__shfl(int(nch), j));
-    }
-    const uint32_t nmax = wave_max_u32(my_nfull);
-    if (nmax == 0) return;
-    const uint8_t* dummy = g_ring_dummy + 16 * dq;
-    auto issue = [&](uint32_t c) {
-        uint8_t* dst = wbuf + 4096 * (c % R);
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            __builtin_amdgcn_global_load_lds(c < nc[k] ? src[k] + 64ull * c : dummy, dst + 1024 * k, 16, 0, 0);
-    };
-    const uint32_t lds0 = uint32_t(reinterpret_cast<uintptr_t>(wbuf));
-    const uint32_t swz = (uint32_t(lane) >> 2) & 3u;
-    // quad i of window b: chunk b + (qi >> 2), quad (qi & 3) ^ swz of this lane's row
-    uint32_t qoff[5], qch[5];
-#pragma unroll
-    for (int i = 0; i < 5; ++i) {
-        const uint32_t qi = (o >> 4) + uint32_t(i);
-        qch[i] = qi >> 2;
-        qoff[i] = 64u * uint32_t(lane) + 16u * ((qi & 3u) ^ swz);
-    }
-    // chunk b's slot is uniform; a lane's quads from chunk b+1 add the (uniform)
-    // distance to the next slot
-    auto read_window = [&](uint32_t b, u32x4 v[5]) {
-        const uint32_t s0 = lds0 + 4096u * (b % R);
-        const uint32_t s1 = lds0 + 4096u * ((b + 1) % R);
-#pragma unroll
-        for (int i = 0; i < 5; ++i) v[i] = ds_read_b128_asm(qoff[i] + (qch[i] ? s1 : s0));
-    };
-    const uint32_t s = o & 15u;
-#pragma unroll
-    for (uint32_t c = 0; c < uint32_t(R); ++c) issue(c);
-    if (R == 3) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    // The lgkmcnt wait names the ds_read destinations as in/out operands, so
-    // no copy or use of them can be scheduled before it.
-    u32x4 cur[5];
-    read_window(0u, cur);
-    asm volatile("s_waitcnt lgkmcnt(0)"
-                 : "+v"(cur[0]), "+v"(cur[1]), "+v"(cur[2]), "+v"(cur[3]), "+v"(cur[4])
-                 :
-                 : "memory");
-    for (uint32_t b = 0; b < nmax; ++b) {
-        issue(b + R);
-        if (R == 3) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        u32x4 nxt[5];
-        read_window(b + 1, nxt);
-        uint32_t d[20];
-#pragma unroll
-        for (int i = 0; i < 5; ++i) {
-            d[4 * i] = cur[i].x;
-            d[4 * i + 1] = cur[i].y;
-            d[4 * i + 2] = cur[i].z;
-            d[4 * i + 3] = cur[i].w;
-        }
-        uint32_t w[16];
-        be16_funnel(d, s, w);
-        if (b < my_nfull) sha1_compress(h, w);
-        asm volatile("s_waitcnt lgkmcnt(0)"
-                     : "+v"(nxt[0]), "+v"(nxt[1]), "+v"(nxt[2]), "+v"(nxt[3]), "+v"(nxt[4])
-                     :
-                     : "memory");
-#pragma unroll
-        for (int i = 0; i < 5; ++i) cur[i] = nxt[i];
-    }
-    // every DMA must land before the slots are reused
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 template <int N>
@@ -856,32 +609,25 @@ __device__ __forceinline__ void sha1_blocks_ring_vc(uint8_t* wbuf, const uint8_t
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// LOAD 9: line-pair stage for values that are not 64-byte aligned (records in a
-// Data table: the Value starts 30 + KeySize bytes into its record).  Block b of
-// a value is bytes [o + 64 b, o + 64 b + 64) of its aligned line pair
-// [A + 64 b, A + 64 b + 128), A = p & ~63, o = p & 63.  Eight LDS-DMA
-// instructions per block move the pairs of all 64 values: instruction k
-// serves values 8k .. 8k+7, lane l quad (l & 7) of value 8k + (l >> 3), so
-// value j's pair lands contiguously at wbuf + 128 j and the lane reads its
-// window with four byte-unaligned ds_read_b128 (no register funnel).  Every
-// DMA source is 16-byte aligned and inside a line that holds bytes of the
-// value's block (quads past o + 63 are clamped to the last needed one), so no
-// request straddles two lines.  The addresses are one 32-bit offset per role
-// from a wave-uniform base plus the uniform 64 b; this needs every live value
-// of the wave to have the same full-block count and the wave's pairs to lie
-// within 4 GiB of the base.  Otherwise it returns false and does nothing (the
-// caller runs the LOAD 8 stream).  Stage: 8 KiB per wave.
-
-// kWindow (LOAD 10): the same stream with only each value's 80-byte window row
-// (five aligned quads from (o & ~15), clamped like the pair's), so a wave's
-// stage is 5 KiB, five DMA instructions move a block (quad g = 64 k + l of
-// instruction k is quad g % 5 of value g / 5), and eight waves per SIMD fit
-// the 160 KiB LDS (eight 20 KiB workgroups per CU).
-// kWindow is a literal at every call site (the function is inlined and folded).
-__device__ __forceinline__ bool sha1_blocks_pair(const bool kWindow, uint8_t* wbuf, const uint8_t* p, bool live, uint32_t my_nfull,
+// The 80-byte window stage for values that are not 64-byte aligned and whose
+// full-block counts are equal across the wave (records of one size whose
+// offsets mod 64 differ).  Block b of a value at o = p & 63 lies in the five
+// aligned quads from (p & ~15) + 64 b; five LDS-DMA instructions per block
+// fetch them for all 64 values (quad g = 64 k + l of instruction k is quad
+// g % 5 of value g / 5; quads past o + 63 are clamped to the last needed one,
+// so every request is aligned, inside one line, and inside a line that holds
+// bytes of the value's block).  Value j's row is 80 contiguous bytes at wbuf +
+// 80 j, and the lane reads its 64-byte window with four byte-unaligned
+// ds_read_b128 at 80 j + (o & 15): no register funnel, 16 v_perm per block as
+// in the aligned path.  The addresses are a 32-bit offset per role from a
+// wave-uniform base plus the uniform 64 b (the wave's rows must lie within 4
+// GiB of the base).  Stage: 5 KiB per wave (eight waves per SIMD fit the 160 KiB
+// LDS).  Returns false, doing nothing, when the wave does not qualify; the
+// caller then runs the value-relative stream.
+__device__ __forceinline__ bool sha1_blocks_pair(uint8_t* wbuf, const uint8_t* p, bool live, uint32_t my_nfull,
                                                  uint32_t h[5]) {
-    const int kDma = kWindow ? 5 : 8;          // DMA instructions per block
-    const uint32_t kRow = kWindow ? 80u : 128u;
+    constexpr int kDma = 5;  // DMA instructions per block
+    constexpr uint32_t kRow = 80u;
     const int lane = threadIdx.x & 63;
     const uint32_t nmax = wave_max_u32(live ? my_nfull : 0u);
     if (nmax == 0) return true;  // no live value has a full block
@@ -894,27 +640,25 @@ __device__ __forceinline__ bool sha1_blocks_pair(const bool kWindow, uint8_t* wb
     const uint8_t* base = reinterpret_cast<const uint8_t*>(wb);
     // lane 0 is live whenever any lane is (dead lanes are the grid's tail), so
     // dead values' roles re-read lane 0's quads into their unused rows
-    uint32_t voff[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    uint32_t voff[kDma];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        if (k >= kDma) break;
+    for (int k = 0; k < kDma; ++k) {
         const uint32_t g = 64u * uint32_t(k) + uint32_t(lane);
-        const int j = kWindow ? int(g / 5u) : 8 * k + (lane >> 3);
-        const uint32_t qi = kWindow ? g - 5u * uint32_t(j) : uint32_t(lane) & 7u;
+        const int j = int(g / 5u);
+        const uint32_t qi = g - 5u * uint32_t(j);
         const bool lj = __shfl(int(live), j) != 0;
         const uint32_t src = lj ? uint32_t(j) : 0u;
         const uint32_t rj = uint32_t(__shfl(int(uint32_t(rel)), int(src)));
         const uint32_t oj = uint32_t(__shfl(int(o), int(src)));
         const uint32_t qlast = (oj + 63u) >> 4;
-        voff[k] = rj + 16u * min((kWindow ? (oj >> 4) : 0u) + qi, qlast);
+        voff[k] = rj + 16u * min((oj >> 4) + qi, qlast);
     }
     auto issue = [&](uint32_t b) {
         const uint32_t cb = 64u * b;
 #pragma unroll
-        for (int k = 0; k < 8; ++k)
-            if (k < kDma) __builtin_amdgcn_global_load_lds(base + (voff[k] + cb), wbuf + 1024 * k, 16, 0, 0);
+        for (int k = 0; k < kDma; ++k) __builtin_amdgcn_global_load_lds(base + (voff[k] + cb), wbuf + 1024 * k, 16, 0, 0);
     };
-    const uint32_t rd = uint32_t(reinterpret_cast<uintptr_t>(wbuf)) + kRow * uint32_t(lane) + (kWindow ? (o & 15u) : o);
+    const uint32_t rd = uint32_t(reinterpret_cast<uintptr_t>(wbuf)) + kRow * uint32_t(lane) + (o & 15u);
     issue(0u);
     for (uint32_t b = 0; b < nmax; ++b) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1009,9 +753,6 @@ __device__ __forceinline__ bool sha1_blocks_shift(uint8_t* wbuf, const uint8_t* 
     const uint32_t q = o0 >> 2;
     const uint32_t sel = be_sel(o0 & 3u);
     uint32_t a[16], b[16], w[16];
-#ifndef NKV_SHIFT_REGS
-#define NKV_SHIFT_REGS 0  // experiment builds: segments straight into registers, no LDS-DMA stage
-#endif
     // Whole 128-byte lines into registers: when every live value's segment 0
     // starts a line and the block counts are equal, each lane loads its aligned
     // lines (two segments, eight 16-byte loads) once, no LDS.  Three segment
@@ -1049,7 +790,7 @@ __device__ __forceinline__ bool sha1_blocks_shift(uint8_t* wbuf, const uint8_t* 
         }
         return true;
     }
-    if (!NKV_SHIFT_REGS && wbuf && __all(!live || my_nfull == nmax)) {
+    if (wbuf && __all(!live || my_nfull == nmax)) {
         // Equal block counts: the segments go HBM -> LDS by LDS-DMA, one segment
         // of lookahead, in k_leaf's aligned stage layout (value j's segment at
         // wbuf + 64 j, chunks XOR-swizzled; sha1_blocks_lds), then into the
@@ -1171,7 +912,7 @@ template <bool LINES = false>
 __device__ __forceinline__ void sha1_blocks_any(uint8_t* wbuf, const uint8_t* p, bool live, uint32_t my_nfull,
                                                 uint32_t h[5]) {
     if (sha1_blocks_shift<NoRaw, LINES>(wbuf, p, live, my_nfull, h)) return;
-    if (sha1_blocks_pair(true, wbuf, p, live, my_nfull, h)) return;
+    if (sha1_blocks_pair(wbuf, p, live, my_nfull, h)) return;
     const int lane = threadIdx.x & 63;
     const uint32_t q = (uint32_t(lane) & 3u) ^ ((uint32_t(lane) >> 4) & 3u);
     const uint8_t* src[4];
@@ -1193,31 +934,35 @@ __device__ __forceinline__ void sha1_blocks_any(uint8_t* wbuf, const uint8_t* p,
 
 
 // MODE 0: value i at base + i*stride, length L.  MODE 1: base + off[i], len[i].
-// perm (MODE 1 only, nullable): lane i hashes leaf perm[i] (length bucketing).
+// perm (MODE 1 only, nullable): lane i hashes leaf perm[i]; a pass after
+// k_leaf_records skips the values it hashed (off == kDone).
 // No tree level is fused here: a wave-level step costs a whole SHA-1
 // instruction stream however few lanes it keeps, so levels built inside the
 // leaf kernel (6 per wave, or the workgroup's last wave finishing its 256-leaf
 // subtree) cost 3-7 % of a 4 KiB leaf launch, more than k_reduce2 at full lane
 // use plus its launch.
-// LOAD: 0 = any alignment (register funnel); 1 = 16-byte aligned, LDS-DMA
-// stage; 2 = aligned, direct loads; 3 = aligned, direct non-temporal loads.
-#ifndef NKV_RUNS_WAVES
-#define NKV_RUNS_WAVES 4  // waves per SIMD of the run-load paths (LOAD 4, 5)
-#endif
+// LOAD 4: 16-byte aligned values in 128-byte runs straight into registers
+// (sha1_blocks_runs<2>: eight global_load_dwordx4 per lane, every 128-byte line
+// fetched once by one lane; 65 VGPRs, 7 waves per SIMD).  LOAD 11: values at
+// any address, each wave by the first stage that fits it: the segment stage
+// when its values share their offset mod 64 (sha1_blocks_shift), the 80-byte
+// window stage when their full-block counts are equal (sha1_blocks_pair), else
+// the value-relative LDS-DMA stream (sha1_blocks_lds).  The other load paths
+// measured in rounds 1-2 (LDS-DMA stage for aligned values, direct and
+// non-temporal loads, 256-byte runs, line-pair stage, runs at each value's own
+// address, deep register prefetch) lost their A/Bs and are gone.
+constexpr int kRunsWaves = 4;  // launch bound of the LOAD 4 kernel
 template <int MODE, int LOAD>
-__global__ __launch_bounds__(kBlock, (LOAD == 6 || LOAD == 7) ? 2 : ((LOAD == 4 || LOAD == 5 || LOAD == 12) ? NKV_RUNS_WAVES : (LOAD == 9 ? 5 : kLeafWavesPerSimd))) void k_leaf(const uint8_t* __restrict__ base,
-                                                  const uint64_t* __restrict__ off,
-                                                  const uint64_t* __restrict__ len, uint64_t stride,
-                                                  uint64_t L, const uint32_t* __restrict__ perm,
-                                                  uint64_t n, uint8_t* __restrict__ nodes, Gate gate) {
-    // 16 KiB: four wave-private 4 KiB LDS-DMA stages (LOAD 1, 8); 8 KiB each for LOAD 9, 5 KiB for LOAD 10
-#ifndef NKV_LEAF_LDS_PAD
-#define NKV_LEAF_LDS_PAD 0  // experiment builds only: extra LDS per workgroup to cap occupancy
-#endif
-    __shared__ __attribute__((aligned(16))) uint8_t
-        smem[kBlock * (LOAD == 9 ? 128 : (LOAD == 10 || LOAD == 11 ? 80 : 64)) + NKV_LEAF_LDS_PAD];
+__global__ __launch_bounds__(kBlock, LOAD == 4 ? kRunsWaves : kLeafWavesPerSimd) void k_leaf(
+    const uint8_t* __restrict__ base, const uint64_t* __restrict__ off, const uint64_t* __restrict__ len,
+    uint64_t stride, uint64_t L, const uint32_t* __restrict__ perm, uint64_t n, uint8_t* __restrict__ nodes,
+    Gate gate) {
+    static_assert(LOAD == 4 || LOAD == 11, "leaf load path");
+    // LOAD 11: four wave-private 5 KiB stages (the window stage's 80-byte rows)
+    __shared__ __attribute__((aligned(16))) uint8_t smem[LOAD == 11 ? kBlock * 80 : 16];
     if (!gate.open()) return;
     NKV_STAMP(0);
+    const ClockProbe clk;
     const uint64_t g = blockIdx.x;
     const uint64_t t = g * kBlock + threadIdx.x;
     uint32_t h[5] = {0u, 0u, 0u, 0u, 0u};
@@ -1236,36 +981,25 @@ __global__ __launch_bounds__(kBlock, (LOAD == 6 || LOAD == 7) ? 2 : ((LOAD == 4 
             ln = len[leaf];
         }
     }
-    if ((LOAD >= 2 && LOAD <= 7) || LOAD == 12) {
-        sha1_init(h);
+    sha1_init(h);
+    if constexpr (LOAD == 4) {
         if (live) {
-            if (LOAD == 2) sha1_blocks_direct<false>(p, uint32_t(ln >> 6), h);
-            else if (LOAD == 3) sha1_blocks_direct<true>(p, uint32_t(ln >> 6), h);
-            else if (LOAD == 4 || LOAD == 12) sha1_blocks_runs<2>(p, uint32_t(ln >> 6), h);
-            else if (LOAD == 5) sha1_blocks_runs<4>(p, uint32_t(ln >> 6), h);
-            else if (LOAD == 6) sha1_blocks_deep<true, 4>(p, uint32_t(ln >> 6), h);
-            else sha1_blocks_deep<false, 4>(p, uint32_t(ln >> 6), h);
-            if (LOAD == 7 || LOAD == 12) sha1_tail<false>(p, ln, h);
-            else sha1_tail<true>(p, ln, h);
+            sha1_blocks_runs<2>(p, uint32_t(ln >> 6), h);
+            sha1_tail<true>(p, ln, h);
             store_digest(nodes, leaf, h);
         }
-    } else if (LOAD == 1 || LOAD == 8 || LOAD == 9 || LOAD == 10 || LOAD == 11) {
-        // wave-cooperative LDS-DMA stream of the full blocks, then the tail.
-        // The DMA reads each value's own blocks at the value's address, so it
-        // serves any alignment (LOAD 8: unaligned values, unaligned tail); only
-        // full blocks are fetched, so every byte read belongs to the value.
+    } else {
+        // wave-cooperative stages of the full blocks, then the tail.  Every
+        // stage reads only full blocks' bytes, so nothing past a value is read.
         const int lane = threadIdx.x & 63;
         const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-        uint8_t* wbuf = smem + (LOAD == 9 ? 8192 : (LOAD == 10 || LOAD == 11 ? 5120 : 4096)) * wave;
+        uint8_t* wbuf = smem + 5120 * wave;
         const uint32_t q = (uint32_t(lane) & 3u) ^ ((uint32_t(lane) >> 4) & 3u);
         const uint32_t my_nfull = live ? uint32_t(ln >> 6) : 0u;
-        sha1_init(h);
-        bool staged = false;
-        if constexpr (LOAD == 11) staged = sha1_blocks_shift(wbuf, p, live, my_nfull, h);
-        if constexpr (LOAD == 9 || LOAD == 10 || LOAD == 11)
-            if (!staged) staged = sha1_blocks_pair(LOAD != 9, wbuf, p, live, my_nfull, h);
+        bool staged = sha1_blocks_shift(wbuf, p, live, my_nfull, h);
+        if (!staged) staged = sha1_blocks_pair(wbuf, p, live, my_nfull, h);
         if (staged) {
-            // line-pair stage done (wave-uniform)
+            // done (wave-uniform)
         } else if (MODE == 0) {
             // value j of this wave at wave_base + j * stride (32-bit offsets:
             // saddr-form DMA, one VGPR of addressing)
@@ -1301,7 +1035,7 @@ __global__ __launch_bounds__(kBlock, (LOAD == 6 || LOAD == 7) ? 2 : ((LOAD == 4 
             };
             sha1_blocks_lds(wbuf, wave_max_u32(my_nfull), my_nfull, issue, h);
         }
-        if constexpr (LOAD == 11 && MODE == 1) {
+        if constexpr (MODE == 1) {
             // reload the value's place instead of keeping it live through the
             // register stage (its two 16-dword segment sets need the VGPRs)
             asm volatile("" ::: "memory");
@@ -1312,13 +1046,11 @@ __global__ __launch_bounds__(kBlock, (LOAD == 6 || LOAD == 7) ? 2 : ((LOAD == 4 
             }
         }
         if (live) {
-            sha1_tail<LOAD == 1>(p, ln, h);
+            sha1_tail<false>(p, ln, h);
             store_digest(nodes, leaf, h);
         }
-    } else if (live) {
-        sha1_value<false>(p, ln, h);
-        store_digest(nodes, leaf, h);
     }
+    clk.end();
     NKV_STAMP(1);
     NKV_STAMP(2);
 #ifdef NKV_DIAG
@@ -1385,18 +1117,14 @@ struct CrcBE {
 // voff / vlen for the length-sorted leaf pass; a hashed value's voff becomes
 // kDone.  Each workgroup leaves (0, deferred ? ~0 : 0, 0) in part, folded by
 // k_locate_fold into the range whose wide Gate opens the sorted pass.
-#ifndef NKV_VERIFY_LINES
-#define NKV_VERIFY_LINES 1  // whole 128-byte lines into registers for line-aligned records (as k_leaf_records)
-#endif
-#ifndef NKV_VERIFY_WAVES
-#define NKV_VERIFY_WAVES (NKV_VERIFY_LINES ? 4 : 7)  // the line path with the CRC state takes ~105 VGPRs
-#endif
-__global__ __launch_bounds__(kBlock, NKV_VERIFY_WAVES) void k_leaf_verify(
+constexpr int kVerifyWaves = 4;  // whole lines in registers with the CRC state: ~105 VGPRs
+__global__ __launch_bounds__(kBlock, kVerifyWaves) void k_leaf_verify(
     const uint8_t* __restrict__ stream, uint64_t stream_len, const uint64_t* __restrict__ rec_off, uint64_t n,
     int policy, uint64_t* __restrict__ voff, uint64_t* __restrict__ vlen, uint8_t* __restrict__ nodes,
     uint32_t* __restrict__ crc_out, unsigned long long* __restrict__ stats, uint32_t* __restrict__ part,
     uint32_t* __restrict__ flags, uint32_t* __restrict__ flags_next) {
     if (flags) pass_flags_reset(flags_next);
+    const ClockProbe clk;
     // ONE LDS object (a second one can cost the DMA loop its waits): four
     // 4 KiB wave stages, the 4 KiB of byte-swapped word tables (CrcBE), then
     // T[0] for the bytewise steps: 21 KiB, seven workgroups per CU
@@ -1483,7 +1211,7 @@ __global__ __launch_bounds__(kBlock, NKV_VERIFY_WAVES) void k_leaf_verify(
         };
         // records of one size share their offset mod 64: each line once
         // through the segment stage (LOAD 11); else the value-relative stream
-        if (!sha1_blocks_shift<decltype(hook), NKV_VERIFY_LINES != 0>(wbuf, p, live, my_nfull, h, hook))
+        if (!sha1_blocks_shift<decltype(hook), true>(wbuf, p, live, my_nfull, h, hook))
             sha1_blocks_lds(wbuf, whi, my_nfull, issue, h, hook);
         if (live) {
             sha1_tail<false>(p, ln, h, hook);  // the tail's checksum from the same loads
@@ -1530,6 +1258,7 @@ __global__ __launch_bounds__(kBlock, NKV_VERIFY_WAVES) void k_leaf_verify(
             }
         }
     }
+    clk.end();
 }
 
 // K1q: ragged batches, work-queue form.  Values are length-sorted, longest
@@ -1554,22 +1283,20 @@ __global__ __launch_bounds__(kBlock, NKV_VERIFY_WAVES) void k_leaf_verify(
 constexpr uint32_t kSimdKeys = 8 * 8 * 2 * 16 * 4;  // xcc, se, sh, cu, simd
 constexpr uint32_t kQueueHeader = 8;  // tickets, first short group, pad, work (u64), pad
 
-// LOAD 6 / 7: deep register prefetch (aligned / any alignment); 8: LDS chunk
-// ring, 2 slots; 9 / 10: pipelined LDS ring, 3 / 4 slots (12 / 16 KiB per wave);
-// 11 / 12 / 13: pipelined ring of value-relative chunks, 2 / 3 / 4 slots.
-template <int LOAD>
-constexpr int queue_ring_slots() {
-    return LOAD == 8 || LOAD == 11 ? 2 : (LOAD == 9 || LOAD == 12 ? 3 : (LOAD == 10 || LOAD == 13 ? 4 : 0));
-}
-template <int LOAD>
-__global__ __launch_bounds__(64, queue_ring_slots<LOAD>() == 4 ? 2 : (queue_ring_slots<LOAD>() == 3 ? 3 : (queue_ring_slots<LOAD>() == 2 ? 4 : 2))) void k_leaf_queue(const uint8_t* __restrict__ base,
+// Values are staged through a pipelined wave-private LDS ring of
+// value-relative chunks (sha1_blocks_ring_vc, kQueueRing = 3 slots of 4 KiB:
+// two blocks of DMA lookahead; 3 waves per SIMD fit).  The other rings and the
+// register-prefetch forms of rounds 1-2 lost their A/Bs.
+constexpr int kQueueRing = 3;
+__global__ __launch_bounds__(64, kQueueRing) void k_leaf_queue(const uint8_t* __restrict__ base,
                                                        const uint64_t* __restrict__ off,
                                                        const uint64_t* __restrict__ len,
                                                        const uint32_t* __restrict__ perm, uint64_t n,
                                                        uint32_t ngroups, uint32_t simds, uint32_t* __restrict__ q,
                                                        uint8_t* __restrict__ nodes, Gate gate) {
-    __shared__ __attribute__((aligned(16))) uint8_t smem[queue_ring_slots<LOAD>() ? 4096 * queue_ring_slots<LOAD>() : 16];
+    __shared__ __attribute__((aligned(16))) uint8_t smem[4096 * kQueueRing];
     if (!gate.open()) return;
+    const ClockProbe clk;
     const int lane = threadIdx.x;
     uint32_t hw, xcc;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
@@ -1606,30 +1333,16 @@ __global__ __launch_bounds__(64, queue_ring_slots<LOAD>() == 4 ? 2 : (queue_ring
         g = __builtin_amdgcn_readfirstlane(g);
         if (g == 0xFFFFFFFFu) break;
         const uint64_t i = uint64_t(g) * 64 + lane;
-        if constexpr (LOAD >= 8) {
-            const uint64_t leaf = i < n ? perm[i] : 0;
-            const uint64_t vo = i < n ? off[leaf] : kDone;
-            const bool live = vo != kDone;  // kDone: hashed by k_leaf_records
-            const uint8_t* p = live ? base + vo : base;
-            const uint64_t ln = live ? len[leaf] : 0;
-            uint32_t h[5];
-            sha1_init(h);
-            if constexpr (LOAD == 8) sha1_blocks_ring(smem, p, uint32_t(ln >> 6), h);
-            else if constexpr (LOAD <= 10) sha1_blocks_ring_pipe<queue_ring_slots<LOAD>()>(smem, p, uint32_t(ln >> 6), h);
-            else sha1_blocks_ring_vc<queue_ring_slots<LOAD>()>(smem, p, uint32_t(ln >> 6), h);
-            if (live) {
-                sha1_tail<false>(p, ln, h);
-                store_digest(nodes, leaf, h);
-            }
-        } else if (i < n && off[perm[i]] != kDone) {
-            const uint64_t leaf = perm[i];
-            const uint8_t* p = base + off[leaf];
-            const uint64_t ln = len[leaf];
-            uint32_t h[5];
-            sha1_init(h);
-            sha1_blocks_deep<LOAD == 6, 4>(p, uint32_t(ln >> 6), h);
-            if (LOAD == 6) sha1_tail<true>(p, ln, h);
-            else sha1_tail<false>(p, ln, h);
+        const uint64_t leaf = i < n ? perm[i] : 0;
+        const uint64_t vo = i < n ? off[leaf] : kDone;
+        const bool live = vo != kDone;  // kDone: hashed by k_leaf_records
+        const uint8_t* p = live ? base + vo : base;
+        const uint64_t ln = live ? len[leaf] : 0;
+        uint32_t h[5];
+        sha1_init(h);
+        sha1_blocks_ring_vc<kQueueRing>(smem, p, uint32_t(ln >> 6), h);
+        if (live) {
+            sha1_tail<false>(p, ln, h);
             store_digest(nodes, leaf, h);
         }
 #ifdef NKV_DIAG
@@ -1637,6 +1350,7 @@ __global__ __launch_bounds__(64, queue_ring_slots<LOAD>() == 4 ? 2 : (queue_ring
         if (d_groups++ == 0) d_first = __builtin_amdgcn_s_memrealtime();
 #endif
     }
+    clk.end();
 #ifdef NKV_DIAG
     if (g_diag && lane == 0) {
         unsigned long long* d = g_diag + size_t(blockIdx.x) * 8;
@@ -2056,21 +1770,14 @@ __global__ __launch_bounds__(kBlock) void k_locate_fold(const uint32_t* __restri
 // which k_locate_fold turns into err and a range whose wide Gate opens the
 // sorted pass only when something was deferred.  A header outside the
 // stream flags bad and hashes the empty value (as k_locate).
-#ifndef NKV_RECORDS_RUNS
-#define NKV_RECORDS_RUNS 0  // k_leaf_records hashes narrow waves from 128-byte register runs at each value's own address
-#endif
-#ifndef NKV_RECORDS_LINES
-#define NKV_RECORDS_LINES 1  // narrow waves of line-aligned records: whole 128-byte lines into registers
-#endif
-#ifndef NKV_RECORDS_WAVES
-#define NKV_RECORDS_WAVES (NKV_RECORDS_LINES ? 5 : kLeafWavesPerSimd)  // the line path takes ~86 VGPRs
-#endif
-__global__ __launch_bounds__(kBlock, NKV_RECORDS_RUNS ? NKV_RUNS_WAVES : NKV_RECORDS_WAVES) void k_leaf_records(
+constexpr int kRecordsWaves = 5;  // narrow waves of line-aligned records take whole lines: ~86 VGPRs
+__global__ __launch_bounds__(kBlock, kRecordsWaves) void k_leaf_records(
     const uint8_t* __restrict__ stream, uint64_t stream_len, const uint64_t* __restrict__ rec_off, uint64_t n,
     int policy, uint64_t* __restrict__ voff, uint64_t* __restrict__ vlen, uint8_t* __restrict__ nodes,
     uint32_t* __restrict__ part, uint32_t* __restrict__ flags, uint32_t* __restrict__ flags_next) {
     __shared__ __attribute__((aligned(16))) uint8_t smem[kBlock * 80];
     if (flags) pass_flags_reset(flags_next);
+    const ClockProbe clk;
     const uint64_t t = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
     const bool live = t < n;
     uint64_t o = 0, l = 0;
@@ -2106,8 +1813,7 @@ __global__ __launch_bounds__(kBlock, NKV_RECORDS_RUNS ? NKV_RUNS_WAVES : NKV_REC
         const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
         uint32_t h[5];
         sha1_init(h);
-        if (NKV_RECORDS_RUNS) sha1_blocks_runs<2>(stream + o, live ? b32 : 0u, h);
-        else sha1_blocks_any<NKV_RECORDS_LINES != 0>(smem + 5120 * wave, stream + o, live, live ? b32 : 0u, h);
+        sha1_blocks_any<true>(smem + 5120 * wave, stream + o, live, live ? b32 : 0u, h);
         // reload the value's place (written above by this lane) rather than
         // keeping it, or its addresses, live through the stage
         asm volatile("" ::: "memory");
@@ -2143,6 +1849,7 @@ __global__ __launch_bounds__(kBlock, NKV_RECORDS_RUNS ? NKV_RUNS_WAVES : NKV_REC
             part[3 * blockIdx.x + 2] = f & 1u;
         }
     }
+    clk.end();
 }
 
 // Range of full-block counts of a batch: out[0] = min, out[1] = max.  Lets
@@ -2223,47 +1930,26 @@ static void leaf_kernel(const uint8_t* base, const uint64_t* off, const uint64_t
                        perm, n, nodes, gate);
 }
 
+// load (NKV_OPT_LEAF_LOAD): 4 = 128-byte register runs for 16-byte aligned
+// values (anything else takes 11); 11 = the staged paths for every value
 template <int MODE>
-static void leaf_dispatch(int load, const uint8_t* base, const uint64_t* off, const uint64_t* len,
+static void leaf_dispatch(int load, bool aligned, const uint8_t* base, const uint64_t* off, const uint64_t* len,
                           uint64_t stride, uint64_t L, const uint32_t* perm, uint64_t n, uint8_t* nodes,
                           hipStream_t s, Gate g) {
-    switch (load) {
-        case 1: leaf_kernel<MODE, 1>(base, off, len, stride, L, perm, n, nodes, s, g); break;
-        case 2: leaf_kernel<MODE, 2>(base, off, len, stride, L, perm, n, nodes, s, g); break;
-        case 3: leaf_kernel<MODE, 3>(base, off, len, stride, L, perm, n, nodes, s, g); break;
-        case 4: leaf_kernel<MODE, 4>(base, off, len, stride, L, perm, n, nodes, s, g); break;
-        case 5: leaf_kernel<MODE, 5>(base, off, len, stride, L, perm, n, nodes, s, g); break;
-        case 6: leaf_kernel<MODE, 6>(base, off, len, stride, L, perm, n, nodes, s, g); break;
-        case 7: leaf_kernel<MODE, 7>(base, off, len, stride, L, perm, n, nodes, s, g); break;
-        case 8: leaf_kernel<MODE, 8>(base, off, len, stride, L, perm, n, nodes, s, g); break;
-        case 9: leaf_kernel<MODE, 9>(base, off, len, stride, L, perm, n, nodes, s, g); break;
-        case 10: leaf_kernel<MODE, 10>(base, off, len, stride, L, perm, n, nodes, s, g); break;
-        case 11: leaf_kernel<MODE, 11>(base, off, len, stride, L, perm, n, nodes, s, g); break;
-        case 12: leaf_kernel<MODE, 12>(base, off, len, stride, L, perm, n, nodes, s, g); break;
-        default: leaf_kernel<MODE, 0>(base, off, len, stride, L, perm, n, nodes, s, g); break;
-    }
+    if (load == 4 && aligned) leaf_kernel<MODE, 4>(base, off, len, stride, L, perm, n, nodes, s, g);
+    else leaf_kernel<MODE, 11>(base, off, len, stride, L, perm, n, nodes, s, g);
 }
 
 hipError_t launch_leaf_strided(const uint8_t* base, uint64_t stride, uint64_t L, uint64_t n, int load,
                                uint8_t* nodes, hipStream_t s) {
     const bool al = ((reinterpret_cast<uintptr_t>(base) | stride) & 15) == 0;
-    // Aligned values: 128-byte runs into registers (LOAD 4, the default) or the
-    // LDS-DMA stage (1).  Unaligned ones (direct loads need 16 B; LDS-DMA serves
-    // any alignment): the segment stage (LOAD 11) for waves whose values share
-    // their offset mod 64, else the 80-byte window stage (LOAD 10), else the
-    // value-relative stream
-    if (!al && load != 9 && load != 10 && load != 11 && load != 12) load = (load == 1 || load == 4) ? 11 : 0;
-    leaf_dispatch<0>(load, base, nullptr, nullptr, stride, L, nullptr, n, nodes, s, Gate{});
+    leaf_dispatch<0>(load, al, base, nullptr, nullptr, stride, L, nullptr, n, nodes, s, Gate{});
     return hipGetLastError();
 }
 
-hipError_t launch_leaf_offsets(const uint8_t* base, const uint64_t* off, const uint64_t* len,
-                               const uint32_t* perm, uint64_t n, bool aligned, int load, uint8_t* nodes,
-                               hipStream_t s, bool deep, Gate gate) {
-    if (perm && deep) load = aligned ? 6 : 7;  // ragged, length-sorted: deep prefetch
-    else if (!aligned && load != 9 && load != 10 && load != 11 && load != 12)
-        load = (load == 1 || load == 4) ? 11 : 0;  // as launch_leaf_strided
-    leaf_dispatch<1>(load, base, off, len, 0, 0, perm, n, nodes, s, gate);
+hipError_t launch_leaf_offsets(const uint8_t* base, const uint64_t* off, const uint64_t* len, uint64_t n,
+                               bool aligned, int load, uint8_t* nodes, hipStream_t s, Gate gate) {
+    leaf_dispatch<1>(load, aligned, base, off, len, 0, 0, nullptr, n, nodes, s, gate);
     return hipGetLastError();
 }
 
@@ -2281,27 +1967,13 @@ hipError_t launch_leaf_verify(const uint8_t* stream, uint64_t stream_len, const 
     return hipGetLastError();
 }
 
-hipError_t launch_leaf_queue(const uint8_t* base, const uint64_t* off, const uint64_t* len,
-                             const uint32_t* perm, uint64_t n, bool aligned, int ring, uint32_t* q,
-                             uint32_t simds, uint32_t waves_per_simd, uint8_t* nodes, hipStream_t s, Gate gate) {
+hipError_t launch_leaf_queue(const uint8_t* base, const uint64_t* off, const uint64_t* len, const uint32_t* perm,
+                             uint64_t n, uint32_t* q, uint32_t simds, uint32_t waves_per_simd, uint8_t* nodes,
+                             hipStream_t s, Gate gate) {
     const uint32_t ngroups = uint32_t((n + 63) / 64);
-    const uint32_t waves = simds * waves_per_simd;
-    if (ring == 14)
-        hipLaunchKernelGGL(k_leaf_queue<13>, dim3(waves), dim3(64), 0, s, base, off, len, perm, n, ngroups, simds, q, nodes, gate);
-    else if (ring == 13)
-        hipLaunchKernelGGL(k_leaf_queue<12>, dim3(waves), dim3(64), 0, s, base, off, len, perm, n, ngroups, simds, q, nodes, gate);
-    else if (ring == 12)
-        hipLaunchKernelGGL(k_leaf_queue<11>, dim3(waves), dim3(64), 0, s, base, off, len, perm, n, ngroups, simds, q, nodes, gate);
-    else if (ring == 4)
-        hipLaunchKernelGGL(k_leaf_queue<10>, dim3(waves), dim3(64), 0, s, base, off, len, perm, n, ngroups, simds, q, nodes, gate);
-    else if (ring == 3)
-        hipLaunchKernelGGL(k_leaf_queue<9>, dim3(waves), dim3(64), 0, s, base, off, len, perm, n, ngroups, simds, q, nodes, gate);
-    else if (ring)
-        hipLaunchKernelGGL(k_leaf_queue<8>, dim3(waves), dim3(64), 0, s, base, off, len, perm, n, ngroups, simds, q, nodes, gate);
-    else if (aligned)
-        hipLaunchKernelGGL(k_leaf_queue<6>, dim3(waves), dim3(64), 0, s, base, off, len, perm, n, ngroups, simds, q, nodes, gate);
-    else
-        hipLaunchKernelGGL(k_leaf_queue<7>, dim3(waves), dim3(64), 0, s, base, off, len, perm, n, ngroups, simds, q, nodes, gate);
+    const uint32_t waves = simds * std::min<uint32_t>(std::max<uint32_t>(waves_per_simd, 1u), uint32_t(kQueueRing));
+    hipLaunchKernelGGL(k_leaf_queue, dim3(waves), dim3(64), 0, s, base, off, len, perm, n, ngroups, simds, q, nodes,
+                       gate);
     return hipGetLastError();
 }
 

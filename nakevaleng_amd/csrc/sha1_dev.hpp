@@ -91,14 +91,10 @@ __device__ __forceinline__ void sha1_compress(uint32_t h[5], uint32_t w[16]) {
             f = xor3(b, c, d);
             k = 0xCA62C1D6u;
         }
-#ifdef NKV_SHA1_ADD_CHAIN3
-        uint32_t tmp = rotl(a, 5) + f + e + k + wt;
-#else
         // e + W + K does not depend on this round's a/b, so the critical path
         // through a round is two ops (rotl5 or f, then one add3)
         const uint32_t ewk = add3k(e, wt, k);
         const uint32_t tmp = add3(rotl(a, 5), f, ewk);
-#endif
         e = d;
         d = c;
         c = rotl(b, 30);

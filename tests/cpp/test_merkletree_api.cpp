@@ -2,6 +2,7 @@
 // C-ABI on the GPU and prints "key value" lines that tests/test_cpp_api.py checks
 // against the golden fixtures and the oracle.
 #include <cstdio>
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -110,6 +111,68 @@ int main(int argc, char** argv) {
             t->Root->Data[0] ^= 1;  // the stored root no longer matches the leaves
             std::printf("flush%d_bad_root_validate %d\n", k, int(t->Validate()));
         }
+    }
+    // Serialize walks the live tree (merkletree.go:75-89): Data changed after New
+    // (a leaf and an interior node) is what the file holds
+    {
+        const uint64_t n = 37;
+        auto data = splitmix64_bytes(n * 50, 0xAB);
+        std::vector<MerkleNode> leaves;
+        for (uint64_t i = 0; i < n; ++i) leaves.push_back(NewLeaf(data.data() + i * 50, 50));
+        auto t = New(leaves);
+        MerkleNode* leaf = t->Root;
+        while (leaf->Left) leaf = leaf->Left;
+        leaf->Data.assign(20, 0xAB);
+        t->Root->Right->Data[0] ^= 0xFF;
+        std::printf("mut_img %s\n", hex(t->SerializeBytes()).c_str());
+    }
+    // flushes larger than the arena's stream chunk (32 MiB): settled chunks are
+    // copied to the device during the NewLeaf loop; odd value sizes land at
+    // 16-byte aligned places; streaming off gives the same tree
+    {
+        auto& S = nkv::merkletree::Session::Default();
+        const uint64_t n = 20000;
+        for (size_t vlen : {size_t(4096), size_t(1001)}) {
+            auto data = splitmix64_bytes(n * vlen, 0x5EED + vlen);
+            for (int streaming = 1; streaming >= 0; --streaming) {
+                S.SetStreaming(streaming != 0);
+                std::vector<MerkleNode> leaves;
+                for (uint64_t i = 0; i < n; ++i) leaves.push_back(NewLeaf(data.data() + i * vlen, vlen));
+                auto t = New(leaves);
+                std::printf("big%zu_s%d_root %s\n", vlen, streaming, t->Root->String().c_str());
+            }
+            S.SetStreaming(true);
+        }
+    }
+    // CompactRoots: five Data tables (record.go:191-199) over a group of one GPU
+    // (RCCL) and of device 0 twice (copy transport), one host thread per member
+    {
+        std::vector<nkv::merkletree::DataTable> tabs;
+        for (int t = 0; t < 5; ++t) {
+            nkv::merkletree::DataTable d;
+            const uint64_t recs = 300 + 77 * uint64_t(t), ks = 16, vs = 100 + 13 * uint64_t(t);
+            auto bytes = splitmix64_bytes(recs * (ks + vs), 0xC0 + uint64_t(t));
+            for (uint64_t r = 0; r < recs; ++r) {
+                uint8_t hdr[30] = {};
+                std::memcpy(hdr + 14, &ks, 8);
+                std::memcpy(hdr + 22, &vs, 8);
+                d.data.insert(d.data.end(), hdr, hdr + 30);
+                d.data.insert(d.data.end(), bytes.begin() + long(r * (ks + vs)), bytes.begin() + long((r + 1) * (ks + vs)));
+                d.rec_size.push_back(30 + ks + vs);
+            }
+            FILE* f = std::fopen((dir + "/table" + std::to_string(t) + ".bin").c_str(), "wb");
+            std::fwrite(d.data.data(), 1, d.data.size(), f);
+            std::fclose(f);
+            tabs.push_back(std::move(d));
+        }
+        for (const std::vector<int>& devs : {std::vector<int>{0}, std::vector<int>{0, 0}}) {
+            auto roots = nkv::merkletree::CompactRoots(devs, tabs);
+            for (size_t t = 0; t < roots.size(); ++t)
+                std::printf("compact_g%zu_root%zu %s\n", devs.size(), t,
+                            hex(std::vector<uint8_t>(roots[t].begin(), roots[t].end())).c_str());
+        }
+        nkv::merkletree::Group g1({0});
+        std::printf("group1_transport %d\n", nkv_group_transport(g1.get()));
     }
     return 0;
 }

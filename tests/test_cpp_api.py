@@ -61,3 +61,29 @@ def test_cpp_mirror_on_gpu(tmp_path, oracle):
         assert kv[f"flush{k}_root"] == want[-1].tobytes().hex()
         assert kv[f"flush{k}_validate"] == "1" and kv[f"flush{k}_bad_root_validate"] == "0"
         assert kv[f"flush{k}_swapped_validate"] == "0"  # rehash over swapped children differs
+    # Serialize walks the live tree: Data changed after New shows in the image
+    # exactly as the literal restatement's walk writes it (merkletree.go:75-89)
+    from oracle import merkle_ref as ref
+    data = oracle.splitmix64_bytes(37 * 50, 0xAB)
+    t = ref.New([ref.NewLeaf(data[50 * i:50 * i + 50].tobytes()) for i in range(37)])
+    leaf = t.Root
+    while leaf.Left is not None:
+        leaf = leaf.Left
+    leaf.Data = bytes([0xAB]) * 20
+    d = t.Root.Right.Data
+    t.Root.Right.Data = bytes([d[0] ^ 0xFF]) + bytes(d[1:])
+    assert kv["mut_img"] == t.SerializeBytes().hex()
+    # flushes past the 32 MiB stream chunk, streamed or not, aligned or odd value sizes
+    for vlen in (4096, 1001):
+        data = oracle.splitmix64_bytes(20000 * vlen, 0x5EED + vlen)
+        want = oracle.tree_from_digests(oracle.leaf_hashes_strided(data, vlen, vlen, 20000, threads=8))
+        assert kv[f"big{vlen}_s1_root"] == kv[f"big{vlen}_s0_root"] == want[-1].tobytes().hex()
+    # CompactRoots over a group of one GPU (RCCL) and of device 0 twice (copy)
+    from nakevaleng_amd import record
+    assert kv["group1_transport"] == "1"
+    for t in range(5):
+        stream = open(os.path.join(str(tmp_path), f"table{t}.bin"), "rb").read()
+        rs = np.full(300 + 77 * t, 30 + 16 + 100 + 13 * t, np.uint64)
+        off, ln = record.value_spans(stream, rs)
+        want = oracle.tree_from_digests(oracle.leaf_hashes(np.frombuffer(stream, np.uint8), off, ln))
+        assert kv[f"compact_g1_root{t}"] == kv[f"compact_g2_root{t}"] == want[-1].tobytes().hex()

@@ -6,7 +6,7 @@ on the device or the host, the CRC-verified compaction read), a batch shape
 (one length, small ragged, log-uniform 64 B - 64 KiB like configs[2], zeros
 mixed in), a layout (packed back to back, so mostly unaligned, or with random
 gaps) and a fresh context with random options (load path, ordering policy,
-queue ring / waves / split, records plan, host staging threads and chunk).
+queue waves / split, records plan, table lanes, host staging threads and chunk).
 Every combination must give the oracle's tree: the options choose kernels,
 never results.  Reference:
 merklenode.go:27-34 (leaf), merkletree.go:31-64 (tree), record.go:191-199
@@ -27,11 +27,10 @@ ENTRIES = ["values_dev", "values_host", "strided_dev", "records_dev", "records_h
 
 def _options(rng, _lib):
     return {
-        _lib.NKV_OPT_LEAF_LOAD: int(rng.choice([1, 2, 3, 4, 5, 9, 10, 11, 12])),
+        _lib.NKV_OPT_LEAF_LOAD: int(rng.choice([4, 11])),
         _lib.NKV_OPT_BUCKET: int(rng.integers(0, 3)),
-        _lib.NKV_OPT_DEEP_PREFETCH: int(rng.integers(0, 4)),
-        _lib.NKV_OPT_QUEUE_RING: int(rng.choice([2, 3, 4, 12, 13, 14])),
-        _lib.NKV_OPT_QUEUE_WAVES: int(rng.integers(1, 6)),
+        _lib.NKV_OPT_QUEUE_WAVES: int(rng.integers(1, 4)),
+        _lib.NKV_OPT_TABLE_LANES: int(rng.integers(1, 4)),
         _lib.NKV_OPT_QUEUE_SPLIT: int(rng.choice([0, 1, 8, 32, 1000])),
         _lib.NKV_OPT_RECORDS_FUSED: int(rng.integers(0, 2)),
         _lib.NKV_OPT_HOST_THREADS: int(rng.choice([0, 1, 3, 16])),

@@ -95,7 +95,7 @@ def test_leaf_hash_mixed_wave_alignment(nkv, oracle, bucket):
     assert np.array_equal(got, want)
 
 
-@pytest.mark.parametrize("load", [1, 2, 4, 5, 12])
+@pytest.mark.parametrize("load", [4, 11])
 def test_mixed_sizes_log_uniform(nkv, oracle, load):
     """BASELINE configs[2] shape at reduced count: log-uniform 64 B - 64 KiB values,
     packed back to back (unaligned), every load path."""
@@ -127,24 +127,22 @@ def test_mixed_sizes_log_uniform(nkv, oracle, load):
     assert np.array_equal(nodes, want)
 
 
-@pytest.mark.parametrize("deep,ring", [(0, 2), (1, 2), (2, 2), (3, 2), (3, 3), (3, 4), (3, 12), (3, 13), (3, 14)])
+@pytest.mark.parametrize("waves", [1, 2, 3])
 @pytest.mark.parametrize("n,packed", [(1, True), (63, True), (65, False), (3001, True), (3001, False),
                                       (20000, True)])
-def test_ragged_deep_and_queue_paths(nkv, oracle, deep, ring, n, packed):
-    """Length-sorted ragged batches through each NKV_OPT_DEEP_PREFETCH mode:
-    0 = one-block lookahead, 1 = several blocks, 2 = the work-queue kernel (groups
-    pulled from both ends, claim flags at the meeting point), 3 = the work-queue
-    kernel with the LDS chunk ring of 2 slots, or the pipelined ring of 3 / 4
-    slots (explicit vmcnt / lgkmcnt waits).  Packed = back to back (unaligned
-    path); otherwise 16-B aligned starts (aligned path)."""
+def test_ragged_queue_paths(nkv, oracle, waves, n, packed):
+    """Length-sorted ragged batches through the work-queue kernel (groups pulled
+    from both ends, claim flags at the meeting point, the pipelined ring of
+    value-relative chunks with explicit vmcnt / lgkmcnt waits) at 1-3 waves per
+    SIMD.  Packed = back to back (unaligned); otherwise 16-B aligned starts."""
     torch = _torch()
     _lib, _ = nkv
     ctx = _lib.Context(0)
     _bind(torch, ctx)
-    ctx.set_option(_lib.NKV_OPT_QUEUE_RING, ring)
+    ctx.set_option(_lib.NKV_OPT_QUEUE_WAVES, waves)
     ctx.set_option(_lib.NKV_OPT_BUCKET, 1)
     L = _lib.lib()
-    rng = np.random.default_rng(1000 * n + deep)
+    rng = np.random.default_rng(1000 * n + waves)
     lens = np.floor(2.0 ** rng.uniform(0, 15, n)).astype(np.uint64)
     lens[rng.integers(0, n, max(1, n // 50))] = 0
     step = lens if packed else (lens + 15) // 16 * 16
@@ -153,7 +151,6 @@ def test_ragged_deep_and_queue_paths(nkv, oracle, deep, ring, n, packed):
     data = oracle.splitmix64_bytes(int(off[-1] + lens[-1]) + 1, SEED + n)
     d_data, d_off, d_len = _dev(torch, data), _dev(torch, off), _dev(torch, lens)
     d_nodes = torch.zeros(L.nkv_total_nodes(n) * 20, dtype=torch.uint8, device="cuda")
-    ctx.set_option(_lib.NKV_OPT_DEEP_PREFETCH, deep)
     try:
         for _ in range(2):  # the queue state is reset per launch
             d_nodes.zero_()
@@ -166,10 +163,10 @@ def test_ragged_deep_and_queue_paths(nkv, oracle, deep, ring, n, packed):
         ctx.close()
 
 
-@pytest.mark.parametrize("ring", [2, 3, 4, 12, 13, 14])
+@pytest.mark.parametrize("waves", [1, 3])
 @pytest.mark.parametrize("split", [0, 1, 32, 100000])
 @pytest.mark.parametrize("shape", ["uniform", "skewed"])
-def test_queue_split_policies(nkv, oracle, split, shape, ring):
+def test_queue_split_policies(nkv, oracle, split, shape, waves):
     """Work-queue kernel under every split regime: equal lengths (throughput-
     bound: every wave takes any group) and one very long value among short ones
     (the longest chain bounds the batch: short groups only to the non-priority
@@ -178,7 +175,7 @@ def test_queue_split_policies(nkv, oracle, split, shape, ring):
     _lib, _ = nkv
     ctx = _lib.Context(0)
     _bind(torch, ctx)
-    ctx.set_option(_lib.NKV_OPT_QUEUE_RING, ring)
+    ctx.set_option(_lib.NKV_OPT_QUEUE_WAVES, waves)
     ctx.set_option(_lib.NKV_OPT_BUCKET, 1)  # equal lengths would take input order in auto mode
     L = _lib.lib()
     rng = np.random.default_rng(split + (7 if shape == "uniform" else 8))
@@ -273,7 +270,7 @@ def test_strided_device_path(nkv, oracle, base_off, stride, vlen):
     assert np.array_equal(got, want)
 
 
-@pytest.mark.parametrize("load", [1, 2, 3, 4, 5])
+@pytest.mark.parametrize("load", [4, 11])
 def test_strided_every_load_path(nkv, oracle, load):
     torch = _torch()
     _lib, ctx = nkv
@@ -393,13 +390,14 @@ def test_bucket_modes_narrow_and_wide(nkv, oracle, bucket, spread):
     assert np.array_equal(d_nodes.cpu().numpy().reshape(-1, 20), want)
 
 
-@pytest.mark.parametrize("load", [9, 10, 11, 12])
+@pytest.mark.parametrize("load", [4, 11])
 @pytest.mark.parametrize("shift", [0, 1, 2, 15, 16, 17, 46, 48, 63])
 @pytest.mark.parametrize("n,vlen,rec", [(1, 4050, 4096), (63, 4050, 4096), (3001, 4050, 4096), (777, 327, 400),
                                         (300, 63, 128), (257, 64, 130), (130, 1024, 1100)])
 def test_line_pair_stage_uniform(nkv, oracle, load, shift, n, vlen, rec):
-    """NKV_OPT_LEAF_LOAD 9 / 10 (line-pair / 80-byte-window LDS-DMA stage, byte-unaligned LDS reads): records-like values at
-    every sub-line offset, through the offsets path and the strided path, dead lanes in the last wave."""
+    """The staged paths (segment stage for a shared offset mod 64, 80-byte window stage, value-relative
+    stream; LOAD 4 sends unaligned values there too): records-like values at every sub-line offset,
+    through the offsets path and the strided path, dead lanes in the last wave."""
     torch = _torch()
     _lib, ctx = nkv
     _bind(torch, ctx)
@@ -425,11 +423,11 @@ def test_line_pair_stage_uniform(nkv, oracle, load, shift, n, vlen, rec):
     assert np.array_equal(d_nodes2.cpu().numpy().reshape(-1, 20), want)
 
 
-@pytest.mark.parametrize("load", [9, 10, 11, 12])
+@pytest.mark.parametrize("load", [4, 11])
 @pytest.mark.parametrize("spread", [1, 64, 3000])
 def test_line_pair_stage_ragged_falls_back(nkv, oracle, load, spread):
-    """LOAD 9 in input order over values whose full-block counts differ inside a wave: those waves take
-    the value-relative stream, equal-count waves the line-pair stage; every digest matches."""
+    """Input order over values whose full-block counts differ inside a wave: those waves take
+    the value-relative stream, equal-count waves the window or segment stage; every digest matches."""
     torch = _torch()
     _lib, ctx = nkv
     _bind(torch, ctx)
