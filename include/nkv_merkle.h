@@ -114,12 +114,11 @@ int nkv_ctx_sync(nkv_ctx *ctx);
                                  when the longest value bounds the batch (default 32) */
 #define NKV_OPT_QUEUE_WAVES 5 /* work-queue kernel: waves per SIMD, 1..3 (default 3: its
                                  3-slot, 12 KiB LDS ring per wave) */
-#define NKV_OPT_CRC_LOAD 6    /* record checksums: bit 0 = spans staged as aligned 64-B
-                                 chunks through an LDS ring (else per-lane loads); bits
-                                 1-2 = LDS table copies x workgroup: 0 = 8 x 256,
-                                 1 = 16 x 512, 2 = 32 x 1024 (no ring); 8 = span groups:
-                                 16 lanes per span, one 64-B chunk per lane, chunk states
-                                 combined by CRC advance tables */
+#define NKV_OPT_CRC_LOAD 6    /* record checksums: 0 (default) = one lane per span, slicing-by-4
+                                 from lane-private LDS table columns (no bank conflicts),
+                                 whole 128-byte lines into registers; 8 = 16 lanes per span,
+                                 chunk states combined by CRC advance tables (a few long
+                                 spans) */
 #define NKV_OPT_HOST_THREADS 7 /* host-buffer API: threads that gather caller bytes into the
                                   pinned staging chunks (0 = default: min(16, cores), or
                                   the NKV_HOST_THREADS environment variable) */

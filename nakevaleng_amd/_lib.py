@@ -351,16 +351,24 @@ _default: dict = {}
 
 
 def current_device() -> int:
-    """The device this process works on: torch's current device when a GPU is
-    visible (one process per GPU binds it with torch.cuda.set_device), else the
-    launcher's LOCAL_RANK (0 without a launcher)."""
-    try:
-        import torch
-        if torch.cuda.is_available():
-            return int(torch.cuda.current_device())
-    except ImportError:
-        pass
-    return int(os.environ.get("LOCAL_RANK", "0"))
+    """The device this process works on, one rule for every caller
+    (lsmtree.rank_device, the mirrors' default contexts): the launcher's
+    LOCAL_RANK modulo the visible devices (one process per GPU), else the
+    device torch already works on if this process initialised torch's GPU
+    state, else 0.  It never initialises torch's GPU runtime itself."""
+    local = os.environ.get("LOCAL_RANK")
+    if local is not None:
+        cnt = device_count()
+        return int(local) % cnt if cnt else int(local)
+    import sys
+    torch = sys.modules.get("torch")
+    if torch is not None:
+        try:
+            if torch.cuda.is_initialized():
+                return int(torch.cuda.current_device())
+        except Exception:
+            pass
+    return 0
 
 
 def default_context(device: Optional[int] = None) -> Context:

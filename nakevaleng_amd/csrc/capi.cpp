@@ -521,7 +521,7 @@ int nkv_ctx_set_option(nkv_ctx* c, int key, int64_t value) try {
             c->queue_split = int(std::min<int64_t>(value, 0x7FFFFFFF));
             return NKV_OK;
         case NKV_OPT_CRC_LOAD:
-            if (value < 0 || (value > 5 && (value < 8 || value > 10))) return NKV_ERR_INVALID;
+            if (value != 0 && value != 8) return NKV_ERR_INVALID;
             c->crc_load = int(value);
             return NKV_OK;
         case NKV_OPT_BLOOM_PATH:

@@ -125,7 +125,7 @@ struct nkv_ctx {
     int queue_split = 32;   // NKV_OPT_QUEUE_SPLIT
     int queue_waves = 3;    // NKV_OPT_QUEUE_WAVES
     int bloom_path = 2;     // NKV_OPT_BLOOM_PATH
-    int crc_load = 1;       // NKV_OPT_CRC_LOAD
+    int crc_load = 0;       // NKV_OPT_CRC_LOAD
     int records_fused = 1;  // NKV_OPT_RECORDS_FUSED
     int table_lanes = 2;    // NKV_OPT_TABLE_LANES
     bool timing = false;

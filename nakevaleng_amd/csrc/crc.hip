@@ -7,19 +7,25 @@
 // (record.go:191-204), so the checksum covers one byte span per record:
 // [rec + 30, rec + 30 + KeySize + ValueSize).
 //
-// One lane per span.  Slicing-by-4: one 32-bit word per step, four table
-// lookups from LDS.  The four 256-entry tables are replicated kCrcCopies times
-// and interleaved so lane l reads copy l % kCrcCopies: a ds_read_b32 is served
-// in two 32-lane groups over 32 banks, entry e of table k of copy c sits in
-// bank (8 e + c) % 32, so the 4 lanes sharing a copy inside a group collide only
-// when their entries agree mod 4 (about 2-way on random data instead of ~4-way
-// with one copy).
+// One lane per span (k_crc_lanes).  Slicing-by-4: one 32-bit word per step,
+// four table lookups from LDS.  The 4 x 256 tables are stored once per bank:
+// 32 copies, copy c read only by the lanes l with l % 32 = c, entry e of copy
+// c at byte e * 256 + c * 4 (+ 128 for tables 1 and 3, + 64 KiB for tables 2
+// and 3), so a ds_read_b32 -- served 32 lanes per cycle over 32 banks -- has
+// lane l alone in bank l % 32: no bank conflict, whatever the data (the 8-copy
+// interleave of rounds 1-2 spent 63 % of its LDS cycles in conflicts,
+// profiles/r01_crc_pmc_lds.json).  The row stride of 256 bytes makes each
+// lookup's LDS address ONE v_perm_b32: byte j of x lands in address byte 1,
+// the lane's copy offset (c * 4) in byte 0 and the 64 KiB table half in byte
+// 2, both from a per-lane constant; the 128-byte half comes from the
+// ds_read's immediate offset.  128 KiB of tables: one 1024-thread workgroup
+// per CU (4 waves per SIMD), persistent over the spans.
 //
 // Per span: 0-3 head bytes (byte steps) up to the first 4-aligned address,
-// then whole aligned words in aligned 64-byte chunks (4 x global_load_dwordx4
-// per lane per chunk; every loaded chunk holds a span byte, so no load leaves
-// the span's pages), then 0-3 tail bytes.  Chunks a lane does not own are
-// masked; only a span's first and last chunk mask single words.
+// then whole aligned words from whole aligned 128-byte lines (eight
+// global_load_dwordx4 per lane per line, the next line loaded while this one
+// is checksummed; a line holding a span byte lies in that byte's page), then
+// 0-3 tail bytes.  Only a span's first and last line mask words.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -32,6 +38,43 @@ namespace nkv {
 
 __constant__ CrcTables c_crc = make_crc_tables();
 
+// Lane-private table layout: two 64 KiB halves (tables 0, 1 and 2, 3) of 256
+// rows (entry e) of 64 words: words 0-31 = table 2h, copies 0-31; words 32-63 =
+// table 2h + 1.  k_crc_lanes's only LDS object, so it starts at LDS address 0.
+constexpr uint32_t kLaneTabWords = 2 * 256 * 64;  // 128 KiB
+
+// one lookup: table k (compile-time), byte j (0..3) of x; la = lane constant of
+// table half k >> 1 (c * 4 in byte 0, the half in byte 2)
+template <int K, int J>
+__device__ __forceinline__ uint32_t lane_lut(uint32_t x, uint32_t la) {
+    // address = {0, la.byte2, x.byte J, la.byte0}: v_perm over (hi = x, lo = la)
+    constexpr uint32_t sel = (12u << 24) | (2u << 16) | (uint32_t(4 + J) << 8) | 0u;
+    const uint32_t addr = __builtin_amdgcn_perm(x, la, sel);
+    uint32_t v;
+    if constexpr (K & 1) asm volatile("ds_read_b32 %0, %1 offset:128" : "=v"(v) : "v"(addr));
+    else asm volatile("ds_read_b32 %0, %1" : "=v"(v) : "v"(addr));
+    return v;
+}
+
+// x = crc ^ w form (crc_dev.hpp): the state after word w given x, without the
+// next word (last) or with it folded in (next)
+// (the lookups are inline asm, so the waits are explicit; the wait names the
+// loaded registers as in/out operands, so no use of them is scheduled before it)
+__device__ __forceinline__ uint32_t lane_x_next(uint32_t x, uint32_t w, uint32_t la0, uint32_t la1) {
+    uint32_t a = lane_lut<3, 0>(x, la1), b = lane_lut<2, 1>(x, la1);
+    uint32_t c = lane_lut<1, 2>(x, la0), d = lane_lut<0, 3>(x, la0);
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+    return crc_xor3(crc_xor3(a, b, c), d, w);
+}
+__device__ __forceinline__ uint32_t lane_x_last(uint32_t x, uint32_t la0, uint32_t la1) {
+    return lane_x_next(x, 0u, la0, la1);
+}
+__device__ __forceinline__ uint32_t lane_byte(uint32_t crc, uint32_t b, uint32_t la0) {
+    uint32_t t = lane_lut<0, 0>((crc ^ b) & 0xFFu, la0);
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(t));
+    return t ^ (crc >> 8);
+}
+
 __device__ __forceinline__ uint64_t crc_ld_le64(const uint8_t* p) {
     uint64_t v = 0;
 #pragma unroll
@@ -39,125 +82,137 @@ __device__ __forceinline__ uint64_t crc_ld_le64(const uint8_t* p) {
     return v;
 }
 
-// Same checksum, span bytes staged through a wave-private LDS ring of aligned
-// 64-B chunks (two 4 KiB slots, chunk c in slot c & 1) by wave-cooperative
-// DMA: instruction k moves one chunk of spans 16k .. 16k+15, 64 contiguous
-// bytes each (16 segments per wave-instruction instead of 64 scattered 16-B
-// pieces when every lane reads its own span).  Each lane then reads its own
-// chunk's four quads.  Chunk c+2 goes into chunk c's slot once c is read.
-// Only chunks holding span bytes are fetched (an aligned chunk with one valid
-// byte lies in that byte's page).
-template <int C>
-__device__ __forceinline__ uint32_t crc_span_ring(const uint8_t* s, uint64_t len, const uint32_t* tab,
-                                                  uint8_t* wbuf) {
-    const int lane = threadIdx.x & 63;
-    uint32_t crc = 0xFFFFFFFFu;
-    const uint32_t o = uint32_t(reinterpret_cast<uintptr_t>(s)) & 63u;
-    const uint32_t nch = len ? uint32_t((o + len + 63) >> 6) : 0u;
-    const uint32_t dq = (uint32_t(lane) & 3u) ^ ((uint32_t(lane) >> 4) & 3u);
-    const uint8_t* src[4];
-    uint32_t nc[4];
+// Crc, KeySize, ValueSize of the record header at p (record.go:191-199: Crc at
+// +0, KeySize at +14, ValueSize at +22) from aligned 8-byte loads, each inside
+// the aligned word that holds a header byte (no page past the header).
+__device__ __forceinline__ void crc_header(const uint8_t* p, uint32_t& stored, uint64_t& ks, uint64_t& vs) {
+    const uint32_t m = uint32_t(reinterpret_cast<uintptr_t>(p) & 7u);
+    const uint64_t* q = reinterpret_cast<const uint64_t*>(p - m);
+    uint64_t w[5];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int j = 16 * k + (lane >> 2);
-        const uint64_t aj = uint64_t(__shfl(int64_t(reinterpret_cast<uintptr_t>(s - o)), j));
-        src[k] = reinterpret_cast<const uint8_t*>(aj) + 16 * dq;
-        nc[k] = uint32_t(__shfl(int(nch), j));
-    }
-    const uint32_t nmax = crc_wave_max(nch);
-    if (nmax == 0) return 0u;
-    auto issue = [&](uint32_t c) {
-        uint8_t* dst = wbuf + 4096 * (c & 1u);
+    for (int i = 0; i < 5; ++i) w[i] = (i < 4 || m + 29 >= 32) ? q[i] : 0ull;
+    auto at = [&](uint32_t off) {  // 8 bytes from header offset off
+        const uint32_t o = m + off, k = o >> 3, sh = (o & 7u) * 8u;
+        uint64_t lo = 0, hi = 0;
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if (c < nc[k]) __builtin_amdgcn_global_load_lds(src[k] + 64ull * c, dst + 1024 * k, 16, 0, 0);
+        for (int i = 0; i < 4; ++i) {
+            lo = uint32_t(i) == k ? w[i] : lo;
+            hi = uint32_t(i) == k ? w[i + 1] : hi;
+        }
+        return sh ? (lo >> sh) | (hi << (64u - sh)) : lo;
     };
-    const uint32_t swz = (uint32_t(lane) >> 2) & 3u;
-    const uint64_t e = uint64_t(o) + len;  // span end, relative to the first chunk
-    issue(0u);
-    issue(1u);
+    stored = uint32_t(at(0));
+    ks = at(14);
+    vs = at(22);
+}
+
+// CRC-32/IEEE of [s, s + len) for every lane of the wave (dead lanes: len 0),
+// from whole aligned 128-byte lines, with the lane-private tables.
+__device__ __forceinline__ uint32_t crc_span_lines(const uint8_t* s, uint64_t len, uint32_t la0, uint32_t la1) {
+    uint32_t crc = 0xFFFFFFFFu;
+    const uint64_t sa = uint64_t(reinterpret_cast<uintptr_t>(s));
+    const uint64_t ea = sa + len;
+    const uint64_t s4 = (sa + 3) & ~uint64_t(3);
+    const uint64_t e4 = ea & ~uint64_t(3);
+    const uint64_t hb = s4 < ea ? s4 : ea;
+    for (uint64_t a = sa; a < hb; ++a) crc = lane_byte(crc, s[a - sa], la0);
+    const uint64_t A = s4 & ~uint64_t(127);
+    const uint32_t nl = e4 > s4 ? uint32_t((e4 - A + 127) >> 7) : 0u;
+    const uint32_t nmax = crc_wave_max(nl);
+    // s + (A - sa): stays a global pointer (no integer-to-pointer cast)
+    const uint4* q = reinterpret_cast<const uint4*>(s + (A - sa));
+    uint4 cur[8], nxt[8];
+    if (nl > 0) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) cur[i] = q[i];
+    }
     for (uint32_t c = 0; c < nmax; ++c) {
-        const uint8_t* rd = wbuf + 4096 * (c & 1u) + 64 * lane;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // chunk c landed (explicit LDS-DMA wait)
-        uint4 v[4];
+        if (c + 1 < nl) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = *reinterpret_cast<const uint4*>(rd + 16 * (uint32_t(i) ^ swz));
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot reads done before refill
-        if (c + 2 < nmax) issue(c + 2);
-        if (c < nch) {
-            const uint32_t w[16] = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w,
-                                    v[2].x, v[2].y, v[2].z, v[2].w, v[3].x, v[3].y, v[3].z, v[3].w};
-            const uint64_t b0 = 64ull * c;  // chunk start, relative
-            if (b0 >= o && b0 + 64 <= e) {
-                crc = crc_block16<C>(crc, w, tab);
+            for (int i = 0; i < 8; ++i) nxt[i] = q[8 * (c + 1) + i];
+        }
+        if (c < nl) {
+            const uint32_t* w = reinterpret_cast<const uint32_t*>(cur);
+            const uint64_t b0 = A + 128ull * c;
+            if (b0 >= s4 && b0 + 128 <= e4) {
+                uint32_t x = crc ^ w[0];
+#pragma unroll
+                for (int j = 1; j < 32; ++j) x = lane_x_next(x, w[j], la0, la1);
+                crc = lane_x_last(x, la0, la1);
             } else {
-#pragma unroll
-                for (int j = 0; j < 16; ++j) {
-                    const uint64_t a = b0 + 4 * j;
-                    const uint32_t lo = a >= o ? 0u : (o - a >= 4 ? 4u : uint32_t(o - a));
-                    const uint32_t hi = a >= e ? 0u : (e - a >= 4 ? 4u : uint32_t(e - a));
-                    if (lo == 0u && hi == 4u) {
-                        crc = crc_word<C>(crc, w[j], tab);
-                    } else {
-                        for (uint32_t b = lo; b < hi; ++b) crc = crc_byte<C>(crc, (w[j] >> (8 * b)) & 0xFFu, tab);
-                    }
-                }
+                const uint64_t lo = s4 > b0 ? (s4 - b0) >> 2 : 0;
+                const uint64_t hi = e4 - b0 >= 128 ? 32 : (e4 - b0) >> 2;
+                for (uint32_t j = uint32_t(lo); j < uint32_t(hi); ++j) crc = lane_x_last(crc ^ w[j], la0, la1);
             }
         }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) cur[i] = nxt[i];
     }
+    const uint64_t tb = e4 > hb ? e4 : hb;
+    for (uint64_t a = tb; a < ea; ++a) crc = lane_byte(crc, s[a - sa], la0);
     return ~crc;
 }
 
 // RECORDS: span of record i from its header at base + off[i] (len unused),
 // checked against stream_len; stats[0] += records whose stored Crc differs,
 // stats[1] = min such index, stats[2] |= 1 on a header outside the stream.
-// Otherwise span i = [base + off[i], + len[i]).
-template <bool RECORDS, bool RING, int C, int B>
-__global__ __launch_bounds__(B) void k_crc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
-                                           const uint64_t* __restrict__ len, uint64_t stream_len, uint64_t n,
-                                           uint32_t* __restrict__ out, unsigned long long* __restrict__ stats,
-                                           Gate gate) {
-    __shared__ uint32_t tab[4 * 256 * C];
+// Otherwise span i = [base + off[i], + len[i]).  Persistent: the grid is one
+// workgroup per CU, each loading the tables once.
+constexpr int kCrcLanesWG = 1024;
+template <bool RECORDS>
+__global__ __launch_bounds__(kCrcLanesWG) void k_crc_lanes(const uint8_t* __restrict__ base,
+                                                            const uint64_t* __restrict__ off,
+                                                            const uint64_t* __restrict__ len, uint64_t stream_len,
+                                                            uint64_t n, uint32_t* __restrict__ out,
+                                                            unsigned long long* __restrict__ stats, Gate gate) {
+    __shared__ uint32_t tab[kLaneTabWords];
     if (!gate.open()) return;
-    __shared__ __attribute__((aligned(16))) uint8_t ring[RING ? B / 64 : 1][RING ? 8192 : 16];
-    for (int i = threadIdx.x; i < 4 * 256 * C; i += B) tab[i] = (&c_crc.t[0][0])[i / C];
+    for (uint32_t i = threadIdx.x; i < kLaneTabWords; i += kCrcLanesWG) {
+        const uint32_t half = i >> 14, e = (i >> 6) & 255u, k = 2u * half + ((i >> 5) & 1u);
+        tab[i] = c_crc.t[k][e];  // every copy c = i & 31 holds the same entry
+    }
     __syncthreads();
-    const uint32_t* mytab = tab + (threadIdx.x % C);
-    const uint64_t i = uint64_t(blockIdx.x) * B + threadIdx.x;
-    const uint8_t* s = base;
-    uint64_t L = 0;
-    uint32_t stored = 0;
-    bool live = i < n, hdr_bad = false;
-    if (live) {
-        if (RECORDS) {
-            const uint64_t r = off[i];
-            if (header_in(r, stream_len)) {
-                const uint64_t ks = crc_ld_le64(base + r + 14);
-                const uint64_t vs = crc_ld_le64(base + r + 22);
-                if (ks <= stream_len && vs <= stream_len && r + 30 + ks + vs <= stream_len) {
-                    s = base + r + 30;
-                    L = ks + vs;
-                    stored = uint32_t(base[r]) | uint32_t(base[r + 1]) << 8 | uint32_t(base[r + 2]) << 16 |
-                             uint32_t(base[r + 3]) << 24;
+    // lane constants of the two halves: the copy offset (byte 0), the half (byte 2)
+    const uint32_t la0 = (threadIdx.x & 31u) * 4u, la1 = la0 | 0x10000u;
+    const uint64_t stride = uint64_t(gridDim.x) * kCrcLanesWG;
+    const uint64_t w0 = uint64_t(blockIdx.x) * kCrcLanesWG + (threadIdx.x & ~63u);  // this wave's first span
+    for (uint64_t wb = w0; wb < n; wb += stride) {  // wave-uniform loop
+        const uint64_t i = wb + (threadIdx.x & 63u);
+        const bool live = i < n;
+        const uint8_t* s = base;
+        uint64_t L = 0;
+        uint32_t stored = 0;
+        bool hdr_bad = false;
+        if (live) {
+            if (RECORDS) {
+                const uint64_t r = off[i];
+                if (header_in(r, stream_len)) {
+                    uint64_t ks, vs;
+                    crc_header(base + r, stored, ks, vs);
+                    if (ks <= stream_len && vs <= stream_len && r + 30 + ks + vs <= stream_len) {
+                        s = base + r + 30;
+                        L = ks + vs;
+                    } else {
+                        hdr_bad = true;
+                    }
                 } else {
                     hdr_bad = true;
                 }
             } else {
-                hdr_bad = true;
+                s = base + off[i];
+                L = len[i];
             }
-        } else {
-            s = base + off[i];
-            L = len[i];
         }
-    }
-    const uint32_t crc = RING ? crc_span_ring<C>(s, L, mytab, ring[threadIdx.x >> 6]) : crc_span<C>(s, L, mytab);
-    if (!live) return;
-    if (out) out[i] = crc;
-    if (RECORDS && stats) {
-        if (hdr_bad) atomicOr(stats + 2, 1ull);
-        else if (crc != stored) {
-            atomicAdd(stats, 1ull);
-            atomicMin(stats + 1, (unsigned long long)i);
+        const uint32_t crc = crc_span_lines(s, L, la0, la1);
+        if (live) {
+            if (out) out[i] = crc;
+            if (RECORDS && stats) {
+                if (hdr_bad) atomicOr(stats + 2, 1ull);
+                else if (crc != stored) {
+                    atomicAdd(stats, 1ull);
+                    atomicMin(stats + 1, (unsigned long long)i);
+                }
+            }
         }
     }
 }
@@ -345,32 +400,20 @@ static void launch_crc_group(int per_cu, const uint8_t* base, const uint64_t* of
                        out, stats, gate);
 }
 
-// variant 8 / 9: span-group kernel with 8 x 512 / 32 x 1024 table copies x
-// workgroup.  Else bit 0 = LDS chunk ring; bits 1-2 = table copies x workgroup
-// size: 0 = 8 x 256, 1 = 16 x 512, 2 = 32 x 1024.
+// variant (NKV_OPT_CRC_LOAD) 0: one lane per span, lane-private tables
+// (k_crc_lanes, one 1024-thread workgroup per CU); 8: 16 lanes per span
+// (k_crc_group, 8 x 512 interleaved table copies: for a few long spans)
 template <bool RECORDS>
 static void launch_crc(int variant, const uint8_t* base, const uint64_t* off, const uint64_t* len,
                        uint64_t stream_len, uint64_t n, uint32_t* out, unsigned long long* stats, hipStream_t s,
                        Gate gate) {
     if (variant == 8) return launch_crc_group<RECORDS, 8, 512>(2, base, off, len, stream_len, n, out, stats, s, gate);
-    if (variant == 9) return launch_crc_group<RECORDS, 32, 1024>(1, base, off, len, stream_len, n, out, stats, s, gate);
-    if (variant == 10) return launch_crc_group<RECORDS, 4, 512>(4, base, off, len, stream_len, n, out, stats, s, gate);
-    const bool ring = variant & 1;
-    const int cfg = (variant >> 1) & 3;
-    const int B = cfg == 0 ? 256 : (cfg == 1 ? 512 : 1024);
-    const dim3 grid(uint32_t((n + B - 1) / B)), block(B);
-#define NKV_CRC_LAUNCH(R, C, BB) \
-    hipLaunchKernelGGL((k_crc<RECORDS, R, C, BB>), grid, block, 0, s, base, off, len, stream_len, n, out, stats, gate)
-    if (cfg == 0) {
-        if (ring) NKV_CRC_LAUNCH(true, 8, 256);
-        else NKV_CRC_LAUNCH(false, 8, 256);
-    } else if (cfg == 1) {
-        if (ring) NKV_CRC_LAUNCH(true, 16, 512);
-        else NKV_CRC_LAUNCH(false, 16, 512);
-    } else {
-        NKV_CRC_LAUNCH(false, 32, 1024);  // 128 KiB of tables: no room for a ring
-    }
-#undef NKV_CRC_LAUNCH
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const uint64_t want = (n + kCrcLanesWG - 1) / kCrcLanesWG;
+    const uint32_t grid = uint32_t(std::max<uint64_t>(1, std::min<uint64_t>(want, uint64_t(cus))));
+    hipLaunchKernelGGL((k_crc_lanes<RECORDS>), dim3(grid), dim3(kCrcLanesWG), 0, s, base, off, len, stream_len, n,
+                       out, stats, gate);
 }
 
 hipError_t launch_crc_spans(const uint8_t* base, const uint64_t* off, const uint64_t* len, uint64_t n,

@@ -121,8 +121,8 @@ hipError_t sort_by_length_desc(const uint64_t* len, uint64_t n, uint32_t* perm, 
                                Gate gate = Gate{}, QueueInit qi = QueueInit{}, CopyWords cw = CopyWords{});
 // crc.hip: CRC-32/IEEE of byte spans / of records' Key ++ Value (stats: 3 x u64,
 // initialised by the launcher).
-// variant: NKV_OPT_CRC_LOAD (bit 0 LDS chunk ring; bits 1-2 table copies x
-// workgroup size).
+// variant: NKV_OPT_CRC_LOAD (0 = one lane per span, lane-private tables; 8 =
+// 16 lanes per span).
 hipError_t launch_crc_spans(const uint8_t* base, const uint64_t* off, const uint64_t* len, uint64_t n,
                             uint32_t* out, int variant, hipStream_t s);
 // init_stats: reset stats to {0, UINT64_MAX, 0} first (false: the caller did)

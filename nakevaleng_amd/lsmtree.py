@@ -24,21 +24,27 @@ def shard(num_tables: int, world: int, rank: int) -> List[int]:
 
 def rank_device(device=None) -> int:
     """The GPU this rank hashes on: `device` when given (an int or torch.device),
-    else the launcher's LOCAL_RANK (one process per GPU, modulo the visible
-    devices), else the process's current device."""
-    import os
+    else _lib.current_device() -- the same rule the mirrors' default contexts
+    use (LOCAL_RANK modulo the visible devices, else torch's device if torch
+    already set one up, else 0)."""
     if device is not None:
         return device.index if hasattr(device, "index") else int(device)
-    local = os.environ.get("LOCAL_RANK")
-    if local is not None:
-        try:
-            import torch
-            cnt = torch.cuda.device_count()
-        except ImportError:
-            cnt = 0
-        return int(local) % cnt if cnt else int(local)
     from . import _lib
     return _lib.current_device()
+
+
+def _call_build(build, table, dev):
+    """build(table, device), or build(table) for a one-argument builder (the
+    form compact_roots took before round 2)."""
+    import inspect
+    try:
+        params = [p for p in inspect.signature(build).parameters.values()
+                  if p.kind in (p.POSITIONAL_ONLY, p.POSITIONAL_OR_KEYWORD)]
+        takes_device = len(params) >= 2 or any(p.kind == p.VAR_POSITIONAL
+                                               for p in inspect.signature(build).parameters.values())
+    except (TypeError, ValueError):  # builtins without a signature: try the two-argument form
+        takes_device = True
+    return build(table, dev) if takes_device else build(table)
 
 
 def gpu_table_root(table: Table, device: Optional[int] = None) -> bytes:
@@ -90,9 +96,9 @@ def compact_roots(tables: Sequence[Table], build: Callable[[Table, int], bytes] 
                   device=None) -> List[bytes]:
     """Build the Merkle tree of every table this rank owns and all-gather the roots.
 
-    `build(table, device)` maps one table to its root; the default hashes on
-    this rank's GPU (rank_device(device): LOCAL_RANK under one process per GPU),
-    and the roots are gathered from that same device over RCCL.
+    `build(table, device)` (or `build(table)`) maps one table to its root; the
+    default hashes on this rank's GPU (rank_device(device): LOCAL_RANK under one
+    process per GPU), and the roots are gathered from that same device over RCCL.
     """
     import torch.distributed as dist
 
@@ -101,7 +107,7 @@ def compact_roots(tables: Sequence[Table], build: Callable[[Table, int], bytes] 
     dev = rank_device(device)
     if build is None:
         build = gpu_table_root
-    local = {i: build(tables[i], dev) for i in shard(len(tables), world, rank)}
+    local = {i: _call_build(build, tables[i], dev) for i in shard(len(tables), world, rank)}
     if world == 1:
         return [local[i] for i in range(len(tables))]
     import torch

@@ -75,15 +75,32 @@ def test_compact_roots_world2(oracle, k):
 
 
 def test_rank_device_resolution(monkeypatch):
-    from nakevaleng_amd import lsmtree
+    """One device rule for lsmtree and the mirrors' default contexts:
+    explicit device, else LOCAL_RANK modulo the visible devices, else torch's
+    device only if torch already initialised its GPU state, else 0."""
+    from nakevaleng_amd import _lib, lsmtree
     import torch
-    monkeypatch.setattr(torch.cuda, "device_count", lambda: 0)
+    monkeypatch.setattr(_lib, "device_count", lambda: 0)
     assert lsmtree.rank_device(3) == 3
     assert lsmtree.rank_device(torch.device("cuda", 5)) == 5
     monkeypatch.setenv("LOCAL_RANK", "6")
-    assert lsmtree.rank_device() == 6
-    monkeypatch.setattr(torch.cuda, "device_count", lambda: 4)
-    assert lsmtree.rank_device() == 2  # LOCAL_RANK modulo the visible devices
+    assert lsmtree.rank_device() == 6 == _lib.current_device()
+    monkeypatch.setattr(_lib, "device_count", lambda: 4)
+    assert lsmtree.rank_device() == 2 == _lib.current_device()  # LOCAL_RANK modulo the visible devices
     monkeypatch.delenv("LOCAL_RANK")
-    monkeypatch.setattr(torch.cuda, "is_available", lambda: False)
-    assert lsmtree.rank_device() == 0
+    monkeypatch.setattr(torch.cuda, "is_initialized", lambda: False)
+    assert lsmtree.rank_device() == 0 == _lib.current_device()
+    monkeypatch.setattr(torch.cuda, "is_initialized", lambda: True)
+    monkeypatch.setattr(torch.cuda, "current_device", lambda: 1)
+    assert lsmtree.rank_device() == 1 == _lib.current_device()
+
+
+def test_compact_roots_takes_one_or_two_argument_builders():
+    """build(table) (the pre-round-2 form) and build(table, device) both work."""
+    from nakevaleng_amd import lsmtree
+    tables = [(b"x" * 10, [10]), (b"y" * 20, [20])]
+    seen = []
+    assert lsmtree.compact_roots(tables, build=lambda t: t[0][:1] * 20) == [b"x" * 20, b"y" * 20]
+    assert lsmtree.compact_roots(tables, build=lambda t, d: seen.append(d) or t[0][:1] * 20, device=3) == \
+        [b"x" * 20, b"y" * 20]
+    assert seen == [3, 3]

@@ -30,7 +30,7 @@ def _stream(rng, n, kmax=40, vmax=3000):
     return recs, np.frombuffer(stream, np.uint8).copy(), sizes, off
 
 
-@pytest.mark.parametrize("load", [0, 1, 2, 3, 4, 8, 9, 10])
+@pytest.mark.parametrize("load", [0, 8])
 def test_crc32_spans_every_alignment_and_length(nkv, oracle, load):
     torch = _torch()
     _lib, ctx = nkv
@@ -49,7 +49,7 @@ def test_crc32_spans_every_alignment_and_length(nkv, oracle, load):
     torch.cuda.synchronize()
     got = d_out.cpu().numpy().view(np.uint32)
     want = [oracle.crc32(data[int(o):int(o + l)]) for o, l in zip(off, lens)]
-    ctx.set_option(_lib.NKV_OPT_CRC_LOAD, 1)
+    ctx.set_option(_lib.NKV_OPT_CRC_LOAD, 0)
     assert got.tolist() == want
 
 
@@ -66,7 +66,7 @@ def test_crc32_check_value(nkv):
     assert int(out.cpu().numpy().view(np.uint32)[0]) == 0xCBF43926
 
 
-@pytest.mark.parametrize("load", [0, 1, 2, 3, 4, 8, 9, 10])
+@pytest.mark.parametrize("load", [0, 8])
 @pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 257, 3000])
 def test_record_crc_device_matches_oracle_and_stored(nkv, oracle, n, load):
     torch = _torch()
@@ -93,7 +93,7 @@ def test_record_crc_device_matches_oracle_and_stored(nkv, oracle, n, load):
     assert int(stats[0]) == want_bad == len(bad_idx)
     assert int(stats[1]) == (bad_idx[0] if bad_idx else 2**64 - 1)
     assert int(stats[2]) == 0
-    ctx.set_option(_lib.NKV_OPT_CRC_LOAD, 1)
+    ctx.set_option(_lib.NKV_OPT_CRC_LOAD, 0)
 
 
 def test_record_crc_host_api_and_mirror(nkv, oracle):

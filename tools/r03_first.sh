@@ -22,6 +22,9 @@ timeout -k 10 300 python -u bench.py --backend capi --config one_tree --verify >
 echo capi_one_tree; cat $O/capi_one_tree.json
 timeout -k 10 400 python -u bench.py --config api_flush --verify > $O/api_flush.json 2> $O/api_flush.err || exit $?
 echo api_flush; python -c "import json; d=json.load(open('$O/api_flush.json')); d.pop('cycles'); print(json.dumps(d))"
+timeout -k 10 200 python -u tools/bench_crc.py --verify > $O/crc_lanes.json 2> $O/crc_lanes.err || exit $?
+timeout -k 10 200 python -u tools/bench_crc.py --crc-load 8 > $O/crc_group.json 2> $O/crc_group.err || exit $?
+echo crc; cat $O/crc_lanes.json $O/crc_group.json
 timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit $?
 timeout -k 10 900 python -u -m pytest tests -q --timeout 120 --timeout-method thread -m gpu > $O/pytest_gpu.log 2>&1
 rc=$?; echo "gpu suite rc=$rc"; tail -3 $O/pytest_gpu.log
