@@ -161,6 +161,14 @@ namespace {
 
 int member_bind(nkv_group* grp, int i) { return st(hipSetDevice(grp->dev[i])); }
 
+// bytes from member j's device memory to member i's, on member i's stream (a
+// plain device copy when both are the same GPU, else a peer copy over xGMI)
+hipError_t copy_between(nkv_group* grp, int i, void* dst, int j, const void* src, size_t bytes) {
+    if (grp->dev[i] == grp->dev[j])
+        return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, grp->ctx[i]->stream);
+    return hipMemcpyPeerAsync(dst, grp->dev[i], src, grp->dev[j], bytes, grp->ctx[i]->stream);
+}
+
 // All-gather `bytes` from src[i] (member i) into dst[i] (g * bytes on member i),
 // on the members' streams.
 int allgather(nkv_group* grp, const void* const* src, void* const* dst, size_t bytes) {
@@ -189,8 +197,7 @@ int allgather(nkv_group* grp, const void* const* src, void* const* dst, size_t b
         TRY(member_bind(grp, i));
         for (int j = 0; j < g; ++j) {
             HIPTRY(hipStreamWaitEvent(grp->ctx[i]->stream, grp->ev[j], 0));
-            HIPTRY(hipMemcpyPeerAsync(static_cast<uint8_t*>(dst[i]) + bytes * j, grp->dev[i], src[j], grp->dev[j],
-                                      bytes, grp->ctx[i]->stream));
+            HIPTRY(copy_between(grp, i, static_cast<uint8_t*>(dst[i]) + bytes * j, j, src[j], bytes));
         }
         TRY(make_event(&grp->ev2[i]));
         HIPTRY(hipEventRecord(grp->ev2[i], grp->ctx[i]->stream));
@@ -559,8 +566,7 @@ int nkv_group_tree_fetch(nkv_group* grp, uint8_t* nodes_out, uint8_t* img_out) t
         const uint8_t* lv = static_cast<const uint8_t*>(grp->levels[r].p);
         for (int L = 0; L <= k; ++L) {
             const uint64_t dst = start_of(n, L) + uint64_t(r) * (grp->span >> L);
-            HIPTRY(hipMemcpyPeerAsync(full + 20 * dst, grp->dev[0], lv + 20 * start_of(m, L), grp->dev[r],
-                                      20 * count_of(m, L), c0->stream));
+            HIPTRY(copy_between(grp, 0, full + 20 * dst, r, lv + 20 * start_of(m, L), 20 * count_of(m, L)));
         }
     }
     if (grp->G > 1) {
