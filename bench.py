@@ -91,6 +91,7 @@ def parse():
     ap.add_argument("--leaf-load", type=int, default=0,
                     help="NKV_OPT_LEAF_LOAD override (0 = library default 4: 128-byte register runs for aligned "
                          "values; 11: the staged paths for every value)")
+    ap.add_argument("--queue-split", type=int, default=-1, help="NKV_OPT_QUEUE_SPLIT override")
     ap.add_argument("--queue-waves", type=int, default=0, help="NKV_OPT_QUEUE_WAVES override (1..3)")
     ap.add_argument("--records-fused", type=int, default=-1, help="NKV_OPT_RECORDS_FUSED override (0, 1)")
     ap.add_argument("--leaves", type=int, default=1 << 20)

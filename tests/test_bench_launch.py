@@ -203,3 +203,26 @@ def test_preroll_same_step_count_on_every_rank():
         p.join(timeout=60)
     assert res[0][0] == res[1][0] == res[0][1] == res[1][1]
     assert res[0][0] % 8 == 0 and min(res[0][2], res[1][2]) >= 0.1
+
+
+def test_every_option_flag_reaches_the_context(monkeypatch):
+    """bench.set_options maps each override flag to its NKV_OPT_* key (no GPU:
+    a recording stand-in for the context)."""
+    from nakevaleng_amd import _lib
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--leaf-load", "11", "--queue-split", "8", "--queue-waves", "2",
+                                      "--records-fused", "0", "--bucket", "1", "--table-lanes", "3"])
+    args = bench.parse()
+
+    class Rec:
+        def __init__(self):
+            self.opts = {}
+
+        def set_option(self, k, v):
+            self.opts[k] = v
+    r = Rec()
+    bench.set_options(args, _lib, r)
+    assert r.opts == {_lib.NKV_OPT_LEAF_LOAD: 11, _lib.NKV_OPT_QUEUE_SPLIT: 8, _lib.NKV_OPT_QUEUE_WAVES: 2,
+                      _lib.NKV_OPT_RECORDS_FUSED: 0, _lib.NKV_OPT_BUCKET: 1, _lib.NKV_OPT_TABLE_LANES: 3}
+    for cfg in ("sstable4k", "mixed", "records", "records_verify", "one_tree", "runs4", "api_flush"):
+        monkeypatch.setattr(sys, "argv", ["bench.py", "--config", cfg])
+        assert bench.parse().config == cfg
