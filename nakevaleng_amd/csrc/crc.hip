@@ -140,9 +140,15 @@ __device__ __forceinline__ uint32_t crc_span_lines(const uint8_t* s, uint64_t le
                 for (int j = 1; j < 32; ++j) x = lane_x_next(x, w[j], la0, la1);
                 crc = lane_x_last(x, la0, la1);
             } else {
-                const uint64_t lo = s4 > b0 ? (s4 - b0) >> 2 : 0;
-                const uint64_t hi = e4 - b0 >= 128 ? 32 : (e4 - b0) >> 2;
-                for (uint32_t j = uint32_t(lo); j < uint32_t(hi); ++j) crc = lane_x_last(crc ^ w[j], la0, la1);
+                // a span's first or last line: every word steps, the ones outside
+                // [s4, e4) are discarded (static indices keep the line in VGPRs)
+                const uint32_t lo = s4 > b0 ? uint32_t((s4 - b0) >> 2) : 0u;
+                const uint32_t hi = e4 - b0 >= 128 ? 32u : uint32_t((e4 - b0) >> 2);
+#pragma unroll
+                for (int j = 0; j < 32; ++j) {
+                    const uint32_t u = lane_x_last(crc ^ w[j], la0, la1);
+                    crc = (uint32_t(j) >= lo && uint32_t(j) < hi) ? u : crc;
+                }
             }
         }
 #pragma unroll
