@@ -37,6 +37,10 @@
 #include <unordered_map>
 #include <vector>
 
+#if defined(__SSE2__)
+#include <emmintrin.h>
+#endif
+
 #include "nkv_merkle.h"
 
 namespace nkv {
@@ -84,6 +88,12 @@ class Session {
     // device copy at once (nkv_host_stream), so the copy overlaps the rest of
     // the NewLeaf loop.
     static constexpr uint64_t kStreamChunk = uint64_t(32) << 20;
+    // Values of at least kStreamCopy bytes go to the arena with non-temporal
+    // stores: the arena is written once and then read by the DMA engine, so
+    // pulling its lines into the cache first (the read-for-ownership of a
+    // plain store) only costs memory bandwidth.  Fence() orders them before
+    // any DMA that reads the arena.
+    static constexpr size_t kStreamCopy = 256;
     std::pair<std::shared_ptr<Batch>, uint64_t> AddLeaf(const uint8_t* data, size_t n) {
         if (!batch_ || batch_->resolved) {
             batch_ = std::make_shared<Batch>();
@@ -93,12 +103,13 @@ class Session {
         }
         const uint64_t at = (used_ + 15) & ~uint64_t(15);
         Reserve(at + n);
-        if (n) std::memcpy(static_cast<uint8_t*>(arena_) + at, data, n);
+        CopyIn(static_cast<uint8_t*>(arena_) + at, data, n);
         batch_->off.push_back(at);
         batch_->len.push_back(n);
         used_ = at + n;
         if (stream_ && used_ >= streamed_ + kStreamChunk) {
             streamed_ = used_ - used_ % kStreamChunk;
+            Fence();
             check(nkv_host_stream(ctx_, arena_, streamed_), "nkv_host_stream");
         }
         return {batch_, batch_->off.size() - 1};
@@ -115,11 +126,41 @@ class Session {
         if (b.resolved) return;
         const uint64_t n = b.off.size();
         b.digests.assign(20 * n, 0);
+        Fence();
         check(nkv_leaf_hash(ctx_, arena(), b.off.data(), b.len.data(), n, b.digests.data()), "NewLeaf");
         b.resolved = true;
     }
 
+    // makes the arena's non-temporal stores visible to the DMA engine
+    static void Fence() {
+#if defined(__SSE2__)
+        _mm_sfence();
+#endif
+    }
+
    private:
+    // dst is 16-byte aligned (AddLeaf's places)
+    static void CopyIn(uint8_t* dst, const uint8_t* src, size_t n) {
+#if defined(__SSE2__)
+        if (n >= kStreamCopy) {
+            const size_t body = n & ~size_t(63);
+            for (size_t i = 0; i < body; i += 64) {
+                const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i));
+                const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 16));
+                const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 32));
+                const __m128i d = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 48));
+                _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i), a);
+                _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 16), b);
+                _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 32), c);
+                _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 48), d);
+            }
+            if (n > body) std::memcpy(dst + body, src + body, n - body);
+            return;
+        }
+#endif
+        if (n) std::memcpy(dst, src, n);
+    }
+
     void Reserve(uint64_t bytes) {
         if (bytes <= cap_) return;
         uint64_t want = cap_ ? cap_ * 2 : (uint64_t(1) << 20);
@@ -128,6 +169,7 @@ class Session {
         check(nkv_host_alloc(ctx_, want, &p), "nkv_host_alloc");
         ++allocs_;
         if (arena_) {
+            Fence();
             std::memcpy(p, arena_, used_);
             nkv_host_free(ctx_, arena_);
         }
@@ -228,10 +270,13 @@ class MerkleTree {  // merkletree.go:13-15
 
     std::vector<uint8_t> SerializeBytes() {
         std::vector<uint8_t> w;
-        std::deque<MerkleNode*> q{Root};
-        while (!q.empty()) {
-            MerkleNode* n = q.front();
-            q.pop_front();
+        std::vector<MerkleNode*> q{Root};  // BFS queue: q[head..) still to visit
+        if (!nodes_.empty()) {
+            q.reserve(nodes_.size());
+            w.reserve(21 * nodes_.size());
+        }
+        for (size_t head = 0; head < q.size(); ++head) {
+            MerkleNode* n = q[head];
             if (n->Left) q.push_back(n->Left);
             if (n->Right) q.push_back(n->Right);
             n->Serialize(w);
@@ -424,6 +469,7 @@ inline std::unique_ptr<MerkleTree> New(std::vector<MerkleNode> level, std::strin
     for (uint64_t i = 0; same_batch && i < n; ++i)
         same_batch = level[i].pend == b0 && level[i].pend_idx == i && !level[i].Left && !level[i].Right;
     if (same_batch) {
+        Session::Fence();
         check(nkv_tree_from_values(ctx, Session::Default().arena(), b0->off.data(), b0->len.data(), n,
                                    nullptr, nodes, nullptr),
               "New");
@@ -455,9 +501,10 @@ inline std::unique_ptr<MerkleTree> New(std::vector<MerkleNode> level, std::strin
     // `l := level[i]`), then parents level by level with the empty pad node
     auto& pool = t->nodes_;
     std::vector<MerkleNode*> below;
-    for (auto& x : level) {
+    below.reserve(n + 1);
+    for (auto& x : level) {  // `level` is New's own copy: move out of it
         x.Resolve();
-        pool.push_back(x);
+        pool.push_back(std::move(x));
         below.push_back(&pool.back());
     }
     t->n_ = n;
@@ -469,6 +516,7 @@ inline std::unique_ptr<MerkleTree> New(std::vector<MerkleNode> level, std::strin
         }
         std::vector<MerkleNode*> cur;
         const uint64_t s = nkv_level_start(n, L), c = nkv_level_count(n, L);
+        cur.reserve(c + 1);
         for (uint64_t i = 0; i < c; ++i) {
             MerkleNode m(std::vector<uint8_t>(nodes + 20 * (s + i), nodes + 20 * (s + i) + 20));
             m.Left = below[2 * i];

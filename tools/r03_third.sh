@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 3, third pass: the CRC kernel after the scratch fix, mixed (configs[2])
 # with two tables per step against one after another, records / records_verify
-# after the pruning, then tools/r03_pmc.sh (kernel summaries and PMC passes).
+# after the pruning, api_flush with the non-temporal arena copy, then tools/r03_pmc.sh (kernel summaries and PMC passes).
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
 O=gpurun_out/r03c
@@ -19,4 +19,6 @@ timeout -k 10 300 python -u bench.py --config mixed --tables 2 --table-lanes 1 $
 timeout -k 10 300 python -u bench.py --config records $N --verify > $O/records.json 2> $O/records.err || exit $?
 timeout -k 10 300 python -u bench.py --config records_verify $N --verify > $O/records_verify.json 2> $O/records_verify.err || exit $?
 for f in mixed mixed2 mixed2_serial mixed_b mixed2_b mixed2_serial_b records records_verify; do python -c "import json; d=json.load(open('$O/$f.json')); print('$f', d['value'], d['ms_per_step'], d.get('sclk_mhz'), d['kernel_ms'], d.get('verified_vs_oracle'))"; done
+timeout -k 10 600 python -u bench.py --config api_flush --verify > $O/api_flush.json 2> $O/api_flush.err || exit $?
+cat $O/api_flush.json
 bash tools/r03_pmc.sh
