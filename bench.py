@@ -30,12 +30,13 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.
 # issuing one VALU instruction per VALU_CYCLES cycles (the half-rate ops
 # v_add3 / v_alignbit / v_perm set the cadence, profiles/r01_valu_rate.txt),
 # VALU_PER_WAVE_BLOCK instructions per wave per 64-byte block (PMC
-# SQ_INSTS_VALU per launch / wave-blocks), 4096 bytes per
+# SQ_INSTS_VALU per launch / wave-blocks: leaf from the register-run kernel,
+# profiles/r03_leaf_valu_pmc.json; verify from round 2), 4096 bytes per
 # wave-block (64 lanes x 64 B):
 #   ceiling = SIMDS x f / (VALU_PER_WAVE_BLOCK x VALU_CYCLES) x 4096 B.
 SIMDS = 1024  # 256 CUs x 4
 VALU_CYCLES = 4.0
-VALU_PER_WAVE_BLOCK = {"leaf": 618.5, "verify": 711.0}
+VALU_PER_WAVE_BLOCK = {"leaf": 623.0, "verify": 711.0}
 SHA1_VALU_CEILING_GBS = 4100.0  # fallback without a clock reading: tools/sha1_rate.hip at 2.37 GHz
 SEED = 0x6E616B65
 SEED_MIXED = 0x6E616B66

@@ -103,7 +103,8 @@ class Session {
         }
         const uint64_t at = (used_ + 15) & ~uint64_t(15);
         Reserve(at + n);
-        CopyIn(static_cast<uint8_t*>(arena_) + at, data, n);
+        if (nt_) CopyIn(static_cast<uint8_t*>(arena_) + at, data, n);
+        else if (n) std::memcpy(static_cast<uint8_t*>(arena_) + at, data, n);
         batch_->off.push_back(at);
         batch_->len.push_back(n);
         used_ = at + n;
@@ -116,6 +117,9 @@ class Session {
     }
     // NewLeaf streams settled arena chunks ahead of New (default on)
     void SetStreaming(bool on) { stream_ = on; }
+    // NewLeaf copies values of kStreamCopy bytes or more with non-temporal
+    // stores (default on; off: memcpy)
+    void SetNonTemporal(bool on) { nt_ = on; }
 
     const uint8_t* arena() const { return static_cast<const uint8_t*>(arena_); }
     // nkv_host_alloc calls so far: a sealed batch's arena is reused by the next
@@ -181,7 +185,7 @@ class Session {
     nkv_ctx* ctx_ = nullptr;
     void* arena_ = nullptr;
     uint64_t cap_ = 0, used_ = 0, epoch_ = 0, allocs_ = 0, streamed_ = 0;
-    bool stream_ = true;
+    bool stream_ = true, nt_ = true;
     std::shared_ptr<Batch> batch_;
 };
 

@@ -106,8 +106,47 @@ __device__ __forceinline__ void crc_header(const uint8_t* p, uint32_t& stored, u
     vs = at(22);
 }
 
+// A readable 128-byte line (zeros) for lanes that have no line of their own to
+// load: every line load of the span loop below is issued by every lane.
+__device__ __align__(128) uint4 g_crc_line[8];
+
+__device__ __forceinline__ void crc_line_load(const uint4* q, uint4 v[8]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = q[i];
+}
+
+// The aligned 128-byte line v at address b0 stepped into crc: every word of a
+// line inside [s4, e4), else (a span's first or last line) every word steps and
+// the ones outside are discarded (static indices keep the line in VGPRs).
+__device__ __forceinline__ uint32_t crc_line(uint32_t crc, const uint4 v[8], uint64_t b0, uint64_t s4, uint64_t e4,
+                                             uint32_t la0, uint32_t la1) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(v);
+    if (b0 >= s4 && b0 + 128 <= e4) {
+        uint32_t x = crc ^ w[0];
+#pragma unroll
+        for (int j = 1; j < 32; ++j) x = lane_x_next(x, w[j], la0, la1);
+        return lane_x_last(x, la0, la1);
+    }
+    const uint32_t lo = s4 > b0 ? uint32_t((s4 - b0) >> 2) : 0u;
+    const uint32_t hi = e4 - b0 >= 128 ? 32u : uint32_t((e4 - b0) >> 2);
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+        const uint32_t u = lane_x_last(crc ^ w[j], la0, la1);
+        crc = (uint32_t(j) >= lo && uint32_t(j) < hi) ? u : crc;
+    }
+    return crc;
+}
+
 // CRC-32/IEEE of [s, s + len) for every lane of the wave (dead lanes: len 0),
 // from whole aligned 128-byte lines, with the lane-private tables.
+//
+// Two line buffers in turn: line c + 1 loads while line c is checksummed.  The
+// loads are unconditional -- a lane past its last line reloads that line, a
+// lane with no line loads g_crc_line -- so every path issues the same loads and
+// the compiler's wait before a line's first word is vmcnt(8) (only the
+// line in flight may still be outstanding).  With the loads under per-lane
+// conditions, or a buffer copy at the loop end, its merged counts forced
+// vmcnt(0) in mid-line, which waited for the prefetch as well (4.67 TB/s).
 __device__ __forceinline__ uint32_t crc_span_lines(const uint8_t* s, uint64_t len, uint32_t la0, uint32_t la1) {
     uint32_t crc = 0xFFFFFFFFu;
     const uint64_t sa = uint64_t(reinterpret_cast<uintptr_t>(s));
@@ -119,40 +158,16 @@ __device__ __forceinline__ uint32_t crc_span_lines(const uint8_t* s, uint64_t le
     const uint64_t A = s4 & ~uint64_t(127);
     const uint32_t nl = e4 > s4 ? uint32_t((e4 - A + 127) >> 7) : 0u;
     const uint32_t nmax = crc_wave_max(nl);
+    const uint32_t last = nl ? nl - 1 : 0u;
     // s + (A - sa): stays a global pointer (no integer-to-pointer cast)
-    const uint4* q = reinterpret_cast<const uint4*>(s + (A - sa));
-    uint4 cur[8], nxt[8];
-    if (nl > 0) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) cur[i] = q[i];
-    }
-    for (uint32_t c = 0; c < nmax; ++c) {
-        if (c + 1 < nl) {
-#pragma unroll
-            for (int i = 0; i < 8; ++i) nxt[i] = q[8 * (c + 1) + i];
-        }
-        if (c < nl) {
-            const uint32_t* w = reinterpret_cast<const uint32_t*>(cur);
-            const uint64_t b0 = A + 128ull * c;
-            if (b0 >= s4 && b0 + 128 <= e4) {
-                uint32_t x = crc ^ w[0];
-#pragma unroll
-                for (int j = 1; j < 32; ++j) x = lane_x_next(x, w[j], la0, la1);
-                crc = lane_x_last(x, la0, la1);
-            } else {
-                // a span's first or last line: every word steps, the ones outside
-                // [s4, e4) are discarded (static indices keep the line in VGPRs)
-                const uint32_t lo = s4 > b0 ? uint32_t((s4 - b0) >> 2) : 0u;
-                const uint32_t hi = e4 - b0 >= 128 ? 32u : uint32_t((e4 - b0) >> 2);
-#pragma unroll
-                for (int j = 0; j < 32; ++j) {
-                    const uint32_t u = lane_x_last(crc ^ w[j], la0, la1);
-                    crc = (uint32_t(j) >= lo && uint32_t(j) < hi) ? u : crc;
-                }
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < 8; ++i) cur[i] = nxt[i];
+    const uint4* q = nl ? reinterpret_cast<const uint4*>(s + (A - sa)) : g_crc_line;
+    uint4 va[8], vb[8];
+    crc_line_load(q, va);
+    for (uint32_t c = 0; c < nmax; c += 2) {
+        crc_line_load(q + 8 * min(c + 1, last), vb);
+        if (c < nl) crc = crc_line(crc, va, A + 128ull * c, s4, e4, la0, la1);
+        crc_line_load(q + 8 * min(c + 2, last), va);
+        if (c + 1 < nl) crc = crc_line(crc, vb, A + 128ull * (c + 1), s4, e4, la0, la1);
     }
     const uint64_t tb = e4 > hb ? e4 : hb;
     for (uint64_t a = tb; a < ea; ++a) crc = lane_byte(crc, s[a - sa], la0);

@@ -19,7 +19,7 @@
 //   root_ms       Root.String()
 //   walk_ms / write_ms   Serialize: BFS walk of the live tree, file write
 //
-// Usage: api_flush N VLEN CYCLES DIR [STREAMING=1] [SEED]
+// Usage: api_flush N VLEN CYCLES DIR [STREAMING=1] [SEED] [NONTEMPORAL=1]
 #include <fcntl.h>
 #include <unistd.h>
 
@@ -56,7 +56,7 @@ static void fill(uint8_t* out, uint64_t n, uint64_t seed, int threads) {
 
 int main(int argc, char** argv) {
     if (argc < 5) {
-        std::fprintf(stderr, "usage: %s N VLEN CYCLES DIR [STREAMING] [SEED]\n", argv[0]);
+        std::fprintf(stderr, "usage: %s N VLEN CYCLES DIR [STREAMING] [SEED] [NONTEMPORAL]\n", argv[0]);
         return 2;
     }
     const uint64_t n = std::strtoull(argv[1], nullptr, 10), vlen = std::strtoull(argv[2], nullptr, 10);
@@ -64,10 +64,12 @@ int main(int argc, char** argv) {
     const std::string dir = argv[4];
     const bool streaming = argc > 5 ? std::atoi(argv[5]) != 0 : true;
     const uint64_t seed = argc > 6 ? std::strtoull(argv[6], nullptr, 0) : 0x6E616B65ull;
+    const bool nontemporal = argc > 7 ? std::atoi(argv[7]) != 0 : true;
     std::vector<uint8_t> memtable(n * vlen);
     fill(memtable.data(), memtable.size(), seed, 16);
     Session& S = Session::Default();
     S.SetStreaming(streaming);
+    S.SetNonTemporal(nontemporal);
     check(nkv_ctx_set_timing(S.ctx(), NKV_TIMING_EVENTS), "timing");
     for (int cyc = 0; cyc < cycles; ++cyc) {
         const std::string fname = dir + "/api_flush-1-" + std::to_string(cyc) + "-metadata.db";
@@ -94,12 +96,12 @@ int main(int argc, char** argv) {
         if (nkv_ctx_last_host_timing(S.ctx(), &up, &ker, &down) != NKV_OK) up = ker = down = -1;
         const double total = ms(t0, t5);
         std::printf(
-            "{\"cycle\": %d, \"n\": %llu, \"value_bytes\": %llu, \"streaming\": %d, \"gib_s\": %.3f, "
+            "{\"cycle\": %d, \"n\": %llu, \"value_bytes\": %llu, \"streaming\": %d, \"nontemporal\": %d, \"gib_s\": %.3f, "
             "\"total_ms\": %.3f, \"newleaf_ms\": %.3f, \"new_call_ms\": %.3f, \"upload_ms\": %.3f, "
             "\"kernels_ms\": %.3f, \"download_ms\": %.3f, \"materialize_ms\": %.3f, \"root_ms\": %.3f, "
             "\"walk_ms\": %.3f, \"write_ms\": %.3f, \"image_bytes\": %zu, \"arena_allocs\": %llu, "
             "\"root\": \"%s\"}\n",
-            cyc, (unsigned long long)n, (unsigned long long)vlen, int(streaming),
+            cyc, (unsigned long long)n, (unsigned long long)vlen, int(streaming), int(nontemporal),
             double(n * vlen) / (total * 1e-3) / double(1ull << 30), total, ms(t0, t1),
             tree->LastNewTiming().call_ms, up, ker, down, tree->LastNewTiming().materialize_ms, ms(t2, t3),
             ms(t3, t4), ms(t4, t5), img.size(), (unsigned long long)S.arena_allocs(), root.c_str());
