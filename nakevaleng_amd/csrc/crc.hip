@@ -110,17 +110,25 @@ __device__ __forceinline__ void crc_header(const uint8_t* p, uint32_t& stored, u
 // load: every line load of the span loop below is issued by every lane.
 __device__ __align__(128) uint4 g_crc_line[8];
 
-__device__ __forceinline__ void crc_line_load(const uint4* q, uint4 v[8]) {
+// A line is eight 16-byte vector loads into vector registers: as vectors (not
+// uint4 structs, whose fields the compiler splits into dword loads and
+// re-merges) the loads stay aligned dwordx4 at offsets 0, 16, ... 112.
+typedef uint32_t crc_v4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void crc_line_load(const uint4* q, crc_v4 v[8]) {
+    const crc_v4* p = reinterpret_cast<const crc_v4*>(q);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = q[i];
+    for (int i = 0; i < 8; ++i) v[i] = p[i];
 }
 
 // The aligned 128-byte line v at address b0 stepped into crc: every word of a
 // line inside [s4, e4), else (a span's first or last line) every word steps and
 // the ones outside are discarded (static indices keep the line in VGPRs).
-__device__ __forceinline__ uint32_t crc_line(uint32_t crc, const uint4 v[8], uint64_t b0, uint64_t s4, uint64_t e4,
+__device__ __forceinline__ uint32_t crc_line(uint32_t crc, const crc_v4 v[8], uint64_t b0, uint64_t s4, uint64_t e4,
                                              uint32_t la0, uint32_t la1) {
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(v);
+    uint32_t w[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) w[j] = v[j >> 2][j & 3];
     if (b0 >= s4 && b0 + 128 <= e4) {
         uint32_t x = crc ^ w[0];
 #pragma unroll
@@ -137,40 +145,71 @@ __device__ __forceinline__ uint32_t crc_line(uint32_t crc, const uint4 v[8], uin
     return crc;
 }
 
+// Bytes j0 .. j0 + nb - 1 (nb 0..3) of the little-endian word hw stepped into crc.
+__device__ __forceinline__ uint32_t crc_word_bytes(uint32_t crc, uint32_t hw, uint32_t j0, uint32_t nb,
+                                                   uint32_t la0) {
+#pragma unroll
+    for (uint32_t j = 0; j < 3; ++j)
+        if (j < nb) crc = lane_byte(crc, (hw >> (8u * (j0 + j))) & 0xFFu, la0);
+    return crc;
+}
+
+// The first line of the record at rec that the span loop can use: the line of
+// its Key || Value's first aligned word (rec + 30 rounded up to 4) when that
+// line also holds header byte 29 (so it is mapped whatever the record's
+// length), else the header's last line.
+__device__ __forceinline__ const uint4* crc_record_line(const uint8_t* rec) {
+    const uint64_t ra = uint64_t(reinterpret_cast<uintptr_t>(rec));
+    const uint64_t b29 = ra + 29, A = ((ra + 33) & ~uint64_t(3)) & ~uint64_t(127);
+    return reinterpret_cast<const uint4*>(rec + ((A <= b29 ? A : b29 & ~uint64_t(127)) - ra));
+}
+
 // CRC-32/IEEE of [s, s + len) for every lane of the wave (dead lanes: len 0),
 // from whole aligned 128-byte lines, with the lane-private tables.
 //
+// The caller has loaded hw, the aligned word holding the span's first byte
+// (used when the span starts inside it); va holds the line at va_from, and
+// when that is the span's first line the loop starts from it.  The records
+// kernel loads that line together with the record header, so the header's
+// line is read from memory once (loaded after the header, as in the first
+// version, the line had left the L2 under the stream and was read again:
+// 1.086 x the payload read, now 1.055).  The 0-3 tail bytes come from one
+// aligned word loaded before the loop.
+//
 // Two line buffers in turn: line c + 1 loads while line c is checksummed.  The
-// loads are unconditional -- a lane past its last line reloads that line, a
-// lane with no line loads g_crc_line -- so every path issues the same loads and
-// the compiler's wait before a line's first word is vmcnt(8) (only the
-// line in flight may still be outstanding).  With the loads under per-lane
+// loop's loads are unconditional -- a line past the span (or a lane with none)
+// loads g_crc_line, which stays in the caches -- so every path issues the same
+// loads and the compiler's wait before a line's first word is vmcnt(8) (only
+// the line in flight may still be outstanding).  With the loads under per-lane
 // conditions, or a buffer copy at the loop end, its merged counts forced
 // vmcnt(0) in mid-line, which waited for the prefetch as well (4.67 TB/s).
-__device__ __forceinline__ uint32_t crc_span_lines(const uint8_t* s, uint64_t len, uint32_t la0, uint32_t la1) {
-    uint32_t crc = 0xFFFFFFFFu;
+__device__ __forceinline__ uint32_t crc_span_lines(const uint8_t* s, uint64_t len, uint32_t hw, crc_v4 va[8],
+                                                   const uint4* va_from, uint32_t la0, uint32_t la1) {
     const uint64_t sa = uint64_t(reinterpret_cast<uintptr_t>(s));
     const uint64_t ea = sa + len;
     const uint64_t s4 = (sa + 3) & ~uint64_t(3);
     const uint64_t e4 = ea & ~uint64_t(3);
     const uint64_t hb = s4 < ea ? s4 : ea;
-    for (uint64_t a = sa; a < hb; ++a) crc = lane_byte(crc, s[a - sa], la0);
+    const uint64_t tb = e4 > hb ? e4 : hb;
     const uint64_t A = s4 & ~uint64_t(127);
     const uint32_t nl = e4 > s4 ? uint32_t((e4 - A + 127) >> 7) : 0u;
     const uint32_t nmax = crc_wave_max(nl);
-    const uint32_t last = nl ? nl - 1 : 0u;
     // s + (A - sa): stays a global pointer (no integer-to-pointer cast)
-    const uint4* q = nl ? reinterpret_cast<const uint4*>(s + (A - sa)) : g_crc_line;
-    uint4 va[8], vb[8];
-    crc_line_load(q, va);
+    const uint4* q = reinterpret_cast<const uint4*>(s + (A - sa));
+    auto line = [&](uint32_t c) { return c < nl ? q + 8 * c : g_crc_line; };
+    // the tail word holds bytes of the span when there is a tail
+    const uint32_t* tp = ea > tb ? reinterpret_cast<const uint32_t*>(s + (tb - sa)) : reinterpret_cast<const uint32_t*>(g_crc_line);
+    const uint32_t tw = *tp;
+    if (line(0) != va_from) crc_line_load(line(0), va);
+    uint32_t crc = crc_word_bytes(0xFFFFFFFFu, hw, uint32_t(sa & 3u), uint32_t(hb - sa), la0);
+    crc_v4 vb[8];
     for (uint32_t c = 0; c < nmax; c += 2) {
-        crc_line_load(q + 8 * min(c + 1, last), vb);
+        crc_line_load(line(c + 1), vb);
         if (c < nl) crc = crc_line(crc, va, A + 128ull * c, s4, e4, la0, la1);
-        crc_line_load(q + 8 * min(c + 2, last), va);
+        crc_line_load(line(c + 2), va);
         if (c + 1 < nl) crc = crc_line(crc, vb, A + 128ull * (c + 1), s4, e4, la0, la1);
     }
-    const uint64_t tb = e4 > hb ? e4 : hb;
-    for (uint64_t a = tb; a < ea; ++a) crc = lane_byte(crc, s[a - sa], la0);
+    crc = crc_word_bytes(crc, tw, 0u, uint32_t(ea - tb), la0);
     return ~crc;
 }
 
@@ -186,45 +225,61 @@ __global__ __launch_bounds__(kCrcLanesWG) void k_crc_lanes(const uint8_t* __rest
                                                             const uint64_t* __restrict__ len, uint64_t stream_len,
                                                             uint64_t n, uint32_t* __restrict__ out,
                                                             unsigned long long* __restrict__ stats, Gate gate) {
+    constexpr int WG = kCrcLanesWG;
     __shared__ uint32_t tab[kLaneTabWords];
     if (!gate.open()) return;
-    for (uint32_t i = threadIdx.x; i < kLaneTabWords; i += kCrcLanesWG) {
+    for (uint32_t i = threadIdx.x; i < kLaneTabWords; i += WG) {
         const uint32_t half = i >> 14, e = (i >> 6) & 255u, k = 2u * half + ((i >> 5) & 1u);
         tab[i] = c_crc.t[k][e];  // every copy c = i & 31 holds the same entry
     }
     __syncthreads();
     // lane constants of the two halves: the copy offset (byte 0), the half (byte 2)
     const uint32_t la0 = (threadIdx.x & 31u) * 4u, la1 = la0 | 0x10000u;
-    const uint64_t stride = uint64_t(gridDim.x) * kCrcLanesWG;
-    const uint64_t w0 = uint64_t(blockIdx.x) * kCrcLanesWG + (threadIdx.x & ~63u);  // this wave's first span
+    const uint64_t stride = uint64_t(gridDim.x) * WG;
+    const uint64_t w0 = uint64_t(blockIdx.x) * WG + (threadIdx.x & ~63u);  // this wave's first span
     for (uint64_t wb = w0; wb < n; wb += stride) {  // wave-uniform loop
         const uint64_t i = wb + (threadIdx.x & 63u);
         const bool live = i < n;
+        // (loading the next span's offset a span ahead measured the same)
+        const uint64_t off_i = live ? off[i] : 0;
+        const uint64_t len_i = live && !RECORDS ? len[i] : 0;
         const uint8_t* s = base;
         uint64_t L = 0;
         uint32_t stored = 0;
         bool hdr_bad = false;
-        if (live) {
-            if (RECORDS) {
-                const uint64_t r = off[i];
-                if (header_in(r, stream_len)) {
-                    uint64_t ks, vs;
-                    crc_header(base + r, stored, ks, vs);
-                    if (ks <= stream_len && vs <= stream_len && r + 30 + ks + vs <= stream_len) {
-                        s = base + r + 30;
-                        L = ks + vs;
-                    } else {
-                        hdr_bad = true;
-                    }
-                } else {
-                    hdr_bad = true;
-                }
+        crc_v4 va[8];
+        const uint4* first = g_crc_line;
+        uint32_t hw = 0;
+        if (RECORDS) {
+            // The header, the aligned word holding byte 29 (the span Key || Value
+            // starts at +30, so its 0-3 head bytes share that word) and the
+            // span's first line, issued together: one memory read of the
+            // header's line.  Lanes without a header in the stream read
+            // g_crc_line instead.
+            const uint64_t r = live ? off_i : 0;
+            const bool hin = live && header_in(r, stream_len);
+            const uint8_t* rec = hin ? base + r : reinterpret_cast<const uint8_t*>(g_crc_line);
+            first = crc_record_line(rec);
+            crc_line_load(first, va);
+            const uint64_t ra = uint64_t(reinterpret_cast<uintptr_t>(rec));
+            hw = *reinterpret_cast<const uint32_t*>(rec + (((ra + 29) & ~uint64_t(3)) - ra));
+            uint64_t ks, vs;
+            crc_header(rec, stored, ks, vs);
+            if (!hin) {
+                hdr_bad = live;
+            } else if (ks <= stream_len && vs <= stream_len && r + 30 + ks + vs <= stream_len) {
+                s = base + r + 30;
+                L = ks + vs;
             } else {
-                s = base + off[i];
-                L = len[i];
+                hdr_bad = true;
             }
+        } else if (live) {
+            s = base + off_i;
+            L = len_i;
+            const uint32_t m = uint32_t(reinterpret_cast<uintptr_t>(s) & 3u);
+            hw = *(m && L ? reinterpret_cast<const uint32_t*>(s - m) : reinterpret_cast<const uint32_t*>(g_crc_line));
         }
-        const uint32_t crc = crc_span_lines(s, L, la0, la1);
+        const uint32_t crc = crc_span_lines(s, L, hw, va, RECORDS ? first : nullptr, la0, la1);
         if (live) {
             if (out) out[i] = crc;
             if (RECORDS && stats) {
@@ -431,10 +486,12 @@ static void launch_crc(int variant, const uint8_t* base, const uint64_t* off, co
     if (variant == 8) return launch_crc_group<RECORDS, 8, 512>(2, base, off, len, stream_len, n, out, stats, s, gate);
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const uint64_t want = (n + kCrcLanesWG - 1) / kCrcLanesWG;
-    const uint32_t grid = uint32_t(std::max<uint64_t>(1, std::min<uint64_t>(want, uint64_t(cus))));
-    hipLaunchKernelGGL((k_crc_lanes<RECORDS>), dim3(grid), dim3(kCrcLanesWG), 0, s, base, off, len, stream_len, n,
-                       out, stats, gate);
+    auto go = [&](auto kernel, int wg) {
+        const uint64_t want = (n + wg - 1) / wg;
+        const uint32_t grid = uint32_t(std::max<uint64_t>(1, std::min<uint64_t>(want, uint64_t(cus))));
+        hipLaunchKernelGGL(kernel, dim3(grid), dim3(wg), 0, s, base, off, len, stream_len, n, out, stats, gate);
+    };
+    go(k_crc_lanes<RECORDS>, kCrcLanesWG);
 }
 
 hipError_t launch_crc_spans(const uint8_t* base, const uint64_t* off, const uint64_t* len, uint64_t n,

@@ -427,6 +427,8 @@ def test_pruned_variants_are_refused(nkv):
     for v in (0, 4, 5):
         assert L.nkv_ctx_set_option(ctx.h, _lib.NKV_OPT_QUEUE_WAVES, v) == _lib.NKV_ERR_INVALID
     assert L.nkv_ctx_set_option(ctx.h, _lib.NKV_OPT_QUEUE_WAVES, 3) == _lib.NKV_OK
+    for v in (1, 2, 9, 10):  # the CRC kernel: lane-private tables (0) or the span groups (8)
+        assert L.nkv_ctx_set_option(ctx.h, _lib.NKV_OPT_CRC_LOAD, v) == _lib.NKV_ERR_INVALID
     for v in (0, 9):
         assert L.nkv_ctx_set_option(ctx.h, _lib.NKV_OPT_TABLE_LANES, v) == _lib.NKV_ERR_INVALID
     ctx.set_option(_lib.NKV_OPT_TABLE_LANES, 2)
