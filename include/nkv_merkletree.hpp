@@ -142,8 +142,8 @@ class Session {
 #endif
     }
 
-   private:
-    // dst is 16-byte aligned (AddLeaf's places)
+    // NewLeaf's arena copy (public for its CPU test); dst is 16-byte aligned
+    // (AddLeaf's places)
     static void CopyIn(uint8_t* dst, const uint8_t* src, size_t n) {
 #if defined(__SSE2__)
         if (n >= kStreamCopy) {
@@ -165,6 +165,7 @@ class Session {
         if (n) std::memcpy(dst, src, n);
     }
 
+   private:
     void Reserve(uint64_t bytes) {
         if (bytes <= cap_) return;
         uint64_t want = cap_ ? cap_ * 2 : (uint64_t(1) << 20);

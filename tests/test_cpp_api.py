@@ -27,6 +27,20 @@ def test_cpp_mirror_compiles(tmp_path):
     assert os.path.exists(build_binary(str(tmp_path)))
 
 
+def test_arena_copy_in_cpu(tmp_path):
+    """NewLeaf's arena copy (non-temporal stores from 256 bytes up) is exact for
+    every length and source alignment, and writes nothing past the value."""
+    from nakevaleng_amd import build as b
+    so = b.build()
+    libdir = os.path.dirname(so)
+    exe = os.path.join(str(tmp_path), "test_copy_in")
+    subprocess.check_call(["g++", "-std=c++17", "-O2", "-Wall", "-I", os.path.join(ROOT, "include"),
+                           os.path.join(ROOT, "tests", "cpp", "test_copy_in.cpp"), "-L", libdir, "-lnkvmerkle",
+                           f"-Wl,-rpath,{libdir}", "-o", exe])
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0 and out.stdout.startswith("ok"), out.stdout + out.stderr
+
+
 @pytest.mark.gpu
 def test_cpp_mirror_on_gpu(tmp_path, oracle):
     exe = build_binary(str(tmp_path))
