@@ -30,13 +30,14 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.
 # issuing one VALU instruction per VALU_CYCLES cycles (the half-rate ops
 # v_add3 / v_alignbit / v_perm set the cadence, profiles/r01_valu_rate.txt),
 # VALU_PER_WAVE_BLOCK instructions per wave per 64-byte block (PMC
-# SQ_INSTS_VALU per launch / wave-blocks: leaf from the register-run kernel,
-# profiles/r03_leaf_valu_pmc.json; verify from round 2), 4096 bytes per
+# SQ_INSTS_VALU per launch / wave-blocks of payload: leaf from the register-run
+# kernel, profiles/r03_leaf_valu_pmc.json; records (k_leaf_records) and verify
+# (k_leaf_verify) per 64 bytes of Value, profiles/r03_records_pmc.json), 4096 bytes per
 # wave-block (64 lanes x 64 B):
 #   ceiling = SIMDS x f / (VALU_PER_WAVE_BLOCK x VALU_CYCLES) x 4096 B.
 SIMDS = 1024  # 256 CUs x 4
 VALU_CYCLES = 4.0
-VALU_PER_WAVE_BLOCK = {"leaf": 623.0, "verify": 711.0}
+VALU_PER_WAVE_BLOCK = {"leaf": 623.0, "records": 631.7, "verify": 737.9}
 SHA1_VALU_CEILING_GBS = 4100.0  # fallback without a clock reading: tools/sha1_rate.hip at 2.37 GHz
 SEED = 0x6E616B65
 SEED_MIXED = 0x6E616B66
@@ -378,12 +379,17 @@ def build_tables(args, torch, _lib, L, ctx, rank, T, device="cuda"):
     return tabs
 
 
-def valu_ceiling(mhz, verify):
+def valu_kind(config):
+    """Which VALU_PER_WAVE_BLOCK entry a config's leaf kernel is priced at."""
+    return {"records_verify": "verify", "records": "records"}.get(config, "leaf")
+
+
+def valu_ceiling(mhz, kind):
     """GB/s the leaf kernel would reach issuing one VALU per VALU_CYCLES on every
     SIMD at the measured clock (None without a clock reading)."""
     if not mhz:
         return None
-    per = VALU_PER_WAVE_BLOCK["verify" if verify else "leaf"]
+    per = VALU_PER_WAVE_BLOCK[kind]
     return SIMDS * mhz * 1e6 / (per * VALU_CYCLES) * 4096 / 1e9
 
 
@@ -657,7 +663,7 @@ def main():
         value = total_bytes / elapsed / 2**30
         table_bytes = t0_["nbytes"]
         achieved = table_bytes / (leaf_ms * 1e-3) / 1e9  # algorithmic payload bytes per K1 launch
-        ceiling = valu_ceiling(sclk, verify_crc)
+        ceiling = valu_ceiling(sclk, valu_kind(args.config))
         traffic, traffic_bounds = pmc_traffic(args, n, vlen, table_bytes)
         out = {
             "metric": "GiB/s Merkle leaf-hash + tree-reduce over device-resident record blocks",
@@ -701,7 +707,7 @@ def main():
                 # VALU-issue ceiling at the measured clock (sclk_mhz) and the
                 # fraction of it the leaf kernel reached
                 "valu_ceiling": round(ceiling, 1) if ceiling else SHA1_VALU_CEILING_GBS,
-                "valu_ceiling_basis": (f"{SIMDS} SIMDs x {sclk:.0f} MHz / ({VALU_PER_WAVE_BLOCK['verify' if verify_crc else 'leaf']}"
+                "valu_ceiling_basis": (f"{SIMDS} SIMDs x {sclk:.0f} MHz / ({VALU_PER_WAVE_BLOCK[valu_kind(args.config)]}"
                                        f" VALU per wave-block x {VALU_CYCLES:g} cycles) x 4096 B") if ceiling else
                                       "tools/sha1_rate.hip at 2.37 GHz (no clock reading)",
                 "valu_frac": round(achieved / (ceiling or SHA1_VALU_CEILING_GBS), 4),
@@ -876,7 +882,7 @@ def main_capi(args, T):
     leaf_ms = leaf_ms_tot / max(calls, 1)
     table_bytes = per[0][0]["nbytes"]
     achieved = table_bytes / (leaf_ms * 1e-3) / 1e9 if calls else None
-    ceiling = valu_ceiling(sclk, args.config == "records_verify")
+    ceiling = valu_ceiling(sclk, valu_kind(args.config))
     out = {
         "metric": "GiB/s Merkle leaf-hash + tree-reduce over device-resident record blocks",
         "value": round(nbytes * args.steps / elapsed / 2**30, 2),

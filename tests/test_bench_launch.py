@@ -226,3 +226,16 @@ def test_every_option_flag_reaches_the_context(monkeypatch):
     for cfg in ("sstable4k", "mixed", "records", "records_verify", "one_tree", "runs4", "api_flush"):
         monkeypatch.setattr(sys, "argv", ["bench.py", "--config", cfg])
         assert bench.parse().config == cfg
+
+
+def test_valu_ceiling_prices_each_kernel_at_its_own_count():
+    """records / records_verify are priced at their kernels' PMC counts
+    (profiles/r03_records_pmc.json), every other config at the leaf kernel's."""
+    assert bench.valu_kind("records_verify") == "verify"
+    assert bench.valu_kind("records") == "records"
+    for c in ("cfg2", "mixed", "runs4", "one_tree"):
+        assert bench.valu_kind(c) == "leaf"
+    assert bench.valu_ceiling(None, "leaf") is None
+    # 1024 SIMDs at 2.2 GHz, one VALU per 4 cycles, 623 per 4 KiB wave-block
+    assert abs(bench.valu_ceiling(2200.0, "leaf") - 1024 * 2.2e9 / (623.0 * 4) * 4096 / 1e9) < 1e-6
+    assert bench.valu_ceiling(2200.0, "verify") < bench.valu_ceiling(2200.0, "records") < bench.valu_ceiling(2200.0, "leaf")
