@@ -23,20 +23,17 @@
 // no CPU hashing path: without a HIP device every hashing call throws.
 #pragma once
 
-#include <algorithm>
 #include <array>
 #include <chrono>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <deque>
 #include <exception>
-#include <initializer_list>
-#include <iterator>
 #include <memory>
 #include <stdexcept>
 #include <string>
 #include <thread>
-#include <type_traits>
 #include <unordered_map>
 #include <vector>
 
@@ -193,84 +190,8 @@ class Session {
     std::shared_ptr<Batch> batch_;
 };
 
-// MerkleNode.Data: a byte string that keeps up to kInline bytes (a digest)
-// inside the node.  Go's []byte is a view into shared storage, so the Go
-// shim's New slices one digest array for every node; a std::vector here
-// would cost a heap allocation per node (2 Mi of them per 1 Mi-leaf tree).
-class Bytes {
-   public:
-    static constexpr size_t kInline = 24;
-    Bytes() = default;
-    Bytes(const uint8_t* p, size_t n) { assign(p, p + n); }
-    Bytes(std::initializer_list<uint8_t> v) { assign(v.begin(), v.end()); }
-    Bytes(const std::vector<uint8_t>& v) { assign(v.begin(), v.end()); }  // NOLINT: implicit, as Go's []byte
-    Bytes(const Bytes& o) { assign(o.begin(), o.end()); }
-    Bytes(Bytes&& o) noexcept : n_(o.n_), heap_(std::move(o.heap_)) {
-        std::memcpy(in_, o.in_, sizeof in_);
-        o.n_ = 0;
-    }
-    Bytes& operator=(const Bytes& o) {
-        if (this != &o) assign(o.begin(), o.end());
-        return *this;
-    }
-    Bytes& operator=(Bytes&& o) noexcept {
-        if (this != &o) {
-            n_ = o.n_;
-            heap_ = std::move(o.heap_);
-            std::memcpy(in_, o.in_, sizeof in_);
-            o.n_ = 0;
-        }
-        return *this;
-    }
-    size_t size() const { return n_; }
-    bool empty() const { return n_ == 0; }
-    uint8_t* data() { return heap_ ? heap_.get() : in_; }
-    const uint8_t* data() const { return heap_ ? heap_.get() : in_; }
-    uint8_t* begin() { return data(); }
-    uint8_t* end() { return data() + n_; }
-    const uint8_t* begin() const { return data(); }
-    const uint8_t* end() const { return data() + n_; }
-    uint8_t& operator[](size_t i) { return data()[i]; }
-    const uint8_t& operator[](size_t i) const { return data()[i]; }
-    void clear() { resize_raw(0); }
-    void assign(size_t n, uint8_t v) {
-        resize_raw(n);
-        std::memset(data(), v, n);
-    }
-    template <class It, class = typename std::enable_if<!std::is_integral<It>::value>::type>
-    void assign(It b, It e) {
-        const size_t n = size_t(std::distance(b, e));
-        if (n > kInline) {  // b, e may point into this object's own storage
-            std::unique_ptr<uint8_t[]> h(new uint8_t[n]);
-            std::copy(b, e, h.get());
-            heap_ = std::move(h);
-            n_ = n;
-            return;
-        }
-        uint8_t tmp[kInline];
-        std::copy(b, e, tmp);
-        heap_.reset();
-        n_ = n;
-        std::memcpy(in_, tmp, n);
-    }
-    std::vector<uint8_t> vec() const { return std::vector<uint8_t>(begin(), end()); }
-    operator std::vector<uint8_t>() const { return vec(); }  // NOLINT
-    bool operator==(const Bytes& o) const { return n_ == o.n_ && std::equal(begin(), end(), o.begin()); }
-    bool operator!=(const Bytes& o) const { return !(*this == o); }
-
-   private:
-    void resize_raw(size_t n) {
-        if (n > kInline) heap_.reset(new uint8_t[n]);
-        else heap_.reset();
-        n_ = n;
-    }
-    size_t n_ = 0;
-    std::unique_ptr<uint8_t[]> heap_;
-    uint8_t in_[kInline];
-};
-
 struct MerkleNode {  // merklenode.go:15-19
-    Bytes Data;
+    std::vector<uint8_t> Data;
     MerkleNode* Left = nullptr;
     MerkleNode* Right = nullptr;
 
@@ -279,9 +200,9 @@ struct MerkleNode {  // merklenode.go:15-19
     uint64_t pend_idx = 0;
 
     MerkleNode() = default;
-    explicit MerkleNode(const std::vector<uint8_t>& d) : Data(d) {}
+    explicit MerkleNode(std::vector<uint8_t> d) : Data(std::move(d)) {}
 
-    const Bytes& Resolve() {
+    const std::vector<uint8_t>& Resolve() {
         if (pend) {
             Session::Default().ResolveBatch(*pend);
             Data.assign(pend->digests.begin() + 20 * pend_idx, pend->digests.begin() + 20 * pend_idx + 20);
@@ -490,7 +411,7 @@ class MerkleTree {  // merkletree.go:13-15
             std::vector<MerkleNode*> owners;
             for (MerkleNode* n : lv[d]) {
                 if (!n->Left) {
-                    val[n] = n->Resolve().vec();
+                    val[n] = n->Resolve();
                 } else {
                     std::vector<uint8_t> m = val[n->Left];
                     const auto& r = val[n->Right];
@@ -507,7 +428,7 @@ class MerkleTree {  // merkletree.go:13-15
         return val[root];
     }
 
-    std::vector<MerkleNode> nodes_;  // owns every node of the tree (reserved up front: stable addresses)
+    std::deque<MerkleNode> nodes_;  // owns every node of the tree (stable addresses)
     std::vector<uint8_t> levels_;
     uint64_t n_ = 0;  // leaves New built the tree from
     NewTiming timing_;
@@ -584,10 +505,6 @@ inline std::unique_ptr<MerkleTree> New(std::vector<MerkleNode> level, std::strin
     // materialize the pointer tree: copies of the given leaves (Go copies
     // `l := level[i]`), then parents level by level with the empty pad node
     auto& pool = t->nodes_;
-    const int lv = nkv_num_levels(n);
-    uint64_t pads = 0;  // one empty node per odd level below the top
-    for (int L = 0; L + 1 < lv; ++L) pads += nkv_level_count(n, L) & 1u;
-    pool.reserve(total + pads);  // no reallocation below: the pointers stay valid
     std::vector<MerkleNode*> below;
     below.reserve(n + 1);
     for (auto& x : level) {  // `level` is New's own copy: move out of it
@@ -596,6 +513,7 @@ inline std::unique_ptr<MerkleTree> New(std::vector<MerkleNode> level, std::strin
         below.push_back(&pool.back());
     }
     t->n_ = n;
+    const int lv = nkv_num_levels(n);
     for (int L = 1; L < lv; ++L) {
         if (below.size() % 2) {
             pool.emplace_back();  // MerkleNode{Data: []byte{}} (merkletree.go:32-34)
@@ -605,12 +523,11 @@ inline std::unique_ptr<MerkleTree> New(std::vector<MerkleNode> level, std::strin
         const uint64_t s = nkv_level_start(n, L), c = nkv_level_count(n, L);
         cur.reserve(c + 1);
         for (uint64_t i = 0; i < c; ++i) {
-            pool.emplace_back();
-            MerkleNode& m = pool.back();
-            m.Data.assign(nodes + 20 * (s + i), nodes + 20 * (s + i) + 20);
+            MerkleNode m(std::vector<uint8_t>(nodes + 20 * (s + i), nodes + 20 * (s + i) + 20));
             m.Left = below[2 * i];
             m.Right = below[2 * i + 1];
-            cur.push_back(&m);
+            pool.push_back(std::move(m));
+            cur.push_back(&pool.back());
         }
         below.swap(cur);
     }

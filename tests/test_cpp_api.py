@@ -29,8 +29,7 @@ def test_cpp_mirror_compiles(tmp_path):
 
 def test_arena_copy_in_cpu(tmp_path):
     """NewLeaf's arena copy (non-temporal stores from 256 bytes up) is exact for
-    every length and source alignment, and writes nothing past the value; the
-    inline-digest Data type copies, moves and assigns exactly."""
+    every length and source alignment, and writes nothing past the value."""
     from nakevaleng_amd import build as b
     so = b.build()
     libdir = os.path.dirname(so)
