@@ -378,7 +378,8 @@ int nkv_group_transport(const nkv_group *grp);
 int nkv_group_ctx(nkv_group *grp, int i, nkv_ctx **out);
 int nkv_group_sync(nkv_group *grp);
 /* d_roots[i]: 20 bytes on member i.  All-gather them: d_out[i] (nullable
- * array, or entries) receives the g * 20 bytes on member i; roots_out
+ * array, or entries) receives the g * 20 bytes on member i (a d_roots or d_out
+ * entry that is not device memory of member i's GPU: NKV_ERR_INVALID); roots_out
  * (nullable host buffer, g * 20 bytes) a copy (then the call synchronizes,
  * else it is asynchronous on the members' streams). */
 int nkv_group_roots_allgather(nkv_group *grp, const void *const *d_roots, void *const *d_out,

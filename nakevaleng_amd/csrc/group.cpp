@@ -397,7 +397,10 @@ int nkv_group_roots_allgather(nkv_group* grp, const void* const* d_roots, void* 
     const int g = grp->g;
     std::vector<void*> dst(g);
     for (int i = 0; i < g; ++i) {
-        if (!d_roots[i]) return NKV_ERR_INVALID;
+        // each member's buffers must live on its device (RCCL and the copies
+        // read and write them there)
+        if (!on_device(d_roots[i], grp->dev[i])) return NKV_ERR_INVALID;
+        if (d_out && d_out[i] && !on_device(d_out[i], grp->dev[i])) return NKV_ERR_INVALID;
         if (d_out && d_out[i]) {
             dst[i] = d_out[i];
         } else {

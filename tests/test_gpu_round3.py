@@ -175,6 +175,9 @@ def test_group_rccl_one_gpu(nkv, oracle):
         got = np.zeros(20, np.uint8)
         _lib.check(L.nkv_group_roots_allgather(grp.h, src, None, _lib.p8(got)))
         assert got.tobytes() == wants[0]
+        # a root in host memory is refused before RCCL sees it
+        bad = (ctypes.c_void_p * 1)(got.ctypes.data)
+        assert L.nkv_group_roots_allgather(grp.h, bad, None, _lib.p8(got)) == _lib.NKV_ERR_INVALID
         # one tree through the split entry (g = 1: member 0 holds every leaf)
         base, off, ln = ragged(5003, 11)
         nodes = np.zeros((L.nkv_total_nodes(5003), 20), np.uint8)
