@@ -1,10 +1,10 @@
 #!/bin/bash
-# Round 3: records_verify with the verify kernel's CRC tables in 4 interleaved
+# Round 3: records_verify with the verify kernel in 1024-thread workgroups and a 16-copy
 # copies (product) against one copy (tools/libnkvmerkle_base.so), same box,
 # after the verify parity tests.
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
-O=gpurun_out/r03p2
+O=gpurun_out/r03r
 mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests/test_gpu_verify.py tests/test_gpu_fuzz.py tests/test_gpu_round2.py tests/test_gpu_api.py -x -q --timeout 120 --timeout-method thread -m gpu > $O/tests.txt 2>&1 || { tail -30 $O/tests.txt; exit 1; }
 tail -1 $O/tests.txt
