@@ -39,6 +39,11 @@ SIMDS = 1024  # 256 CUs x 4
 VALU_CYCLES = 4.0
 VALU_PER_WAVE_BLOCK = {"leaf": 623.0, "records": 631.7, "verify": 737.9}
 SHA1_VALU_CEILING_GBS = 4100.0  # fallback without a clock reading: tools/sha1_rate.hip at 2.37 GHz
+# The mixed config's floor is its longest value: one lane's chain of dependent
+# compressions, on a wave that issues one instruction every ~4.65 cycles when
+# it runs alone on its SIMD -- 2,852 shader cycles per block for SHA-1 from
+# registers (tools/lone_wave.hip, profiles/r02_lone_wave_ilp.txt).
+LONE_WAVE_CYCLES_PER_BLOCK = 2852.0
 SEED = 0x6E616B65
 SEED_MIXED = 0x6E616B66
 
@@ -718,6 +723,14 @@ def main():
             "root": root,
             "cpu_baseline": cpu,
         }
+        if mixed and sclk:
+            # the leaf phase can end no sooner than its longest value's chain
+            longest = max(int((int(t["lens_h"].max()) + 9 + 63) // 64) for t in tabs)
+            floor_ms = longest * LONE_WAVE_CYCLES_PER_BLOCK / (sclk * 1e6) * 1e3
+            out["roofline"].update({"chain_floor_ms": round(floor_ms, 4),
+                                    "chain_floor_basis": f"longest value {longest} compressions x "
+                                                         f"{LONE_WAVE_CYCLES_PER_BLOCK:g} cycles at {sclk:.0f} MHz",
+                                    "chain_frac": round(floor_ms / leaf_ms, 4)})
         if verified is not None:
             out["verified_vs_oracle"] = verified
         if gathered_ok is not None:
