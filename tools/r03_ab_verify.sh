@@ -4,7 +4,7 @@
 # after the verify parity tests.
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
-O=gpurun_out/r03r
+O=gpurun_out/r03v
 mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests/test_gpu_verify.py tests/test_gpu_fuzz.py tests/test_gpu_round2.py tests/test_gpu_api.py -x -q --timeout 120 --timeout-method thread -m gpu > $O/tests.txt 2>&1 || { tail -30 $O/tests.txt; exit 1; }
 tail -1 $O/tests.txt
