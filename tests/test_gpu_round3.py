@@ -236,6 +236,51 @@ def test_group_split_tree_copy_transport(nkv, oracle, g, n):
             assert L.nkv_group_tree_dev(grp.h, (_lib.NkvTable * g)(*bad), n, None, None) == _lib.NKV_ERR_INVALID
 
 
+def values_parts(_lib, g, n, base, off, ln):
+    """Member r's ragged leaf range as a VALUES table: its values' bytes, offsets
+    rebased to them, lengths (device tensors)."""
+    span = _lib.lib().nkv_split_span(n, g)
+    parts, keep = [], []
+    for r in range(g):
+        lo, hi = min(n, r * span), min(n, (r + 1) * span)
+        if hi > lo:
+            b0 = int(off[lo])
+            b1 = int(off[hi - 1] + ln[hi - 1])
+            db = dev(np.concatenate([base[b0:b1], np.zeros(1, np.uint8)]))
+            do, dl = dev((off[lo:hi] - b0).view(np.int64)), dev(ln[lo:hi].view(np.int64))
+            keep += [db, do, dl]
+            parts.append(_lib.table(_lib.NKV_TABLE_VALUES, 0, hi - lo, base=db.data_ptr(), off=do.data_ptr(),
+                                    lens=dl.data_ptr()))
+        else:
+            parts.append(_lib.table(_lib.NKV_TABLE_VALUES, 0, 0))
+    return parts, keep
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_group_split_fuzz_values(nkv, oracle, seed):
+    """Seeded fuzz of the split: n log-uniform in [1, 2^18], g in 1..8 (device 0
+    repeated: copy transport; g = 1 also), ragged unaligned values 0-299 bytes;
+    root, every level and the image against the oracle."""
+    _lib, _ = nkv
+    L = _lib.lib()
+    rng = np.random.default_rng(1000 + seed)
+    n = int(np.exp(rng.uniform(0, np.log(1 << 18))))
+    n = max(1, n)
+    g = int(rng.integers(1, 9))
+    base, off, ln = ragged(n, 2000 + seed)
+    want = want_tree(oracle, base, off, ln)
+    with _lib.Group([0] * g) as grp:
+        parts, keep = values_parts(_lib, g, n, base, off, ln)
+        root = np.zeros(20, np.uint8)
+        _lib.check(L.nkv_group_tree_dev(grp.h, (_lib.NkvTable * g)(*parts), n, None, _lib.p8(root)))
+        assert root.tobytes() == want[-1].tobytes(), (n, g)
+        nodes = np.zeros((L.nkv_total_nodes(n), 20), np.uint8)
+        img = np.zeros(L.nkv_bfs_size(n), np.uint8)
+        _lib.check(L.nkv_group_tree_fetch(grp.h, _lib.p8(nodes), _lib.p8(img)))
+        assert np.array_equal(nodes, want), (n, g)
+        assert img.tobytes() == oracle.bfs_image(want, n), (n, g)
+
+
 @pytest.mark.parametrize("g", [2, 4])
 def test_group_host_forms_copy_transport(nkv, oracle, g):
     """nkv_group_tree_from_values (one tree, one host thread per member) and
