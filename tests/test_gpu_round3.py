@@ -124,6 +124,28 @@ def test_trees_dev_every_kind(nkv, oracle, lanes):
         ctx.set_option(_lib.NKV_OPT_TABLE_LANES, 2)
 
 
+def test_trees_dev_bad_table_then_recovers(nkv, oracle):
+    """A table the call refuses (unknown kind, empty table) among good ones
+    returns an error with every lane joined; the context's next call is right."""
+    _lib, ctx = nkv
+    L = _lib.lib()
+    tabs = make_tables(_lib, L, oracle)
+    ctx.set_option(_lib.NKV_OPT_TABLE_LANES, 3)
+    try:
+        for bad in (_lib.table(99, tabs[0][2].data_ptr(), 5), _lib.table(_lib.NKV_TABLE_STRIDED, 0, 0)):
+            with pytest.raises(_lib.NkvError):
+                ctx.trees([tabs[0][0], bad, tabs[1][0]])
+            ctx.sync()
+        for t in tabs:
+            t[2].zero_()
+        ctx.trees([t[0] for t in tabs])
+        ctx.sync()
+        for t, want, nb, keep in tabs:
+            assert np.array_equal(host_nodes(nb), want), t.kind
+    finally:
+        ctx.set_option(_lib.NKV_OPT_TABLE_LANES, 2)
+
+
 def test_trees_dev_records_err_null(nkv, oracle):
     """RECORDS tables without an err word: the call reports a header outside the
     stream as NKV_ERR_INVALID (after a sync), as nkv_tree_from_records_dev does."""
