@@ -21,11 +21,13 @@
 // ds_read's immediate offset.  128 KiB of tables: one 1024-thread workgroup
 // per CU (4 waves per SIMD), persistent over the spans.
 //
-// Per span: 0-3 head bytes (byte steps) up to the first 4-aligned address,
-// then whole aligned words from whole aligned 128-byte lines (eight
-// global_load_dwordx4 per lane per line, the next line loaded while this one
-// is checksummed; a line holding a span byte lies in that byte's page), then
-// 0-3 tail bytes.  Only a span's first and last line mask words.
+// Per span: 0-3 head bytes (byte steps from the aligned word that holds them)
+// up to the first 4-aligned address, then whole aligned words from whole
+// aligned 128-byte lines (eight global_load_dwordx4 per lane per line, the
+// next line loaded while this one is checksummed; a line holding a span byte
+// lies in that byte's page), then 0-3 tail bytes (from one aligned word).
+// Only a span's first and last line mask words.  The records form loads a
+// record's header, head word and first line together (crc_span_lines).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
