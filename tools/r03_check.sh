@@ -4,7 +4,7 @@
 # the rocprofv3 summary of the default bench.
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
-O=gpurun_out/r03q
+O=gpurun_out/r03y
 mkdir -p $O
 timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
 echo smoke ok
