@@ -909,7 +909,7 @@ def main_capi(args, T):
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u32",
-        "data": f"synthetic: splitmix64 bytes generated in each GPU's HBM",
+        "data": "synthetic: splitmix64 bytes generated in each GPU's HBM",
         "backend": f"capi group: one process, {N} context(s), transport "
                    + ("RCCL" if grp.transport == _lib.NKV_TRANSPORT_RCCL else "copy"),
         "config": {
