@@ -357,6 +357,28 @@ def test_group_trees_dev_copy_transport_roots_in_table_order(nkv, oracle):
         assert L.nkv_group_trees_dev(grp.h, (_lib.NkvTable * k)(*bad), k, None) == _lib.NKV_ERR_INVALID
 
 
+def test_group_roots_allgather_copy_transport(nkv):
+    """The bare all-gather over the copy transport (device 0 listed 3 times):
+    every member's 20 bytes land on every member in member order, through the
+    caller's output buffers and through the group's own."""
+    _lib, _ = nkv
+    L = _lib.lib()
+    g = 3
+    with _lib.Group([0] * g) as grp:
+        src = [torch.arange(20 * r, 20 * r + 20, dtype=torch.uint8, device="cuda") for r in range(g)]
+        outs = [torch.zeros(20 * g, dtype=torch.uint8, device="cuda") for _ in range(g)]
+        want = b"".join(x.cpu().numpy().tobytes() for x in src)
+        got = np.zeros(20 * g, np.uint8)
+        _lib.check(L.nkv_group_roots_allgather(grp.h, (ctypes.c_void_p * g)(*[x.data_ptr() for x in src]),
+                                               (ctypes.c_void_p * g)(*[o.data_ptr() for o in outs]), _lib.p8(got)))
+        assert got.tobytes() == want
+        assert all(o.cpu().numpy().tobytes() == want for o in outs)
+        got[:] = 0
+        _lib.check(L.nkv_group_roots_allgather(grp.h, (ctypes.c_void_p * g)(*[x.data_ptr() for x in src]), None,
+                                               _lib.p8(got)))
+        assert got.tobytes() == want
+
+
 def test_stream_handover_orders_records_calls(nkv, oracle):
     """an asynchronous verify call on stream A, the next on
     stream B at once; the pass flags one call leaves for the next stay ordered."""
