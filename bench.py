@@ -15,6 +15,7 @@ Rank 0 prints one JSON line (see DESIGN.md "Measurement").
 from __future__ import annotations
 
 import argparse
+import ctypes
 import hashlib
 import json
 import os
@@ -65,7 +66,62 @@ def mixed_lengths(target_bytes: int, seed: int):
     return lens, off
 
 
-def parse():
+GOLDEN = os.path.join(ROOT, "tests", "golden", "bench_roots.json")
+_golden = None
+
+
+def golden():
+    """The committed expected roots of the bench's synthetic tables
+    (tests/golden/make_bench_roots.py, the C oracle in the build container)."""
+    global _golden
+    if _golden is None:
+        with open(GOLDEN) as f:
+            _golden = json.load(f)
+    return _golden
+
+
+def expected_roots(config, leaves, value_bytes, rank, T):
+    """Rank `rank`'s T table roots (hex) from the committed fixture, or None when
+    the fixture does not cover this shape (then only --verify checks)."""
+    if config not in ("sstable4k", "runs4"):
+        return None
+    for key in ("sstable4k", "small"):  # the metric's shape; configs[0]'s size (CPU tests)
+        g = golden()[key]
+        if (leaves, value_bytes) == (g["leaves"], g["value_bytes"]):
+            roots = g["roots"].get(str(rank))
+            roots = [roots] if isinstance(roots, str) else roots
+            return roots[:T] if roots is not None and T <= len(roots) else None
+    return None
+
+
+def expected_one_tree(leaves, value_bytes, world):
+    """The root of one tree over ranks 0..world-1's leaves, or None."""
+    g = golden()["one_tree"]
+    if (leaves, value_bytes) != (g["leaves_per_rank"], g["value_bytes"]):
+        return None
+    return g["roots"].get(str(world))
+
+
+def verdict(codes):
+    """Per-rank check codes (1 ok, 0 wrong, -1 not covered) -> verified_vs_oracle:
+    False if any rank is wrong, True if every rank checked out, else None."""
+    if any(c == 0 for c in codes):
+        return False
+    return True if codes and all(c == 1 for c in codes) else None
+
+
+def rank_codes(dist, world, rank, code, device):
+    """Every rank's check code on every rank (one SUM all-reduce of a one-hot
+    vector; `device` is where the backend wants its tensors)."""
+    import torch
+    flags = torch.zeros(world, dtype=torch.int32, device=device)
+    flags[rank] = int(code) + 2  # 1 (not covered), 2 (wrong), 3 (ok): never 0
+    if dist is not None and world > 1:
+        dist.all_reduce(flags)
+    return [int(v) - 2 for v in flags.cpu().tolist()]
+
+
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
@@ -116,7 +172,11 @@ def parse():
                          "per table, pipelined behind the next table (step)")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="do not record per-kernel HIP events inside the timed loop")
-    return ap.parse_args()
+    ap.add_argument("--no-capi", action="store_true",
+                    help="no capi_group / capi_one_tree sub-records (by default rank 0 runs the one-process C-ABI "
+                         "group over the same N GPUs in a fresh child process once the ranks are done)")
+    ap.add_argument("--capi-timeout", type=int, default=600, help="seconds per C-ABI group child")
+    return ap.parse_args(argv)
 
 
 def cpu_baseline(n_leaves: int, vlen: int) -> dict:
@@ -499,6 +559,74 @@ def main():
     rc = ensure_ranks(args, sys.argv[1:])
     if rc is not None:
         sys.exit(rc)
+    out = run_ranks(args, T)
+    if out is None:  # not rank 0: done
+        return
+    import gc
+    import torch
+    gc.collect()  # the tables and their closures hold this run's device buffers
+    torch.cuda.empty_cache()
+    # Rank 0, every rank's GPU state released: the one-process C-ABI group over
+    # the same N GPUs (SURVEY 8e's process model, what the Go drop-in would use;
+    # VERDICT r03 item 1), each in a fresh child process, then the CPU baseline.
+    world = out["n_gpus"]
+    if not args.no_capi and args.config in ("sstable4k", "runs4"):
+        out["capi_group"] = capi_child(args, world, [], args.capi_timeout)
+        if args.config == "sstable4k":
+            out["capi_one_tree"] = capi_child(args, world, ["--config", "one_tree", "--tables", "1"],
+                                              args.capi_timeout)
+    if not args.no_cpu_baseline and args.config in ("sstable4k", "runs4"):
+        # at every N, on rank 0 once the ranks are done (the Go reference is
+        # one process on the same host)
+        out["cpu_baseline"] = cpu_baseline(min(args.cpu_sample_leaves, args.leaves), args.value_bytes)
+    print(json.dumps(out), flush=True)
+
+
+CHILD_ENV_DROP = ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE",
+                  "ROLE_RANK", "ROLE_WORLD_SIZE", "ROLE_NAME", "MASTER_ADDR", "MASTER_PORT",
+                  "TORCHELASTIC_RESTART_COUNT", "TORCHELASTIC_MAX_RESTARTS", "TORCHELASTIC_RUN_ID",
+                  "TORCHELASTIC_USE_AGENT_STORE", "TORCH_NCCL_ASYNC_ERROR_HANDLING", "TORCHELASTIC_ERROR_FILE")
+CAPI_KEYS = ("value", "unit", "n_gpus", "steps", "ms_per_step", "backend", "sclk_mhz", "root_gather_ok",
+             "verified_vs_oracle", "verified_members", "members_agree", "root", "kernel_ms")
+
+
+def capi_cmd(args, world, extra):
+    """The C-ABI group child's command line: this run's flags with the group
+    backend over `world` GPUs (later flags win in argparse)."""
+    argv = [a for a in sys.argv[1:]]
+    return [sys.executable, os.path.abspath(__file__)] + argv + ["--backend", "capi", "--gpus", str(world),
+                                                                  "--no-cpu-baseline"] + list(extra)
+
+
+def capi_child(args, world, extra, timeout, run=None):
+    """Run the one-process group bench (main_capi) in a fresh child, outside
+    any launcher's process group, and return the keys of its JSON line that go
+    into the parent's line (or {"error": ...}: a failed child never fails the
+    bench)."""
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in CHILD_ENV_DROP}
+    env["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    cmd = capi_cmd(args, world, extra)
+    t0 = time.perf_counter()
+    try:
+        p = (run or subprocess.run)(cmd, stdout=subprocess.PIPE, text=True, timeout=timeout, env=env)
+    except subprocess.TimeoutExpired:
+        return {"error": f"timed out after {timeout} s", "cmd": " ".join(cmd[1:])}
+    lines = [x for x in (p.stdout or "").splitlines() if x.startswith("{")]
+    if p.returncode != 0 or not lines:
+        return {"error": f"exit status {p.returncode}", "cmd": " ".join(cmd[1:])}
+    d = json.loads(lines[-1])
+    sub = {k: d[k] for k in CAPI_KEYS if k in d}
+    sub["parallelism"] = d.get("config", {}).get("parallelism")
+    sub["roofline_frac"] = d.get("roofline", {}).get("frac")
+    sub["wall_s"] = round(time.perf_counter() - t0, 1)
+    return sub
+
+
+def run_ranks(args, T):
+    """This rank's measurement (one process per GPU); returns the JSON line's
+    dict on rank 0, None on the others.  Every GPU tensor of the run is
+    released before it returns."""
     import torch
     import torch.distributed as dist
 
@@ -643,8 +771,20 @@ def main():
     torch.cuda.synchronize()
     bfs_ms = e0.elapsed_time(e1) / 5
 
-    verified = None
-    if args.verify and rank == 0:
+    # every rank's roots against the committed oracle roots (no flag needed;
+    # VERDICT r03 item 1): one code per rank, gathered to all ranks
+    if one_tree:
+        want1 = expected_one_tree(n, vlen, world) if rank == 0 else None
+        code = -1 if want1 is None else int(root == want1)
+    else:
+        want = expected_roots(args.config, n, vlen, rank, T)
+        mine = [t["nodes"][-20:].cpu().numpy().tobytes().hex() for t in tabs]
+        code = -1 if want is None else int(mine == want)
+    codes = rank_codes(dist if use_dist else None, world, rank, code, "cuda")
+    if one_tree:
+        codes = codes[:1]  # the root is rank 0's
+    verified = verdict(codes)
+    if args.verify and rank == 0 and verified is None:
         import numpy as np
         from oracle import oracle_c as oc
         if records:
@@ -659,10 +799,7 @@ def main():
         else:
             verified = all(t["want"]() == t["nodes"][-20:].cpu().numpy().tobytes().hex() for t in tabs)
 
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config in ("sstable4k", "runs4"):
-        cpu = cpu_baseline(min(args.cpu_sample_leaves, n), vlen)
-
+    out = None
     if rank == 0:
         total_bytes = nbytes * world * args.steps
         value = total_bytes / elapsed / 2**30
@@ -721,7 +858,7 @@ def main():
                           "bfs_image": round(bfs_ms, 4)},
             "clock_probe_waves": clock_waves,
             "root": root,
-            "cpu_baseline": cpu,
+            "cpu_baseline": None,
         }
         if mixed and sclk:
             # the leaf phase can end no sooner than its longest value's chain
@@ -731,15 +868,21 @@ def main():
                                     "chain_floor_basis": f"longest value {longest} compressions x "
                                                          f"{LONE_WAVE_CYCLES_PER_BLOCK:g} cycles at {sclk:.0f} MHz",
                                     "chain_frac": round(floor_ms / leaf_ms, 4)})
-        if verified is not None:
-            out["verified_vs_oracle"] = verified
+        out["verified_vs_oracle"] = verified
+        out["verified_ranks"] = [None if c < 0 else bool(c) for c in codes]
+        out["verified_basis"] = ("tests/golden/bench_roots.json (C oracle roots of the same seeds, committed)"
+                                 if all(c >= 0 for c in codes) else
+                                 "the C oracle at run time (--verify)" if verified is not None else None)
         if gathered_ok is not None:
             out["root_gather_ok"] = gathered_ok
-        print(json.dumps(out), flush=True)
+    # the ranks leave together; the caller releases this run's tensors (they
+    # live in this frame and in the tables' closures) before any group child
     ctx.close()
+    torch.cuda.synchronize()
     if use_dist:
         dist.barrier()
         dist.destroy_process_group()
+    return out
 
 
 def main_api_flush(args):
@@ -844,10 +987,11 @@ def main_capi(args, T):
         if n & (n - 1):
             raise SystemExit("--config one_tree needs a power-of-two --leaves (ranges aligned to 2^k)")
         parts = (_lib.NkvTable * N)(*[per[m][0]["table"] for m in range(N)])
-        d_root = torch.zeros(20, dtype=torch.uint8, device="cuda:0")
+        d_root = [torch.zeros(20, dtype=torch.uint8, device=f"cuda:{m}") for m in range(N)]
+        droots = (ctypes.c_void_p * N)(*[d.data_ptr() for d in d_root])
 
         def step():
-            _lib.check(L.nkv_group_tree_dev(grp.h, parts, n * N, d_root.data_ptr(), None), "nkv_group_tree_dev")
+            _lib.check(L.nkv_group_tree_dev(grp.h, parts, n * N, droots, None), "nkv_group_tree_dev")
     else:
         order = [per[t % N][t // N] for t in range(N * T)]  # table t on member t % N
         arr = (_lib.NkvTable * (N * T))(*[t["table"] for t in order])
@@ -873,18 +1017,29 @@ def main_capi(args, T):
     sclk, clock_waves = ctxs[0].clock() if not args.no_clock else (None, 0)
     calls, leaf_ms_tot, _ = ctxs[0].timing_summary()
     ctxs[0].set_timing(False)
-    # the gathered roots of the last step, checked against each table's own nodes
+    # the gathered roots of the last step, checked against each table's own
+    # nodes; every member's roots against the committed oracle roots
+    members_agree = None
     if one_tree:
-        root = d_root.cpu().numpy().tobytes().hex()
+        got = [d.cpu().numpy().tobytes().hex() for d in d_root]  # every member reduced the top
+        root = got[0]
+        members_agree = all(r == root for r in got)
         gathered_ok = None
+        want1 = expected_one_tree(n, vlen, N)
+        codes = [-1 if want1 is None else int(r == want1) for r in got]
     else:
         roots = np.zeros(20 * N * T, np.uint8)
         _lib.check(L.nkv_group_trees_dev(grp.h, arr, N * T, _lib.p8(roots)))
         gathered_ok = all(roots[20 * t:20 * t + 20].tobytes() == order[t]["nodes"][-20:].cpu().numpy().tobytes()
                           for t in range(N * T))
         root = per[0][0]["nodes"][-20:].cpu().numpy().tobytes().hex()
-    verified = None
-    if args.verify:
+        codes = []
+        for m in range(N):
+            want = expected_roots(args.config, n, vlen, m, T)
+            mine = [t["nodes"][-20:].cpu().numpy().tobytes().hex() for t in per[m]]
+            codes.append(-1 if want is None else int(mine == want))
+    verified = verdict(codes)
+    if args.verify and verified is None:
         if one_tree:
             from oracle import oracle_c as oc
             host = np.concatenate([oc.splitmix64_bytes(n * vlen, SEED + r) for r in range(N)])
@@ -939,8 +1094,10 @@ def main_capi(args, T):
     }
     if gathered_ok is not None:
         out["root_gather_ok"] = gathered_ok
-    if verified is not None:
-        out["verified_vs_oracle"] = verified
+    if members_agree is not None:
+        out["members_agree"] = members_agree
+    out["verified_vs_oracle"] = verified
+    out["verified_members"] = [None if c < 0 else bool(c) for c in codes]
     print(json.dumps(out), flush=True)
     grp.close()
 

@@ -107,8 +107,6 @@ int nkv_ctx_sync(nkv_ctx *ctx);
                                counts of a batch of >= 4096 values lie within max(1, min/16)
                                of each other, else sorted (decided on the device, no
                                read-back) */
-#define NKV_OPT_DEEP_PREFETCH 3 /* kept for ABI stability: 3 (the work-queue kernel) is the
-                                   only value accepted */
 #define NKV_OPT_QUEUE_SPLIT 4 /* work-queue kernel: groups whose longest value has at most
                                  this many 64-B blocks may go to the non-priority waves
                                  when the longest value bounds the batch (default 32) */
@@ -129,8 +127,6 @@ int nkv_ctx_sync(nkv_ctx *ctx);
                                   staged), then set them in LDS, one workgroup per range; 1 = the
                                   same grouping by a global counting sort (hashes twice); 0 = one
                                   device atomicOr per bit */
-#define NKV_OPT_QUEUE_RING 9   /* kept for ABI stability: 13 (the pipelined 3-slot ring of
-                                  value-relative chunks) is the only value accepted */
 #define NKV_OPT_RECORDS_FUSED 11 /* records form (nkv_tree_from_records*): 1 (default) = one
                                     launch locates each value from its header and hashes it
                                     (k_leaf_records); 0 = a separate locate pass first */
@@ -408,19 +404,25 @@ int nkv_group_trees_from_values(nkv_group *grp, const nkv_values *tables, int k)
  * at 2^k-aligned leaf ranges: member r builds levels 0..k of leaves
  * [r * span, min(n, (r + 1) * span)), span = nkv_split_span(n, g) = 2^k, k =
  * max(1, ceil(log2(ceil(n / g)))); a partial last range re-hashes its lone top node
- * up to level k; the level-k nodes are all-gathered and the top levels reduced on
- * every member.  Outputs as nkv_tree_from_values (each nullable; all host). */
+ * up to level k; the level-k nodes are all-gathered and every member reduces the
+ * top ceil(log2 G) levels (G = ceil(n / span) ranges), so every member holds the
+ * root.  Outputs as nkv_tree_from_values (each nullable; all host). */
 uint64_t nkv_split_span(uint64_t n, int g);
 int nkv_group_tree_from_values(nkv_group *grp, const uint8_t *base, const uint64_t *off, const uint64_t *len,
                                uint64_t n, uint8_t *root20, uint8_t *nodes_out, uint8_t *img_out);
 /* The same over device-resident ranges: parts[r] describes member r's leaf range
- * (a STRIDED or VALUES table on member r's device, n = its range's length, 0 for
- * members past the last range; nodes ignored: the group keeps the levels).
- * d_root (nullable): 20 bytes on member 0 that receive the root; root20 (host,
- * nullable): then the call synchronizes, else it is asynchronous.
+ * (a STRIDED or VALUES table whose pointers live on member r's device, n = its
+ * range's length, 0 for members past the last range; nodes ignored: the group
+ * keeps the levels).  d_roots (nullable array of g entries, each nullable):
+ * d_roots[r] is 20 bytes on member r's device that receive the root member r
+ * reduced (every member's equals the root); root20 (host, nullable): then the
+ * call synchronizes, else it is asynchronous on the members' streams.
  * nkv_group_tree_fetch then copies the latest such tree's nodes (level-major,
- * nkv_total_nodes(n) * 20 bytes) and/or its Serialize image to the host. */
-int nkv_group_tree_dev(nkv_group *grp, const nkv_table *parts, uint64_t n, void *d_root, uint8_t *root20);
+ * nkv_total_nodes(n) * 20 bytes) and/or its Serialize image to the host; after a
+ * refused or failed split call there is no latest tree and it returns
+ * NKV_ERR_INVALID. */
+int nkv_group_tree_dev(nkv_group *grp, const nkv_table *parts, uint64_t n, void *const *d_roots,
+                       uint8_t *root20);
 int nkv_group_tree_fetch(nkv_group *grp, uint8_t *nodes_out, uint8_t *img_out);
 
 #ifdef __cplusplus

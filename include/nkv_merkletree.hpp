@@ -7,9 +7,13 @@
 //
 //   MerkleNode, MERKLE_NODE_EMPTY   ds/merkletree/merklenode.go:11-19
 //   MerkleNode::String              merklenode.go:22-24
-//   NewLeaf                         merklenode.go:27-34  -- deferred: the value is copied
-//                                   into a pinned arena and hashed on the GPU by New()
-//                                   (or on first Resolve()), batched with its neighbours
+//   NewLeaf                         merklenode.go:27-34  -- deferred: the value's copy into
+//                                   a pinned arena is handed to a pool of copy threads
+//                                   and the value is hashed on the GPU by New() (or on
+//                                   first Resolve()), batched with its neighbours.
+//                                   Contract: a value handed to NewLeaf must not change
+//                                   until New returns (both callers, sstable.go:61-63 and
+//                                   lsmtree.go:211, pass values they never mutate)
 //   MerkleNode::Serialize           merklenode.go:37-63
 //   MerkleNode::Deserialize         merklenode.go:67-96  (returns true at EOF)
 //   MerkleTree, New                 merkletree.go:13-25  ("cannot build Merkle Tree from 0 nodes")
@@ -23,14 +27,18 @@
 // no CPU hashing path: without a HIP device every hashing call throws.
 #pragma once
 
+#include <algorithm>
 #include <array>
+#include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
 #include <deque>
 #include <exception>
 #include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -52,16 +60,114 @@ inline void check(int rc, const char* what) {
     if (rc != NKV_OK) throw std::runtime_error(std::string(what) + ": " + nkv_strerror(rc));
 }
 
+// NewLeaf's arena copies off the caller's thread: the
+// caller only records (arena place, value pointer, length); a pool of threads
+// copies whole jobs of consecutive places.  settled() is the arena prefix whose
+// copies have all finished (jobs finish out of order), which the caller streams
+// to the device (nkv_host_stream) while the NewLeaf loop goes on.
+class CopyPool {
+   public:
+    struct Task {
+        uint64_t at;
+        const uint8_t* src;
+        size_t n;
+    };
+    struct Job {
+        uint8_t* base = nullptr;  // the arena the places are in
+        uint64_t end = 0;         // arena bytes [0, end) are covered once this job is done
+        std::vector<Task> tasks;
+        std::atomic<bool> done{false};
+    };
+    using CopyFn = void (*)(uint8_t*, const uint8_t*, size_t);
+
+    explicit CopyPool(int threads, CopyFn copy) : copy_(copy) {
+        for (int i = 0; i < threads; ++i) th_.emplace_back([this] { Work(); });
+    }
+    ~CopyPool() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    CopyPool(const CopyPool&) = delete;
+    CopyPool& operator=(const CopyPool&) = delete;
+    int threads() const { return int(th_.size()); }
+
+    void Submit(std::unique_ptr<Job> j) {
+        Job* raw = j.get();
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            jobs_.push_back(std::move(j));
+            queue_.push_back(raw);
+        }
+        cv_.notify_one();
+    }
+    // the arena prefix whose copies are all done (caller thread only)
+    uint64_t Settled() {
+        std::lock_guard<std::mutex> g(mu_);
+        while (!jobs_.empty() && jobs_.front()->done.load(std::memory_order_acquire)) {
+            settled_ = jobs_.front()->end;
+            jobs_.pop_front();
+        }
+        return settled_;
+    }
+    // wait for every submitted job (their stores are fenced by the workers)
+    void Drain() {
+        std::unique_lock<std::mutex> g(mu_);
+        idle_.wait(g, [this] { return queue_.empty() && busy_ == 0; });
+        while (!jobs_.empty()) {
+            settled_ = jobs_.front()->end;
+            jobs_.pop_front();
+        }
+    }
+    // a new batch starts at arena byte 0
+    void Reset() {
+        Drain();
+        settled_ = 0;
+    }
+
+   private:
+    void Work() {
+        std::unique_lock<std::mutex> g(mu_);
+        while (true) {
+            cv_.wait(g, [this] { return stop_ || !queue_.empty(); });
+            if (queue_.empty()) return;  // stop_
+            Job* j = queue_.front();
+            queue_.pop_front();
+            ++busy_;
+            g.unlock();
+            for (const Task& t : j->tasks) copy_(j->base + t.at, t.src, t.n);
+#if defined(__SSE2__)
+            _mm_sfence();  // this thread's non-temporal stores, before done is seen
+#endif
+            j->done.store(true, std::memory_order_release);
+            g.lock();
+            if (--busy_ == 0 && queue_.empty()) idle_.notify_all();
+        }
+    }
+
+    CopyFn copy_;
+    std::vector<std::thread> th_;
+    std::mutex mu_;
+    std::condition_variable cv_, idle_;
+    std::deque<std::unique_ptr<Job>> jobs_;  // submitted, in arena order, not yet settled
+    std::deque<Job*> queue_;                 // not yet taken by a worker
+    int busy_ = 0;
+    bool stop_ = false;
+    uint64_t settled_ = 0;
+};
+
+struct MerkleNode;
+
 // One device context + the pinned arena that deferred NewLeaf values go to.
 class Session {
    public:
     explicit Session(int device = 0) {
         check(nkv_ctx_create(device, &ctx_), "nkv_ctx_create");
     }
-    ~Session() {
-        if (arena_) nkv_host_free(ctx_, arena_);
-        nkv_ctx_destroy(ctx_);
-    }
+    ~Session();  // below MerkleNode (it frees the recycled node storage)
     Session(const Session&) = delete;
     Session& operator=(const Session&) = delete;
 
@@ -81,13 +187,16 @@ class Session {
         bool resolved = false;
     };
 
-    // Copies `data` into the arena at a 16-byte aligned place (the leaf
-    // kernel's aligned path reads the values where they lie: the library
-    // copies the arena to the device in one DMA, nkv_merkle.h); returns
-    // (batch, index).  Every settled kStreamChunk of the arena starts its
-    // device copy at once (nkv_host_stream), so the copy overlaps the rest of
-    // the NewLeaf loop.
+    // Places `data` in the arena at a 16-byte aligned place (the leaf kernel's
+    // aligned path reads the values where they lie: the library copies the
+    // arena to the device in one DMA, nkv_merkle.h); returns (batch, index).
+    // With copy threads (default) the copy itself is queued for the pool in
+    // jobs of kJobBytes and `data` must stay unchanged until New returns;
+    // with 0 threads it is copied here.  Every settled kStreamChunk of the
+    // arena starts its device copy at once (nkv_host_stream), so the copy
+    // overlaps the rest of the NewLeaf loop.
     static constexpr uint64_t kStreamChunk = uint64_t(32) << 20;
+    static constexpr uint64_t kJobBytes = uint64_t(2) << 20;
     // Values of at least kStreamCopy bytes go to the arena with non-temporal
     // stores: the arena is written once and then read by the DMA engine, so
     // pulling its lines into the cache first (the read-for-ownership of a
@@ -98,28 +207,68 @@ class Session {
         if (!batch_ || batch_->resolved) {
             batch_ = std::make_shared<Batch>();
             batch_->epoch = ++epoch_;
+            Settle();
             used_ = 0;
             streamed_ = 0;
+            if (pool_) pool_->Reset();
         }
         const uint64_t at = (used_ + 15) & ~uint64_t(15);
         Reserve(at + n);
-        if (nt_) CopyIn(static_cast<uint8_t*>(arena_) + at, data, n);
-        else if (n) std::memcpy(static_cast<uint8_t*>(arena_) + at, data, n);
         batch_->off.push_back(at);
         batch_->len.push_back(n);
         used_ = at + n;
-        if (stream_ && used_ >= streamed_ + kStreamChunk) {
-            streamed_ = used_ - used_ % kStreamChunk;
-            Fence();
-            check(nkv_host_stream(ctx_, arena_, streamed_), "nkv_host_stream");
+        if (Pool()) {
+            if (!job_) {
+                job_.reset(new CopyPool::Job());
+                job_->base = static_cast<uint8_t*>(arena_);
+            }
+            if (n) job_->tasks.push_back({at, data, n});
+            job_bytes_ += n;
+            if (job_bytes_ >= kJobBytes) {
+                SubmitJob();
+                if (stream_) {  // checked once per job, not per value
+                    const uint64_t s = pool_->Settled();
+                    if (s >= streamed_ + kStreamChunk) {
+                        streamed_ = s - s % kStreamChunk;
+                        check(nkv_host_stream(ctx_, arena_, streamed_), "nkv_host_stream");
+                    }
+                }
+            }
+        } else {
+            if (nt_) CopyIn(static_cast<uint8_t*>(arena_) + at, data, n);
+            else if (n) std::memcpy(static_cast<uint8_t*>(arena_) + at, data, n);
+            if (stream_ && used_ >= streamed_ + kStreamChunk) {
+                streamed_ = used_ - used_ % kStreamChunk;
+                Fence();
+                check(nkv_host_stream(ctx_, arena_, streamed_), "nkv_host_stream");
+            }
         }
         return {batch_, batch_->off.size() - 1};
     }
+    // Every queued arena copy done (New and every other reader of the arena
+    // call this first).
+    void Settle() {
+        if (!pool_) return;
+        SubmitJob();
+        pool_->Drain();
+    }
+    // NewLeaf's copy threads: 0 = copy on the caller's thread; default
+    // min(16, cores), or the NKV_COPY_THREADS environment variable
+    void SetCopyThreads(int k) {
+        Settle();
+        pool_.reset();
+        copy_threads_ = std::max(0, k);
+        if (copy_threads_) pool_.reset(new CopyPool(copy_threads_, nt_ ? &CopyIn : &PlainCopy));
+    }
+    int CopyThreads() { return Pool() ? pool_->threads() : 0; }
     // NewLeaf streams settled arena chunks ahead of New (default on)
     void SetStreaming(bool on) { stream_ = on; }
     // NewLeaf copies values of kStreamCopy bytes or more with non-temporal
     // stores (default on; off: memcpy)
-    void SetNonTemporal(bool on) { nt_ = on; }
+    void SetNonTemporal(bool on) {
+        nt_ = on;
+        if (pool_) SetCopyThreads(pool_->threads());
+    }
 
     const uint8_t* arena() const { return static_cast<const uint8_t*>(arena_); }
     // nkv_host_alloc calls so far: a sealed batch's arena is reused by the next
@@ -130,6 +279,7 @@ class Session {
         if (b.resolved) return;
         const uint64_t n = b.off.size();
         b.digests.assign(20 * n, 0);
+        Settle();
         Fence();
         check(nkv_leaf_hash(ctx_, arena(), b.off.data(), b.len.data(), n, b.digests.data()), "NewLeaf");
         b.resolved = true;
@@ -164,10 +314,35 @@ class Session {
 #endif
         if (n) std::memcpy(dst, src, n);
     }
+    static void PlainCopy(uint8_t* dst, const uint8_t* src, size_t n) {
+        if (n) std::memcpy(dst, src, n);
+    }
+
+    // New's pointer tree reuses the node storage of trees already destroyed
+    // (no per-node allocation once a flush of that size has run)
+    std::vector<MerkleNode>* TakeNodes();
+    void GiveNodes(std::vector<MerkleNode>* v);
 
    private:
+    CopyPool* Pool() {
+        if (!pool_ && copy_threads_ < 0) {
+            const char* e = std::getenv("NKV_COPY_THREADS");
+            const int hw = int(std::thread::hardware_concurrency());
+            SetCopyThreads(e ? std::atoi(e) : std::min(16, std::max(1, hw)));
+        }
+        return pool_.get();
+    }
+    void SubmitJob() {
+        if (job_) {
+            job_->end = used_;
+            pool_->Submit(std::move(job_));
+        }
+        job_.reset();
+        job_bytes_ = 0;
+    }
     void Reserve(uint64_t bytes) {
         if (bytes <= cap_) return;
+        Settle();  // no queued copy may land in the old block
         uint64_t want = cap_ ? cap_ * 2 : (uint64_t(1) << 20);
         while (want < bytes) want *= 2;
         void* p = nullptr;
@@ -188,6 +363,11 @@ class Session {
     uint64_t cap_ = 0, used_ = 0, epoch_ = 0, allocs_ = 0, streamed_ = 0;
     bool stream_ = true, nt_ = true;
     std::shared_ptr<Batch> batch_;
+    std::unique_ptr<CopyPool> pool_;
+    std::unique_ptr<CopyPool::Job> job_;  // the job NewLeaf is filling
+    uint64_t job_bytes_ = 0;
+    int copy_threads_ = -1;  // -1: not chosen yet (Pool())
+    std::vector<std::vector<MerkleNode>*> spare_;
 };
 
 struct MerkleNode {  // merklenode.go:15-19
@@ -261,11 +441,39 @@ inline MerkleNode NewLeaf(const std::string& v) {
     return NewLeaf(reinterpret_cast<const uint8_t*>(v.data()), v.size());
 }
 
+inline Session::~Session() {
+    pool_.reset();
+    for (auto* v : spare_) delete v;
+    if (arena_) nkv_host_free(ctx_, arena_);
+    nkv_ctx_destroy(ctx_);
+}
+
+inline std::vector<MerkleNode>* Session::TakeNodes() {
+    if (spare_.empty()) return new std::vector<MerkleNode>();
+    auto* v = spare_.back();
+    spare_.pop_back();
+    return v;
+}
+
+inline void Session::GiveNodes(std::vector<MerkleNode>* v) {
+    if (!v) return;
+    if (spare_.size() >= 2) {  // two trees' worth (a flush and the one before)
+        delete v;
+        return;
+    }
+    spare_.push_back(v);
+}
+
 inline std::vector<std::vector<uint8_t>> Sha1Many(const std::vector<std::vector<uint8_t>>& msgs);
 
 class MerkleTree {  // merkletree.go:13-15
    public:
     MerkleNode* Root = nullptr;
+
+    MerkleTree() = default;
+    ~MerkleTree() { Session::Default().GiveNodes(inner_); }
+    MerkleTree(const MerkleTree&) = delete;
+    MerkleTree& operator=(const MerkleTree&) = delete;
 
     // merkletree.go:67-92: write the BFS image; O_WRONLY|O_CREAT without O_TRUNC
     void Serialize(const std::string& fname) {
@@ -276,9 +484,10 @@ class MerkleTree {  // merkletree.go:13-15
     std::vector<uint8_t> SerializeBytes() {
         std::vector<uint8_t> w;
         std::vector<MerkleNode*> q{Root};  // BFS queue: q[head..) still to visit
-        if (!nodes_.empty()) {
-            q.reserve(nodes_.size());
-            w.reserve(21 * nodes_.size());
+        const size_t owned = leaves_.size() + (inner_ ? inner_->size() : 0);
+        if (owned) {
+            q.reserve(owned);
+            w.reserve(21 * owned);
         }
         for (size_t head = 0; head < q.size(); ++head) {
             MerkleNode* n = q[head];
@@ -300,15 +509,17 @@ class MerkleTree {  // merkletree.go:13-15
         size_t k;
         while ((k = std::fread(buf, 1, sizeof buf, f)) > 0) blob.insert(blob.end(), buf, buf + k);
         std::fclose(f);
-        nodes_.clear();
+        leaves_.clear();
+        if (!inner_) inner_ = Session::Default().TakeNodes();
+        inner_->clear();
         const uint8_t* p = blob.data();
         const uint8_t* end = p + blob.size();
         while (true) {
             MerkleNode n;
             if (n.Deserialize(p, end)) break;
-            nodes_.push_back(std::move(n));
+            inner_->push_back(std::move(n));
         }
-        Root = nodes_.empty() ? nullptr : &nodes_.front();
+        Root = inner_->empty() ? nullptr : &inner_->front();
         n_ = 0;  // no longer a tree New built
     }
 
@@ -428,7 +639,10 @@ class MerkleTree {  // merkletree.go:13-15
         return val[root];
     }
 
-    std::deque<MerkleNode> nodes_;  // owns every node of the tree (stable addresses)
+    // the tree's nodes (stable addresses): New's leaves, and the internal nodes +
+    // pads in storage recycled from destroyed trees (Deserialize: every node)
+    std::vector<MerkleNode> leaves_;
+    std::vector<MerkleNode>* inner_ = nullptr;
     std::vector<uint8_t> levels_;
     uint64_t n_ = 0;  // leaves New built the tree from
     NewTiming timing_;
@@ -474,6 +688,7 @@ inline std::unique_ptr<MerkleTree> New(std::vector<MerkleNode> level, std::strin
     for (uint64_t i = 0; same_batch && i < n; ++i)
         same_batch = level[i].pend == b0 && level[i].pend_idx == i && !level[i].Left && !level[i].Right;
     if (same_batch) {
+        Session::Default().Settle();
         Session::Fence();
         check(nkv_tree_from_values(ctx, Session::Default().arena(), b0->off.data(), b0->len.data(), n,
                                    nullptr, nodes, nullptr),
@@ -502,34 +717,47 @@ inline std::unique_ptr<MerkleTree> New(std::vector<MerkleNode> level, std::strin
         }
     }
     const auto c1 = clk::now();
-    // materialize the pointer tree: copies of the given leaves (Go copies
-    // `l := level[i]`), then parents level by level with the empty pad node
-    auto& pool = t->nodes_;
-    std::vector<MerkleNode*> below;
-    below.reserve(n + 1);
-    for (auto& x : level) {  // `level` is New's own copy: move out of it
-        x.Resolve();
-        pool.push_back(std::move(x));
-        below.push_back(&pool.back());
+    // materialize the pointer tree: the given leaves (Go copies `l :=
+    // level[i]`: `level` is New's own copy, kept as the tree's leaves), then
+    // parents level by level with the empty pad node (merkletree.go:32-34), in
+    // node storage recycled from destroyed trees: no allocation per node
+    t->leaves_ = std::move(level);
+    auto& leaves = t->leaves_;
+    if (same_batch) {
+        for (uint64_t i = 0; i < n; ++i) {
+            leaves[i].Data.assign(nodes + 20 * i, nodes + 20 * i + 20);
+            leaves[i].pend.reset();
+        }
     }
     t->n_ = n;
     const int lv = nkv_num_levels(n);
+    uint64_t inner = nkv_total_nodes(n) - n;
+    for (int L = 0; L + 1 < lv; ++L) inner += nkv_level_count(n, L) & 1;  // pads
+    t->inner_ = Session::Default().TakeNodes();
+    std::vector<MerkleNode>& pool = *t->inner_;
+    pool.resize(inner);
+    size_t k = 0;
+    std::vector<MerkleNode*> below;
+    below.reserve(n + 1);
+    for (auto& x : leaves) below.push_back(&x);
     for (int L = 1; L < lv; ++L) {
-        if (below.size() % 2) {
-            pool.emplace_back();  // MerkleNode{Data: []byte{}} (merkletree.go:32-34)
-            below.push_back(&pool.back());
+        if (below.size() % 2) {  // MerkleNode{Data: []byte{}}
+            MerkleNode& p = pool[k++];
+            p.Data.clear();
+            p.Left = p.Right = nullptr;
+            p.pend.reset();
+            below.push_back(&p);
         }
-        std::vector<MerkleNode*> cur;
         const uint64_t s = nkv_level_start(n, L), c = nkv_level_count(n, L);
-        cur.reserve(c + 1);
         for (uint64_t i = 0; i < c; ++i) {
-            MerkleNode m(std::vector<uint8_t>(nodes + 20 * (s + i), nodes + 20 * (s + i) + 20));
+            MerkleNode& m = pool[k++];
+            m.Data.assign(nodes + 20 * (s + i), nodes + 20 * (s + i) + 20);
             m.Left = below[2 * i];
             m.Right = below[2 * i + 1];
-            pool.push_back(std::move(m));
-            cur.push_back(&pool.back());
+            m.pend.reset();
+            below[i] = &m;  // below[2i], below[2i+1] are read before below[i] is written
         }
-        below.swap(cur);
+        below.resize(c);
     }
     t->Root = below[0];
     t->timing_.call_ms = std::chrono::duration<double, std::milli>(c1 - c0).count();

@@ -22,13 +22,11 @@ NKV_ERR_NOMEM = 4
 NKV_ERR_IO = 5
 NKV_OPT_LEAF_LOAD = 1
 NKV_OPT_BUCKET = 2
-NKV_OPT_DEEP_PREFETCH = 3
 NKV_OPT_QUEUE_SPLIT = 4
 NKV_OPT_QUEUE_WAVES = 5
 NKV_OPT_CRC_LOAD = 6
 NKV_OPT_HOST_THREADS = 7
 NKV_OPT_STAGE_CHUNK = 8
-NKV_OPT_QUEUE_RING = 9
 NKV_OPT_BLOOM_PATH = 10
 NKV_OPT_RECORDS_FUSED = 11
 NKV_OPT_TABLE_LANES = 12
@@ -134,7 +132,7 @@ SIGNATURES = {
     "nkv_group_trees_from_values": (_int, [_vp, ctypes.POINTER(NkvValues), _int]),
     "nkv_split_span": (_u64, [_u64, _int]),
     "nkv_group_tree_from_values": (_int, [_vp, _u8p, _u64p, _u64p, _u64, _u8p, _u8p, _u8p]),
-    "nkv_group_tree_dev": (_int, [_vp, _tabp, _u64, _vp, _u8p]),
+    "nkv_group_tree_dev": (_int, [_vp, _tabp, _u64, ctypes.POINTER(_vp), _u8p]),
     "nkv_group_tree_fetch": (_int, [_vp, _u8p, _u8p]),
 }
 

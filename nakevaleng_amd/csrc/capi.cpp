@@ -514,8 +514,6 @@ int nkv_ctx_set_option(nkv_ctx* c, int key, int64_t value) try {
             if (value < 0 || value > 2) return NKV_ERR_INVALID;
             c->bucket = int(value);
             return NKV_OK;
-        case NKV_OPT_DEEP_PREFETCH:  // the work-queue kernel is the only sorted path left
-            return value == 3 ? NKV_OK : NKV_ERR_INVALID;
         case NKV_OPT_QUEUE_SPLIT:
             if (value < 0 || value > 0xFFFFFFFFll) return NKV_ERR_INVALID;
             c->queue_split = int(std::min<int64_t>(value, 0x7FFFFFFF));
@@ -528,8 +526,6 @@ int nkv_ctx_set_option(nkv_ctx* c, int key, int64_t value) try {
             if (value < 0 || value > 2) return NKV_ERR_INVALID;
             c->bloom_path = int(value);
             return NKV_OK;
-        case NKV_OPT_QUEUE_RING:  // the 3-slot value-relative ring is the only one left
-            return value == 13 ? NKV_OK : NKV_ERR_INVALID;
         case NKV_OPT_HOST_THREADS:
             if (value < 0 || value > 256) return NKV_ERR_INVALID;
             c->stage.want_threads = int(value);

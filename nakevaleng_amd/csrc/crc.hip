@@ -42,7 +42,8 @@ __constant__ CrcTables c_crc = make_crc_tables();
 
 // Lane-private table layout: two 64 KiB halves (tables 0, 1 and 2, 3) of 256
 // rows (entry e) of 64 words: words 0-31 = table 2h, copies 0-31; words 32-63 =
-// table 2h + 1.  k_crc_lanes's only LDS object, so it starts at LDS address 0.
+// table 2h + 1.  k_crc_lanes's only LDS object, so it starts at LDS address 0
+// (checked in the kernel).
 constexpr uint32_t kLaneTabWords = 2 * 256 * 64;  // 128 KiB
 
 // one lookup: table k (compile-time), byte j (0..3) of x; la = lane constant of
@@ -53,8 +54,10 @@ __device__ __forceinline__ uint32_t lane_lut(uint32_t x, uint32_t la) {
     constexpr uint32_t sel = (12u << 24) | (2u << 16) | (uint32_t(4 + J) << 8) | 0u;
     const uint32_t addr = __builtin_amdgcn_perm(x, la, sel);
     uint32_t v;
-    if constexpr (K & 1) asm volatile("ds_read_b32 %0, %1 offset:128" : "=v"(v) : "v"(addr));
-    else asm volatile("ds_read_b32 %0, %1" : "=v"(v) : "v"(addr));
+    // "memory": the read depends on the table fill (its address comes from the
+    // table's own LDS address through la, so the fill cannot be dropped either)
+    if constexpr (K & 1) asm volatile("ds_read_b32 %0, %1 offset:128" : "=v"(v) : "v"(addr) : "memory");
+    else asm volatile("ds_read_b32 %0, %1" : "=v"(v) : "v"(addr) : "memory");
     return v;
 }
 
@@ -235,8 +238,14 @@ __global__ __launch_bounds__(kCrcLanesWG) void k_crc_lanes(const uint8_t* __rest
         tab[i] = c_crc.t[k][e];  // every copy c = i & 31 holds the same entry
     }
     __syncthreads();
-    // lane constants of the two halves: the copy offset (byte 0), the half (byte 2)
-    const uint32_t la0 = (threadIdx.x & 31u) * 4u, la1 = la0 | 0x10000u;
+    // lane constants of the two halves: the copy offset (byte 0), the half (byte
+    // 2), built on the table's real LDS address.  The v_perm address
+    // form has no room for a base, so the table must be the kernel's only LDS
+    // object, at address 0: anything else is a build defect, stopped here
+    // rather than left to give wrong checksums.
+    const uint32_t lds_tab = uint32_t(reinterpret_cast<uintptr_t>(tab));
+    if (lds_tab != 0u) __builtin_trap();
+    const uint32_t la0 = lds_tab + (threadIdx.x & 31u) * 4u, la1 = la0 | 0x10000u;
     const uint64_t stride = uint64_t(gridDim.x) * WG;
     const uint64_t w0 = uint64_t(blockIdx.x) * WG + (threadIdx.x & ~63u);  // this wave's first span
     for (uint64_t wb = w0; wb < n; wb += stride) {  // wave-uniform loop

@@ -13,7 +13,8 @@
 //     and the only collective is the all-gather of the 20-byte roots;
 //   - one table too large for one GPU splits at 2^k-aligned leaf ranges
 //     (padding only happens at a level's end, merkletree.go:32-34), the
-//     level-k sub-roots are all-gathered and member 0 reduces the top levels.
+//     level-k sub-roots are all-gathered and every member reduces the top
+//     levels, so every member holds the root.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <string.h>
@@ -80,6 +81,26 @@ bool on_device(const void* p, int device) {
 }
 
 int nccl_st(ncclResult_t r) { return r == ncclSuccess ? NKV_OK : NKV_ERR_DEVICE; }
+
+// Every pointer the table's kind hands to a kernel lives on `device` (ADVICE
+// r03: offsets or stats on another GPU would become peer reads or faults
+// instead of NKV_ERR_INVALID).  Optional outputs may be NULL.
+bool table_on_device(const nkv_table& t, int device) {
+    auto opt = [&](const void* p) { return !p || on_device(p, device); };
+    if (!on_device(t.nodes, device) || !on_device(t.base, device)) return false;
+    switch (t.kind) {
+        case NKV_TABLE_STRIDED:
+            return true;
+        case NKV_TABLE_VALUES:
+            return on_device(t.off, device) && on_device(t.lens, device);
+        case NKV_TABLE_RECORDS:
+            return on_device(t.off, device) && opt(t.err);
+        case NKV_TABLE_VERIFY:
+            return on_device(t.off, device) && opt(t.crc) && opt(t.stats);
+        default:
+            return true;  // the build refuses the kind itself
+    }
+}
 
 }  // namespace
 
@@ -149,12 +170,14 @@ struct nkv_group {
     std::vector<ncclComm_t> comm;
     std::vector<DevBuf> slot, gathered;  // per member: roots to send, g x roots received
     std::vector<hipEvent_t> ev, ev2;     // per member (copy transport, split-tree joins)
-    // the latest split tree (nkv_group_tree_dev / _from_values)
+    // the latest split tree (nkv_group_tree_dev / _from_values); n == 0: none
+    // (a refused or failed split call leaves none, so fetch refuses)
     uint64_t n = 0, span = 0, G = 0;
     int k = 0;
     std::vector<uint64_t> nr;      // leaves per member
     std::vector<DevBuf> levels;    // per member: levels 0..k of its range, level-major
-    DevBuf top, full, img;         // member 0: the top tree, the whole tree, its image
+    std::vector<DevBuf> top;       // per member: the top tree over the G sub-roots
+    DevBuf full, img;              // member 0: the whole tree, its image
 };
 
 namespace {
@@ -221,24 +244,45 @@ int group_sync(nkv_group* grp) {
 // top are its lone node re-hashed, one node each).
 uint64_t range_nodes(uint64_t m, int k) { return m ? start_of(m, k + 1) : 0; }
 
-// The split plan for n leaves over the group; member r's range length.
-void split_plan(nkv_group* grp, uint64_t n) {
-    grp->n = n;
-    grp->span = nkv_split_span(n, grp->g);
-    grp->k = 0;
-    while ((uint64_t(1) << grp->k) < grp->span) ++grp->k;
-    grp->G = (n + grp->span - 1) / grp->span;
-    grp->nr.assign(grp->g, 0);
-    for (int r = 0; r < grp->g; ++r) {
-        const uint64_t lo = std::min(n, uint64_t(r) * grp->span);
-        grp->nr[r] = std::min(n, lo + grp->span) - lo;
+// The split plan for n leaves over g members: span 2^k, G ranges, member r's
+// range length.  Computed apart from the group and committed only once the
+// call's arguments passed (a refused call must not change the plan
+// a later nkv_group_tree_fetch reads).
+struct SplitPlan {
+    uint64_t n = 0, span = 0, G = 0;
+    int k = 0;
+    std::vector<uint64_t> nr;
+};
+
+SplitPlan split_plan(uint64_t n, int g) {
+    SplitPlan p;
+    p.n = n;
+    p.span = nkv_split_span(n, g);
+    while ((uint64_t(1) << p.k) < p.span) ++p.k;
+    p.G = (n + p.span - 1) / p.span;
+    p.nr.assign(g, 0);
+    for (int r = 0; r < g; ++r) {
+        const uint64_t lo = std::min(n, uint64_t(r) * p.span);
+        p.nr[r] = std::min(n, lo + p.span) - lo;
     }
+    return p;
+}
+
+void commit_plan(nkv_group* grp, const SplitPlan& p) {
+    grp->n = p.n;
+    grp->span = p.span;
+    grp->k = p.k;
+    grp->G = p.G;
+    grp->nr = p.nr;
 }
 
 // After every member built levels 0..k of its range into levels[r]: all-gather
-// the level-k sub-roots, reduce the top levels on member 0 into `top`, and
-// put the root at d_root (member 0, nullable) / root20 (host, nullable).
-int split_top(nkv_group* grp, void* d_root, uint8_t* root20) {
+// the level-k sub-roots and reduce the top ceil(log2 G) levels on EVERY member
+// into its own top[r] (every rank computes the top levels; G <= 64
+// nodes, one single-wave chain per member, the members' chains run
+// concurrently), then put member r's root at d_roots[r] (nullable array and
+// entries, each on member r's device) and member 0's at root20 (host, nullable).
+int split_top(nkv_group* grp, void* const* d_roots, uint8_t* root20) {
     const int g = grp->g;
     std::vector<const void*> src(g);
     std::vector<void*> dst(g);
@@ -261,16 +305,21 @@ int split_top(nkv_group* grp, void* d_root, uint8_t* root20) {
     // (the copy transport records its own events; the RCCL kernels order the
     // streams themselves)
     TRY(allgather(grp, src.data(), dst.data(), 20));
-    TRY(member_bind(grp, 0));
-    nkv_ctx* c0 = grp->ctx[0];
     const uint64_t G = grp->G;
     const uint64_t tn = G == 1 ? 1 : total_of(G);
-    TRY(grow(grp->top, 20 * tn));
-    uint8_t* top = static_cast<uint8_t*>(grp->top.p);
-    HIPTRY(hipMemcpyAsync(top, grp->gathered[0].p, 20 * G, hipMemcpyDeviceToDevice, c0->stream));
-    if (G > 1) HIPTRY(launch_reduce(top, G, 0, levels_of(G) - 1, c0->stream));
-    const uint8_t* root = top + 20 * (tn - 1);
-    if (d_root) HIPTRY(hipMemcpyAsync(d_root, root, 20, hipMemcpyDeviceToDevice, c0->stream));
+    for (int r = 0; r < g; ++r) {
+        TRY(member_bind(grp, r));
+        nkv_ctx* c = grp->ctx[r];
+        TRY(grow(grp->top[r], 20 * tn));
+        uint8_t* top = static_cast<uint8_t*>(grp->top[r].p);
+        HIPTRY(hipMemcpyAsync(top, grp->gathered[r].p, 20 * G, hipMemcpyDeviceToDevice, c->stream));
+        if (G > 1) HIPTRY(launch_reduce(top, G, 0, levels_of(G) - 1, c->stream));
+        if (d_roots && d_roots[r])
+            HIPTRY(hipMemcpyAsync(d_roots[r], top + 20 * (tn - 1), 20, hipMemcpyDeviceToDevice, c->stream));
+    }
+    TRY(member_bind(grp, 0));
+    nkv_ctx* c0 = grp->ctx[0];
+    const uint8_t* root = static_cast<const uint8_t*>(grp->top[0].p) + 20 * (tn - 1);
     if (root20) {
         HIPTRY(hipMemcpyAsync(c0->h_small, root, 20, hipMemcpyDeviceToHost, c0->stream));
         HIPTRY(hipStreamSynchronize(c0->stream));
@@ -330,6 +379,7 @@ int nkv_group_create(const int* devices, int g, nkv_group** out) try {
     grp->slot.resize(g);
     grp->gathered.resize(g);
     grp->levels.resize(g);
+    grp->top.resize(g);
     grp->ev.assign(g, nullptr);
     grp->ev2.assign(g, nullptr);
     int rc = NKV_OK;
@@ -362,14 +412,14 @@ void nkv_group_destroy(nkv_group* grp) {
         if (cm) (void)ncclCommDestroy(cm);
     for (int i = 0; i < grp->g; ++i) {
         (void)hipSetDevice(grp->dev[i]);
-        for (DevBuf* b : {&grp->slot[i], &grp->gathered[i], &grp->levels[i]})
+        for (DevBuf* b : {&grp->slot[i], &grp->gathered[i], &grp->levels[i], &grp->top[i]})
             if (b->p) (void)hipFree(b->p);
         if (grp->ev[i]) (void)hipEventDestroy(grp->ev[i]);
         if (grp->ev2[i]) (void)hipEventDestroy(grp->ev2[i]);
     }
     if (!grp->dev.empty()) {
         (void)hipSetDevice(grp->dev[0]);
-        for (DevBuf* b : {&grp->top, &grp->full, &grp->img})
+        for (DevBuf* b : {&grp->full, &grp->img})
             if (b->p) (void)hipFree(b->p);
     }
     for (nkv_ctx* c : grp->ctx) nkv_ctx_destroy(c);
@@ -423,8 +473,7 @@ int nkv_group_trees_dev(nkv_group* grp, const nkv_table* tables, int k, uint8_t*
     if (k == 0) return NKV_OK;
     const int g = grp->g;
     for (int t = 0; t < k; ++t)
-        if (!on_device(tables[t].nodes, grp->dev[t % g]) || !on_device(tables[t].base, grp->dev[t % g]))
-            return NKV_ERR_INVALID;
+        if (!table_on_device(tables[t], grp->dev[t % g])) return NKV_ERR_INVALID;
     const int per = (k + g - 1) / g;  // roots per member (the last slots of some stay unused)
     std::vector<const void*> src(g);
     std::vector<void*> dst(g);
@@ -486,30 +535,46 @@ int nkv_group_trees_from_values(nkv_group* grp, const nkv_values* tables, int k)
     return NKV_OK;
 } NKV_CATCH
 
-int nkv_group_tree_dev(nkv_group* grp, const nkv_table* parts, uint64_t n, void* d_root, uint8_t* root20) try {
-    if (!grp || !parts) return NKV_ERR_INVALID;
+int nkv_group_tree_dev(nkv_group* grp, const nkv_table* parts, uint64_t n, void* const* d_roots,
+                       uint8_t* root20) try {
+    if (!grp) return NKV_ERR_INVALID;
+    grp->n = 0;  // this call replaces the latest tree, refused or not (fetch then refuses)
+    if (!parts) return NKV_ERR_INVALID;
     if (n == 0) return NKV_ERR_EMPTY;
     if (n > kMaxN * uint64_t(grp->g)) return NKV_ERR_INVALID;
-    split_plan(grp, n);
+    const SplitPlan plan = split_plan(n, grp->g);
     for (int r = 0; r < grp->g; ++r) {
-        if (parts[r].n != grp->nr[r]) return NKV_ERR_INVALID;
-        if (grp->nr[r] && !on_device(parts[r].base, grp->dev[r])) return NKV_ERR_INVALID;
+        if (parts[r].n != plan.nr[r]) return NKV_ERR_INVALID;
+        if (plan.nr[r]) {
+            if (parts[r].kind != NKV_TABLE_STRIDED && parts[r].kind != NKV_TABLE_VALUES) return NKV_ERR_INVALID;
+            nkv_table t = parts[r];
+            t.nodes = const_cast<void*>(t.base);  // nodes are the group's: check the rest
+            if (!table_on_device(t, grp->dev[r])) return NKV_ERR_INVALID;
+        }
+        if (d_roots && d_roots[r] && !on_device(d_roots[r], grp->dev[r])) return NKV_ERR_INVALID;
     }
-    for (int r = 0; r < grp->g; ++r) {
+    commit_plan(grp, plan);
+    grp->n = 0;  // until the whole tree stands
+    int rc = NKV_OK;
+    for (int r = 0; r < grp->g && rc == NKV_OK; ++r) {
         if (!grp->nr[r]) continue;
-        TRY(member_bind(grp, r));
-        TRY(build_range(grp, r, parts[r], false, nullptr));
+        rc = member_bind(grp, r);
+        if (rc == NKV_OK) rc = build_range(grp, r, parts[r], false, nullptr);
     }
-    return split_top(grp, d_root, root20);
+    if (rc == NKV_OK) rc = split_top(grp, d_roots, root20);
+    if (rc == NKV_OK) grp->n = n;
+    return rc;
 } NKV_CATCH
 
 int nkv_group_tree_from_values(nkv_group* grp, const uint8_t* base, const uint64_t* off, const uint64_t* len,
                                uint64_t n, uint8_t* root20, uint8_t* nodes_out, uint8_t* img_out) try {
     if (!grp) return NKV_ERR_INVALID;
+    grp->n = 0;  // set again once the whole tree stands
     if (n == 0) return NKV_ERR_EMPTY;
     if (!base || !off || !len) return NKV_ERR_INVALID;
     if (n > kMaxN * uint64_t(grp->g)) return NKV_ERR_INVALID;
-    split_plan(grp, n);
+    commit_plan(grp, split_plan(n, grp->g));
+    grp->n = 0;
     const int g = grp->g;
     std::vector<int> rc(g, NKV_OK);
     // one host thread per member stages its leaf range and builds its levels
@@ -542,7 +607,14 @@ int nkv_group_tree_from_values(nkv_group* grp, const uint8_t* base, const uint64
     for (auto& x : th) x.join();
     for (int r = 0; r < g; ++r) TRY(rc[r]);
     TRY(split_top(grp, nullptr, root20));
-    if (nodes_out || img_out) TRY(nkv_group_tree_fetch(grp, nodes_out, img_out));
+    grp->n = n;
+    if (nodes_out || img_out) {
+        const int fr = nkv_group_tree_fetch(grp, nodes_out, img_out);
+        if (fr != NKV_OK) {
+            grp->n = 0;
+            return fr;
+        }
+    }
     return group_sync(grp);
 } NKV_CATCH
 
@@ -573,7 +645,7 @@ int nkv_group_tree_fetch(nkv_group* grp, uint8_t* nodes_out, uint8_t* img_out) t
         }
     }
     if (grp->G > 1) {
-        const uint8_t* top = static_cast<const uint8_t*>(grp->top.p);
+        const uint8_t* top = static_cast<const uint8_t*>(grp->top[0].p);
         for (int L = k + 1; L < levels_of(n); ++L)
             HIPTRY(hipMemcpyAsync(full + 20 * start_of(n, L), top + 20 * start_of(grp->G, L - k),
                                   20 * count_of(grp->G, L - k), hipMemcpyDeviceToDevice, c0->stream));

@@ -5,6 +5,7 @@ torch.distributed.run (a child process, before any GPU call) instead of
 silently measuring one GPU; under a launcher WORLD_SIZE must equal N.  The
 per-step root all-gather (RootGather) is pipelined over two tree buffers.
 """
+import json
 import os
 import sys
 import types
@@ -239,3 +240,156 @@ def test_valu_ceiling_prices_each_kernel_at_its_own_count():
     # 1024 SIMDs at 2.2 GHz, one VALU per 4 cycles, 623 per 4 KiB wave-block
     assert abs(bench.valu_ceiling(2200.0, "leaf") - 1024 * 2.2e9 / (623.0 * 4) * 4096 / 1e9) < 1e-6
     assert bench.valu_ceiling(2200.0, "verify") < bench.valu_ceiling(2200.0, "records") < bench.valu_ceiling(2200.0, "leaf")
+
+
+# ---------------------------------------------------------------------------
+# round 4: the line verifies every rank against committed
+# roots, carries the CPU baseline at every N, and merges the one-process C-ABI
+# group runs (fresh child processes) as sub-records.
+
+def test_merged_line_shape(monkeypatch, capsys):
+    """main() on rank 0: the ranks' line + capi_group + capi_one_tree + the CPU
+    baseline, one JSON line (stand-ins for the GPU run and the children)."""
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "1", "--steps", "3", "--warmup", "1"])
+    base = {"metric": "m", "value": 1.0, "n_gpus": 1, "verified_vs_oracle": True,
+            "verified_ranks": [True], "cpu_baseline": None}
+    monkeypatch.setattr(bench, "run_ranks", lambda args, T: dict(base))
+    calls = []
+
+    def fake_child(args, world, extra, timeout, run=None):
+        calls.append((world, tuple(extra)))
+        return {"value": 2.0, "verified_vs_oracle": True, "n_gpus": world}
+    monkeypatch.setattr(bench, "capi_child", fake_child)
+    monkeypatch.setattr(bench, "cpu_baseline", lambda n, v: {"value": 1.25, "unit": "GiB/s", "cores": 1,
+                                                              "kind": "port", "sample": f"{n} x {v}"})
+    bench.main()
+    line = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+    assert line["verified_vs_oracle"] is True and line["verified_ranks"] == [True]
+    assert line["capi_group"]["value"] == 2.0 and line["capi_one_tree"]["verified_vs_oracle"] is True
+    assert line["cpu_baseline"]["cores"] == 1 and line["cpu_baseline"]["sample"] == f"{1 << 20} x 4096"
+    assert calls == [(1, ()), (1, ("--config", "one_tree", "--tables", "1"))]
+
+
+def test_merged_line_at_n_gpus_keeps_cpu_baseline(monkeypatch, capsys):
+    """Under the launcher (N = 8, rank 0) the CPU baseline is still measured,
+    and runs4 gets the group sub-record but no one-tree run."""
+    monkeypatch.setenv("WORLD_SIZE", "8")
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "8", "--config", "runs4", "--no-capi"])
+    monkeypatch.setattr(bench, "run_ranks", lambda args, T: {"n_gpus": 8, "value": 8.0})
+    monkeypatch.setattr(bench, "capi_child", lambda *a, **k: pytest.fail("--no-capi"))
+    monkeypatch.setattr(bench, "cpu_baseline", lambda n, v: {"value": 1.0, "cores": 1})
+    bench.main()
+    line = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+    assert line["cpu_baseline"] == {"value": 1.0, "cores": 1} and "capi_group" not in line
+
+
+def test_other_ranks_print_nothing(monkeypatch, capsys):
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2"])
+    monkeypatch.setattr(bench, "run_ranks", lambda args, T: None)
+    monkeypatch.setattr(bench, "capi_child", lambda *a, **k: pytest.fail("only rank 0"))
+    bench.main()
+    assert capsys.readouterr().out == ""
+
+
+def test_capi_child_command_env_and_errors(monkeypatch):
+    """The group child: this run's flags + --backend capi --gpus N, outside the
+    launcher's process group (no WORLD_SIZE / RANK / MASTER_*), its line's keys
+    kept; a failing or hung child gives {"error": ...}, never an exception."""
+    import subprocess
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "4", "--steps", "7"])
+    for k, v in (("WORLD_SIZE", "4"), ("RANK", "0"), ("LOCAL_RANK", "0"), ("MASTER_PORT", "1234")):
+        monkeypatch.setenv(k, v)
+    args = bench.parse(["--gpus", "4", "--steps", "7"])
+    seen = {}
+
+    class P:
+        returncode = 0
+        stdout = "noise\n" + json.dumps({"value": 9.5, "n_gpus": 4, "root_gather_ok": True,
+                                         "verified_vs_oracle": True, "verified_members": [True] * 4,
+                                         "config": {"parallelism": "4 tables"}, "roofline": {"frac": 0.44}}) + "\n"
+
+    def run(cmd, **kw):
+        seen["cmd"], seen["env"] = cmd, kw["env"]
+        return P()
+    sub = bench.capi_child(args, 4, ["--config", "one_tree", "--tables", "1"], 60, run=run)
+    cmd = seen["cmd"]
+    assert cmd[1] == os.path.abspath(bench.__file__)
+    assert cmd[cmd.index("--backend") + 1] == "capi"
+    assert cmd[len(cmd) - 1 - cmd[::-1].index("--gpus") + 1] == "4"  # the last --gpus wins
+    assert cmd[len(cmd) - 1 - cmd[::-1].index("--config") + 1] == "one_tree"
+    assert not any(k in seen["env"] for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"))
+    assert seen["env"]["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+    assert sub["value"] == 9.5 and sub["verified_members"] == [True] * 4 and sub["roofline_frac"] == 0.44
+    assert sub["parallelism"] == "4 tables"
+    # the child's command line parses to the group backend over 4 GPUs
+    child = bench.parse(cmd[2:])
+    assert child.backend == "capi" and child.gpus == 4 and child.config == "one_tree" and child.steps == 7
+
+    class Bad:
+        returncode = 1
+        stdout = ""
+    assert "error" in bench.capi_child(args, 4, [], 60, run=lambda cmd, **kw: Bad())
+
+    def hang(cmd, **kw):
+        raise subprocess.TimeoutExpired(cmd, 60)
+    assert "timed out" in bench.capi_child(args, 4, [], 60, run=hang)["error"]
+
+
+def test_verdict_codes():
+    assert bench.verdict([1, 1, 1]) is True
+    assert bench.verdict([1, 0, 1]) is False
+    assert bench.verdict([1, -1]) is None
+    assert bench.verdict([0, -1]) is False
+    assert bench.verdict([]) is None
+
+
+def test_expected_roots_cover_the_driver_shapes():
+    """The committed roots cover configs[1] on ranks 0-7 (tables 0-3) and the
+    one tree over 1-8 ranks; other shapes fall back to --verify."""
+    for r in range(8):
+        assert len(bench.expected_roots("sstable4k", 1 << 20, 4096, r, 1)) == 1
+        assert len(bench.expected_roots("runs4", 1 << 20, 4096, r, 4)) == 4
+    for N in range(1, 9):
+        assert len(bench.expected_one_tree(1 << 20, 4096, N)) == 40
+    assert bench.expected_roots("sstable4k", 1 << 20, 4096, 8, 1) is None
+    assert bench.expected_roots("mixed", 1 << 20, 4096, 0, 1) is None
+    assert bench.expected_roots("sstable4k", 65536, 4096, 0, 1) is None
+    assert bench.expected_one_tree(65536, 4096, 2) is None
+
+
+def _verify_worker(rank, world, port, bad_rank, q):
+    import torch.distributed as dist
+    from oracle import oracle_c as oc
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # this rank's table at configs[0]'s size, built by the oracle standing in
+    # for the device, seeded as bench.build_tables seeds rank r's table
+    data = oc.splitmix64_bytes(1024 * 1024, bench.SEED + rank)
+    root = oc.tree_from_digests(oc.leaf_hashes_strided(data, 1024, 1024, 1024))[-1].tobytes().hex()
+    if rank == bad_rank:
+        root = ("0" if root[0] != "0" else "1") + root[1:]
+    want = bench.expected_roots("sstable4k", 1024, 1024, rank, 1)
+    code = -1 if want is None else int([root] == want)
+    codes = bench.rank_codes(dist, world, rank, code, "cpu")
+    q.put((rank, codes, bench.verdict(codes)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("bad_rank", [-1, 1])
+def test_rank_verification_world2(oracle, bad_rank):
+    """gloo world 2: each rank checks its own root against the committed roots
+    and every rank learns every rank's result; one wrong rank fails the line."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_verify_worker, args=(r, 2, port, bad_rank, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {r: (codes, v) for r, codes, v in (q.get(timeout=120) for _ in procs)}
+    for p in procs:
+        p.join(timeout=60)
+    want_codes = [1, 1] if bad_rank < 0 else [1, 0]
+    assert res[0] == res[1] == (want_codes, bad_rank < 0)

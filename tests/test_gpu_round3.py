@@ -242,10 +242,12 @@ def test_group_split_tree_copy_transport(nkv, oracle, g, n):
         parts, keep = split_parts(_lib, g, n, data, vl)
         arr = (_lib.NkvTable * g)(*parts)
         root = np.zeros(20, np.uint8)
-        d_root = torch.zeros(20, dtype=torch.uint8, device="cuda")
-        _lib.check(L.nkv_group_tree_dev(grp.h, arr, n, d_root.data_ptr(), _lib.p8(root)))
+        d_roots = [torch.zeros(20, dtype=torch.uint8, device="cuda") for _ in range(g)]
+        _lib.check(L.nkv_group_tree_dev(grp.h, arr, n, (ctypes.c_void_p * g)(*[d.data_ptr() for d in d_roots]),
+                                        _lib.p8(root)))
         assert root.tobytes() == want[-1].tobytes()
-        assert d_root.cpu().numpy().tobytes() == want[-1].tobytes()
+        # every member reduced the top levels and holds the root
+        assert all(d.cpu().numpy().tobytes() == want[-1].tobytes() for d in d_roots)
         nodes = np.zeros((L.nkv_total_nodes(n), 20), np.uint8)
         img = np.zeros(L.nkv_bfs_size(n), np.uint8)
         _lib.check(L.nkv_group_tree_fetch(grp.h, _lib.p8(nodes), _lib.p8(img)))
@@ -256,6 +258,16 @@ def test_group_split_tree_copy_transport(nkv, oracle, g, n):
             bad = list(parts)
             bad[0] = _lib.table(_lib.NKV_TABLE_STRIDED, 0, parts[0].n - 1, base=parts[0].base, stride=vl, length=vl)
             assert L.nkv_group_tree_dev(grp.h, (_lib.NkvTable * g)(*bad), n, None, None) == _lib.NKV_ERR_INVALID
+            # the refused call left no tree behind -- fetch refuses
+            # instead of reading the previous tree's buffers with a new plan
+            assert L.nkv_group_tree_fetch(grp.h, _lib.p8(nodes), _lib.p8(img)) == _lib.NKV_ERR_INVALID
+        # a good split, then a refused one with a larger n, then fetch
+        _lib.check(L.nkv_group_tree_dev(grp.h, arr, n, None, _lib.p8(root)))
+        assert L.nkv_group_tree_dev(grp.h, arr, 4 * n + 3, None, None) == _lib.NKV_ERR_INVALID
+        assert L.nkv_group_tree_fetch(grp.h, _lib.p8(nodes), _lib.p8(img)) == _lib.NKV_ERR_INVALID
+        # a member's root buffer on another device (host memory) is refused
+        droot_bad = (ctypes.c_void_p * g)(*([0] * (g - 1) + [root.ctypes.data]))
+        assert L.nkv_group_tree_dev(grp.h, arr, n, droot_bad, None) == _lib.NKV_ERR_INVALID
 
 
 def values_parts(_lib, g, n, base, off, ln):
@@ -510,12 +522,9 @@ def test_pruned_variants_are_refused(nkv):
         assert L.nkv_ctx_set_option(ctx.h, _lib.NKV_OPT_LEAF_LOAD, v) == _lib.NKV_ERR_INVALID
     for v in (4, 11):
         assert L.nkv_ctx_set_option(ctx.h, _lib.NKV_OPT_LEAF_LOAD, v) == _lib.NKV_OK
-    for v in (0, 1, 2):
-        assert L.nkv_ctx_set_option(ctx.h, _lib.NKV_OPT_DEEP_PREFETCH, v) == _lib.NKV_ERR_INVALID
-    assert L.nkv_ctx_set_option(ctx.h, _lib.NKV_OPT_DEEP_PREFETCH, 3) == _lib.NKV_OK
-    for v in (2, 3, 4, 12, 14):
-        assert L.nkv_ctx_set_option(ctx.h, _lib.NKV_OPT_QUEUE_RING, v) == _lib.NKV_ERR_INVALID
-    assert L.nkv_ctx_set_option(ctx.h, _lib.NKV_OPT_QUEUE_RING, 13) == _lib.NKV_OK
+    for key in (3, 9):  # the retired DEEP_PREFETCH and QUEUE_RING keys (round 4)
+        for v in (0, 3, 13):
+            assert L.nkv_ctx_set_option(ctx.h, key, v) == _lib.NKV_ERR_INVALID
     for v in (0, 4, 5):
         assert L.nkv_ctx_set_option(ctx.h, _lib.NKV_OPT_QUEUE_WAVES, v) == _lib.NKV_ERR_INVALID
     assert L.nkv_ctx_set_option(ctx.h, _lib.NKV_OPT_QUEUE_WAVES, 3) == _lib.NKV_OK

@@ -10,16 +10,19 @@
 // memory (the memtable), one contiguous buffer of n x vlen bytes.  Every cycle
 // is a fresh flush into a fresh file; cycle 0 also allocates the pinned arena,
 // later cycles reuse it (steady state).  One JSON line per cycle:
-//   newleaf_ms    the NewLeaf loop: arena copies (and, streaming on, the DMA of
-//                 every settled 32 MiB chunk starts inside it)
-//   new_call_ms   New's device call (nkv_tree_from_values): the rest of the
-//                 values to HBM, leaf + tree kernels, every digest back
+//   newleaf_ms    the NewLeaf loop: arena places recorded and the copies queued
+//                 for the copy threads (COPY_THREADS = 0: the copies themselves);
+//                 streaming on, the DMA of every settled 32 MiB chunk starts
+//                 inside it
+//   new_call_ms   New's device call: the copy threads' last jobs, the rest of
+//                 the values to HBM, leaf + tree kernels, every digest back
 //     upload_ms / kernels_ms / download_ms   its HIP-event split
 //   materialize_ms  New's pointer tree (2n - 1 nodes + pads)
 //   root_ms       Root.String()
 //   walk_ms / write_ms   Serialize: BFS walk of the live tree, file write
 //
-// Usage: api_flush N VLEN CYCLES DIR [STREAMING=1] [SEED] [NONTEMPORAL=1]
+// Usage: api_flush N VLEN CYCLES DIR [STREAMING=1] [SEED] [NONTEMPORAL=1] [COPY_THREADS=-1]
+// (COPY_THREADS -1: the mirror's default, min(16, cores) or NKV_COPY_THREADS)
 #include <fcntl.h>
 #include <unistd.h>
 
@@ -65,11 +68,13 @@ int main(int argc, char** argv) {
     const bool streaming = argc > 5 ? std::atoi(argv[5]) != 0 : true;
     const uint64_t seed = argc > 6 ? std::strtoull(argv[6], nullptr, 0) : 0x6E616B65ull;
     const bool nontemporal = argc > 7 ? std::atoi(argv[7]) != 0 : true;
+    const int copy_threads = argc > 8 ? std::atoi(argv[8]) : -1;
     std::vector<uint8_t> memtable(n * vlen);
     fill(memtable.data(), memtable.size(), seed, 16);
     Session& S = Session::Default();
     S.SetStreaming(streaming);
     S.SetNonTemporal(nontemporal);
+    if (copy_threads >= 0) S.SetCopyThreads(copy_threads);
     check(nkv_ctx_set_timing(S.ctx(), NKV_TIMING_EVENTS), "timing");
     for (int cyc = 0; cyc < cycles; ++cyc) {
         const std::string fname = dir + "/api_flush-1-" + std::to_string(cyc) + "-metadata.db";
@@ -96,12 +101,13 @@ int main(int argc, char** argv) {
         if (nkv_ctx_last_host_timing(S.ctx(), &up, &ker, &down) != NKV_OK) up = ker = down = -1;
         const double total = ms(t0, t5);
         std::printf(
-            "{\"cycle\": %d, \"n\": %llu, \"value_bytes\": %llu, \"streaming\": %d, \"nontemporal\": %d, \"gib_s\": %.3f, "
+            "{\"cycle\": %d, \"n\": %llu, \"value_bytes\": %llu, \"streaming\": %d, \"nontemporal\": %d, "
+            "\"copy_threads\": %d, \"gib_s\": %.3f, "
             "\"total_ms\": %.3f, \"newleaf_ms\": %.3f, \"new_call_ms\": %.3f, \"upload_ms\": %.3f, "
             "\"kernels_ms\": %.3f, \"download_ms\": %.3f, \"materialize_ms\": %.3f, \"root_ms\": %.3f, "
             "\"walk_ms\": %.3f, \"write_ms\": %.3f, \"image_bytes\": %zu, \"arena_allocs\": %llu, "
             "\"root\": \"%s\"}\n",
-            cyc, (unsigned long long)n, (unsigned long long)vlen, int(streaming), int(nontemporal),
+            cyc, (unsigned long long)n, (unsigned long long)vlen, int(streaming), int(nontemporal), S.CopyThreads(),
             double(n * vlen) / (total * 1e-3) / double(1ull << 30), total, ms(t0, t1),
             tree->LastNewTiming().call_ms, up, ker, down, tree->LastNewTiming().materialize_ms, ms(t2, t3),
             ms(t3, t4), ms(t4, t5), img.size(), (unsigned long long)S.arena_allocs(), root.c_str());

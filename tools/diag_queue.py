@@ -27,12 +27,10 @@ def main():
     ctx = _lib.Context(0)
     ctx.set_stream(torch.cuda.current_stream().cuda_stream)
     deep = int(os.environ.get("DEEP", "3"))
-    ctx.set_option(_lib.NKV_OPT_DEEP_PREFETCH, deep)
     qwaves = int(os.environ.get("QWAVES", "4"))
     ctx.set_option(_lib.NKV_OPT_QUEUE_WAVES, qwaves)
     ctx.set_option(_lib.NKV_OPT_QUEUE_SPLIT, int(os.environ.get("QSPLIT", "32")))
     ring = int(os.environ.get("RING", "13"))
-    ctx.set_option(_lib.NKV_OPT_QUEUE_RING, ring)
     ctx.set_option(_lib.NKV_OPT_BUCKET, 1)
     lens_h, off_h = bench.mixed_lengths(4 << 30, bench.SEED_MIXED)
     n = len(lens_h)
