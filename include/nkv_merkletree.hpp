@@ -203,9 +203,25 @@ class Session {
     // plain store) only costs memory bandwidth.  Fence() orders them before
     // any DMA that reads the arena.
     static constexpr size_t kStreamCopy = 256;
-    std::pair<std::shared_ptr<Batch>, uint64_t> AddLeaf(const uint8_t* data, size_t n) {
+    // defer = false: copied on the caller's thread now (for values the caller
+    // may free at once: NewLeaf's std::string / std::vector forms, often
+    // temporaries in C++, where Go's garbage collector keeps a slice alive)
+    // Returns the value's index in the current batch (batch()).
+    uint64_t AddLeaf(const uint8_t* data, size_t n, bool defer = true) {
         if (!batch_ || batch_->resolved) {
-            batch_ = std::make_shared<Batch>();
+            // a sealed batch nobody else holds is reused: its vectors keep their
+            // capacity (sized for the last flush, no regrowth per flush)
+            const size_t hint = batch_ ? batch_->off.size() : 0;
+            if (batch_ && batch_.use_count() == 1) {
+                batch_->off.clear();
+                batch_->len.clear();
+                batch_->digests.clear();
+                batch_->resolved = false;
+            } else {
+                batch_ = std::make_shared<Batch>();
+                batch_->off.reserve(hint);
+                batch_->len.reserve(hint);
+            }
             batch_->epoch = ++epoch_;
             Settle();
             used_ = 0;
@@ -217,10 +233,11 @@ class Session {
         batch_->off.push_back(at);
         batch_->len.push_back(n);
         used_ = at + n;
-        if (Pool()) {
+        if (defer && Pool()) {
             if (!job_) {
                 job_.reset(new CopyPool::Job());
                 job_->base = static_cast<uint8_t*>(arena_);
+                job_->tasks.reserve(kJobBytes / 4096 + 1);
             }
             if (n) job_->tasks.push_back({at, data, n});
             job_bytes_ += n;
@@ -230,6 +247,7 @@ class Session {
                     const uint64_t s = pool_->Settled();
                     if (s >= streamed_ + kStreamChunk) {
                         streamed_ = s - s % kStreamChunk;
+                        Fence();  // values this thread copied itself (the std::string forms)
                         check(nkv_host_stream(ctx_, arena_, streamed_), "nkv_host_stream");
                     }
                 }
@@ -237,14 +255,15 @@ class Session {
         } else {
             if (nt_) CopyIn(static_cast<uint8_t*>(arena_) + at, data, n);
             else if (n) std::memcpy(static_cast<uint8_t*>(arena_) + at, data, n);
-            if (stream_ && used_ >= streamed_ + kStreamChunk) {
+            if (!pool_ && stream_ && used_ >= streamed_ + kStreamChunk) {
                 streamed_ = used_ - used_ % kStreamChunk;
                 Fence();
                 check(nkv_host_stream(ctx_, arena_, streamed_), "nkv_host_stream");
             }
         }
-        return {batch_, batch_->off.size() - 1};
+        return batch_->off.size() - 1;
     }
+    const std::shared_ptr<Batch>& batch() const { return batch_; }
     // Every queued arena copy done (New and every other reader of the arena
     // call this first).
     void Settle() {
@@ -322,6 +341,16 @@ class Session {
     // (no per-node allocation once a flush of that size has run)
     std::vector<MerkleNode>* TakeNodes();
     void GiveNodes(std::vector<MerkleNode>* v);
+    // New's level arrays, recycled the same way (no 20 * (2n - 1)-byte zero
+    // fill and page faults per flush)
+    std::vector<uint8_t> TakeLevels() {
+        std::vector<uint8_t> v;
+        v.swap(spare_levels_);
+        return v;
+    }
+    void GiveLevels(std::vector<uint8_t>&& v) {
+        if (v.capacity() > spare_levels_.capacity()) spare_levels_.swap(v);
+    }
 
    private:
     CopyPool* Pool() {
@@ -368,6 +397,7 @@ class Session {
     uint64_t job_bytes_ = 0;
     int copy_threads_ = -1;  // -1: not chosen yet (Pool())
     std::vector<std::vector<MerkleNode>*> spare_;
+    std::vector<uint8_t> spare_levels_;
 };
 
 struct MerkleNode {  // merklenode.go:15-19
@@ -375,15 +405,19 @@ struct MerkleNode {  // merklenode.go:15-19
     MerkleNode* Left = nullptr;
     MerkleNode* Right = nullptr;
 
-    // deferred NewLeaf digest (resolved by New or Resolve)
+    // deferred NewLeaf digest (resolved by New or Resolve).  New marks its
+    // leaves resolved with pend_idx = kResolved instead of dropping pend (no
+    // atomic reference-count update per leaf on New's path).
+    static constexpr uint64_t kResolved = ~uint64_t(0);
     std::shared_ptr<Session::Batch> pend;
     uint64_t pend_idx = 0;
+    bool pending() const { return pend && pend_idx != kResolved; }
 
     MerkleNode() = default;
     explicit MerkleNode(std::vector<uint8_t> d) : Data(std::move(d)) {}
 
     const std::vector<uint8_t>& Resolve() {
-        if (pend) {
+        if (pending()) {
             Session::Default().ResolveBatch(*pend);
             Data.assign(pend->digests.begin() + 20 * pend_idx, pend->digests.begin() + 20 * pend_idx + 20);
             pend.reset();
@@ -428,17 +462,24 @@ struct MerkleNode {  // merklenode.go:15-19
     }
 };
 
-inline MerkleNode NewLeaf(const uint8_t* data, size_t n) {  // merklenode.go:27-34
+// merklenode.go:27-34.  The pointer form defers the copy to the session's copy
+// threads: data[0, n) must stay unchanged until New returns (the flush and
+// compaction callers hand over values they never mutate).  The std::vector /
+// std::string forms copy at once (their argument may be a temporary).
+// Data stays empty until the batch is resolved (New, or Resolve / String /
+// Serialize / Validate on the node): one allocation fewer on the caller's
+// thread per value; New fills the leaves' Data on several threads.
+inline MerkleNode NewLeafAt(const uint8_t* data, size_t n, bool defer) {
     MerkleNode m;
-    auto r = Session::Default().AddLeaf(data, n);
-    m.pend = r.first;
-    m.pend_idx = r.second;
-    m.Data.assign(20, 0);
+    Session& S = Session::Default();
+    m.pend_idx = S.AddLeaf(data, n, defer);
+    m.pend = S.batch();
     return m;
 }
-inline MerkleNode NewLeaf(const std::vector<uint8_t>& v) { return NewLeaf(v.data(), v.size()); }
+inline MerkleNode NewLeaf(const uint8_t* data, size_t n) { return NewLeafAt(data, n, true); }
+inline MerkleNode NewLeaf(const std::vector<uint8_t>& v) { return NewLeafAt(v.data(), v.size(), false); }
 inline MerkleNode NewLeaf(const std::string& v) {
-    return NewLeaf(reinterpret_cast<const uint8_t*>(v.data()), v.size());
+    return NewLeafAt(reinterpret_cast<const uint8_t*>(v.data()), v.size(), false);
 }
 
 inline Session::~Session() {
@@ -471,7 +512,10 @@ class MerkleTree {  // merkletree.go:13-15
     MerkleNode* Root = nullptr;
 
     MerkleTree() = default;
-    ~MerkleTree() { Session::Default().GiveNodes(inner_); }
+    ~MerkleTree() {
+        Session::Default().GiveNodes(inner_);
+        Session::Default().GiveLevels(std::move(levels_));
+    }
     MerkleTree(const MerkleTree&) = delete;
     MerkleTree& operator=(const MerkleTree&) = delete;
 
@@ -481,19 +525,32 @@ class MerkleTree {  // merkletree.go:13-15
         check(nkv_write_file(fname.c_str(), img.data(), img.size()), ("Serialize(" + fname + ")").c_str());
     }
 
+    // The queue walk (merkletree.go:75-89) in two passes: the BFS order and the
+    // image size, then every node's bytes (merklenode.go:37-63) written in place
+    // -- no per-node vector growth.
     std::vector<uint8_t> SerializeBytes() {
-        std::vector<uint8_t> w;
         std::vector<MerkleNode*> q{Root};  // BFS queue: q[head..) still to visit
         const size_t owned = leaves_.size() + (inner_ ? inner_->size() : 0);
-        if (owned) {
-            q.reserve(owned);
-            w.reserve(21 * owned);
-        }
+        if (owned) q.reserve(owned);
+        size_t bytes = 0;
         for (size_t head = 0; head < q.size(); ++head) {
             MerkleNode* n = q[head];
             if (n->Left) q.push_back(n->Left);
             if (n->Right) q.push_back(n->Right);
-            n->Serialize(w);
+            const size_t d = n->Resolve().size();
+            bytes += d ? 1 + d : 1;
+        }
+        std::vector<uint8_t> w(bytes);
+        uint8_t* o = w.data();
+        for (MerkleNode* n : q) {
+            const size_t d = n->Data.size();
+            if (!d) {
+                *o++ = MERKLE_NODE_EMPTY;
+            } else {
+                *o++ = 0;
+                std::memcpy(o, n->Data.data(), d);
+                o += d;
+            }
         }
         return w;
     }
@@ -576,7 +633,7 @@ class MerkleTree {  // merkletree.go:13-15
     static bool NewShapedLeaves(MerkleNode* root, uint64_t n, std::vector<MerkleNode*>* out) {
         const int top = nkv_num_levels(n) - 1;
         std::vector<MerkleNode*> cur{root};
-        auto pad_ok = [](const MerkleNode* p) { return !p->Left && !p->Right && p->Data.empty() && !p->pend; };
+        auto pad_ok = [](const MerkleNode* p) { return !p->Left && !p->Right && p->Data.empty() && !p->pending(); };
         for (int L = top; L >= 0; --L) {
             const uint64_t real = nkv_level_count(n, L);
             const bool pad = (real & 1) && L < top;
@@ -679,21 +736,24 @@ inline std::unique_ptr<MerkleTree> New(std::vector<MerkleNode> level, std::strin
     nkv_ctx* ctx = Session::Default().ctx();
     std::unique_ptr<MerkleTree> t(new MerkleTree());
     const uint64_t total = nkv_total_nodes(n);
-    t->levels_.assign(20 * total, 0);
+    Session& S = Session::Default();
+    t->levels_ = S.TakeLevels();
+    t->levels_.resize(20 * total);  // every byte is written below
     uint8_t* nodes = t->levels_.data();
 
     // the flush / compaction pattern: n NewLeaf calls of one batch, in order
-    const auto& b0 = level[0].pend;
-    bool same_batch = b0 && !b0->resolved && b0->off.size() == n;
+    const std::shared_ptr<Session::Batch> b0 = level[0].pend;
+    bool same_batch = level[0].pending() && !b0->resolved && b0->off.size() == n;
     for (uint64_t i = 0; same_batch && i < n; ++i)
         same_batch = level[i].pend == b0 && level[i].pend_idx == i && !level[i].Left && !level[i].Right;
     if (same_batch) {
-        Session::Default().Settle();
+        S.Settle();
         Session::Fence();
-        check(nkv_tree_from_values(ctx, Session::Default().arena(), b0->off.data(), b0->len.data(), n,
-                                   nullptr, nodes, nullptr),
+        check(nkv_tree_from_values(ctx, S.arena(), b0->off.data(), b0->len.data(), n, nullptr, nodes, nullptr),
               "New");
-        b0->digests.assign(nodes, nodes + 20 * n);
+        // other copies of these leaves (the caller kept the slice) resolve later
+        // from the batch; New's own leaves are filled below
+        if (b0.use_count() > 2 + int64_t(n)) b0->digests.assign(nodes, nodes + 20 * n);
         b0->resolved = true;
     } else {
         bool all20 = true;
@@ -717,49 +777,71 @@ inline std::unique_ptr<MerkleTree> New(std::vector<MerkleNode> level, std::strin
         }
     }
     const auto c1 = clk::now();
-    // materialize the pointer tree: the given leaves (Go copies `l :=
-    // level[i]`: `level` is New's own copy, kept as the tree's leaves), then
-    // parents level by level with the empty pad node (merkletree.go:32-34), in
-    // node storage recycled from destroyed trees: no allocation per node
+    // Materialize the pointer tree: the given leaves (Go copies `l := level[i]`:
+    // `level` is New's own copy, kept as the tree's leaves), then the parents of
+    // every level with the empty pad node (merkletree.go:32-34), in node storage
+    // recycled from destroyed trees.  Every node's place is known up front, so
+    // the fill runs on several threads.
     t->leaves_ = std::move(level);
     auto& leaves = t->leaves_;
-    if (same_batch) {
-        for (uint64_t i = 0; i < n; ++i) {
-            leaves[i].Data.assign(nodes + 20 * i, nodes + 20 * i + 20);
-            leaves[i].pend.reset();
-        }
-    }
     t->n_ = n;
     const int lv = nkv_num_levels(n);
-    uint64_t inner = nkv_total_nodes(n) - n;
-    for (int L = 0; L + 1 < lv; ++L) inner += nkv_level_count(n, L) & 1;  // pads
-    t->inner_ = Session::Default().TakeNodes();
+    // pool layout: [level 0's pad], then for L = 1 .. top: level L, [level L's
+    // pad] (a level below the top with an odd count has one)
+    std::vector<uint64_t> lbase(lv + 1, 0), lpad(lv, ~uint64_t(0)), lcnt(lv), lstart(lv);
+    for (int L = 0; L < lv; ++L) {
+        lcnt[L] = nkv_level_count(n, L);
+        lstart[L] = nkv_level_start(n, L);
+    }
+    uint64_t inner = 0;
+    if (lcnt[0] & 1) lpad[0] = inner++;
+    for (int L = 1; L < lv; ++L) {
+        lbase[L] = inner;
+        inner += lcnt[L];
+        if (L + 1 < lv && (lcnt[L] & 1)) lpad[L] = inner++;
+    }
+    lbase[lv] = inner;
+    t->inner_ = S.TakeNodes();
     std::vector<MerkleNode>& pool = *t->inner_;
     pool.resize(inner);
-    size_t k = 0;
-    std::vector<MerkleNode*> below;
-    below.reserve(n + 1);
-    for (auto& x : leaves) below.push_back(&x);
-    for (int L = 1; L < lv; ++L) {
-        if (below.size() % 2) {  // MerkleNode{Data: []byte{}}
-            MerkleNode& p = pool[k++];
-            p.Data.clear();
-            p.Left = p.Right = nullptr;
-            p.pend.reset();
-            below.push_back(&p);
+    auto node_at = [&](int L, uint64_t j) -> MerkleNode* {
+        if (j == lcnt[L]) return &pool[lpad[L]];
+        return L == 0 ? &leaves[j] : &pool[lbase[L] + j];
+    };
+    auto fill = [&](uint64_t lo, uint64_t hi) {  // items [lo, hi): leaves, then pool slots
+        for (uint64_t x = lo; x < hi && x < n; ++x) {
+            if (same_batch) {
+                leaves[x].Data.assign(nodes + 20 * x, nodes + 20 * x + 20);
+                leaves[x].pend_idx = MerkleNode::kResolved;
+            }
         }
-        const uint64_t s = nkv_level_start(n, L), c = nkv_level_count(n, L);
-        for (uint64_t i = 0; i < c; ++i) {
-            MerkleNode& m = pool[k++];
-            m.Data.assign(nodes + 20 * (s + i), nodes + 20 * (s + i) + 20);
-            m.Left = below[2 * i];
-            m.Right = below[2 * i + 1];
-            m.pend.reset();
-            below[i] = &m;  // below[2i], below[2i+1] are read before below[i] is written
+        int L = 1;
+        for (uint64_t x = std::max(lo, n); x < hi; ++x) {
+            const uint64_t k = x - n;
+            while (k >= lbase[L + 1]) ++L;
+            MerkleNode& m = pool[k];
+            const uint64_t j = k - lbase[L];
+            if (k < lbase[L] || j >= lcnt[L]) {  // a pad: MerkleNode{Data: []byte{}}
+                m.Data.clear();
+                m.Left = m.Right = nullptr;
+            } else {
+                const uint64_t i = lstart[L] + j;
+                m.Data.assign(nodes + 20 * i, nodes + 20 * i + 20);
+                m.Left = node_at(L - 1, 2 * j);
+                m.Right = node_at(L - 1, 2 * j + 1);
+            }
+            if (m.pend) m.pend.reset();
+            m.pend_idx = 0;
         }
-        below.resize(c);
-    }
-    t->Root = below[0];
+    };
+    const uint64_t items = n + inner;
+    const int nt = items >= (uint64_t(1) << 16) ? int(std::min<unsigned>(8, std::max(1u, std::thread::hardware_concurrency()))) : 1;
+    std::vector<std::thread> th;
+    for (int k = 1; k < nt; ++k) th.emplace_back(fill, items * k / nt, items * (k + 1) / nt);
+    fill(0, items / nt);
+    for (auto& x : th) x.join();
+    MerkleNode* root = lv == 1 ? &leaves[0] : &pool[lbase[lv - 1]];
+    t->Root = root;
     t->timing_.call_ms = std::chrono::duration<double, std::milli>(c1 - c0).count();
     t->timing_.materialize_ms = std::chrono::duration<double, std::milli>(clk::now() - c1).count();
     return t;

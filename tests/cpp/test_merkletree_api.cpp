@@ -60,7 +60,7 @@ int main(int argc, char** argv) {
         std::printf("empty_err %s\n", err.c_str());
     }
     // the flush pattern: NewLeaf per value, then New, then Serialize
-    for (uint64_t n : {1ull, 2ull, 3ull, 255ull, 256ull, 257ull, 1000ull, 1025ull}) {
+    for (uint64_t n : {1ull, 2ull, 3ull, 255ull, 256ull, 257ull, 1000ull, 1025ull, 70001ull}) {
         const size_t vlen = n > 300 ? 64 : 100;
         auto data = splitmix64_bytes(n * vlen, 0x6E616B65ull + n);
         std::vector<MerkleNode> leaves;
@@ -72,6 +72,11 @@ int main(int argc, char** argv) {
         std::printf("tree%llu_bfs_head %s\n", (unsigned long long)n,
                     hex(std::vector<uint8_t>(img.begin(), img.begin() + std::min<size_t>(64, img.size()))).c_str());
         std::printf("tree%llu_validate %d\n", (unsigned long long)n, int(t->Validate()));
+        if (n == 70001) {  // past the threshold of New's multi-threaded materialization
+            FILE* f = std::fopen((dir + "/tree70001.img").c_str(), "wb");
+            std::fwrite(img.data(), 1, img.size(), f);
+            std::fclose(f);
+        }
         if (n == 1000) {
             // corrupt one leaf of the materialized tree: Validate must fail
             MerkleNode* leaf = t->Root;
@@ -132,17 +137,33 @@ int main(int argc, char** argv) {
     {
         auto& S = nkv::merkletree::Session::Default();
         const uint64_t n = 20000;
-        for (size_t vlen : {size_t(4096), size_t(1001)}) {
-            auto data = splitmix64_bytes(n * vlen, 0x5EED + vlen);
-            for (int streaming = 1; streaming >= 0; --streaming) {
-                S.SetStreaming(streaming != 0);
-                std::vector<MerkleNode> leaves;
-                for (uint64_t i = 0; i < n; ++i) leaves.push_back(NewLeaf(data.data() + i * vlen, vlen));
-                auto t = New(leaves);
-                std::printf("big%zu_s%d_root %s\n", vlen, streaming, t->Root->String().c_str());
+        std::printf("default_copy_threads %d\n", S.CopyThreads());
+        // copy threads: the default pool, the caller's thread (0), a 3-thread
+        // pool; the first 4096-byte flush also grows the arena mid-loop with
+        // copies queued (Reserve settles them first)
+        for (int threads : {-1, 0, 3}) {
+            if (threads >= 0) S.SetCopyThreads(threads);
+            for (size_t vlen : {size_t(4096), size_t(1001)}) {
+                auto data = splitmix64_bytes(n * vlen, 0x5EED + vlen);
+                for (int streaming = 1; streaming >= 0; --streaming) {
+                    S.SetStreaming(streaming != 0);
+                    std::vector<MerkleNode> leaves;
+                    for (uint64_t i = 0; i < n; ++i) leaves.push_back(NewLeaf(data.data() + i * vlen, vlen));
+                    auto t = New(leaves);
+                    std::printf("big%zu_t%d_s%d_root %s\n", vlen, threads, streaming, t->Root->String().c_str());
+                }
+                S.SetStreaming(true);
             }
-            S.SetStreaming(true);
+            // ragged values 0..4999 bytes (jobs cut mid-run, empty values) and a
+            // leaf resolved before New (String() settles the pool first)
+            auto data = splitmix64_bytes(uint64_t(5000) * 9000, 0xBADu);
+            std::vector<MerkleNode> leaves;
+            for (uint64_t i = 0; i < 9000; ++i) leaves.push_back(NewLeaf(data.data() + i * 5000, (i * 37) % 5000));
+            std::printf("ragged_t%d_leaf77 %s\n", threads, leaves[77].String().c_str());
+            auto t = New(leaves);
+            std::printf("ragged_t%d_root %s\n", threads, t->Root->String().c_str());
         }
+        S.SetCopyThreads(16);
     }
     // CompactRoots: five Data tables (record.go:191-199) over a group of one GPU
     // (RCCL) and of device 0 twice (copy transport), one host thread per member

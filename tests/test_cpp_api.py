@@ -62,6 +62,12 @@ def test_cpp_mirror_on_gpu(tmp_path, oracle):
         assert kv[f"tree{n}_bfs_head"] == c["bfs_head_hex"]
         assert kv[f"tree{n}_validate"] == "1"
     assert kv["tree1000_corrupt_validate"] == "0"
+    # a tree New materializes on several threads (70001 leaves of 64 bytes)
+    data = oracle.splitmix64_bytes(70001 * 64, 0x6E616B65 + 70001)
+    want = oracle.tree_from_digests(oracle.leaf_hashes_strided(data, 64, 64, 70001, threads=8))
+    assert kv["tree70001_root"] == want[-1].tobytes().hex() and kv["tree70001_validate"] == "1"
+    img = open(os.path.join(str(tmp_path), "tree70001.img"), "rb").read()
+    assert img == oracle.bfs_image(want, 70001) and int(kv["tree70001_bfs_len"]) == len(img)
     vals = [bytes([ord("a") + i]) * (7 * i) for i in range(10)]
     assert kv["early_leaf3"] == hashlib.sha1(vals[3]).hexdigest()
     want = oracle.tree_from_digests(np.frombuffer(b"".join(hashlib.sha1(v).digest() for v in vals), np.uint8))
@@ -88,10 +94,20 @@ def test_cpp_mirror_on_gpu(tmp_path, oracle):
     t.Root.Right.Data = bytes([d[0] ^ 0xFF]) + bytes(d[1:])
     assert kv["mut_img"] == t.SerializeBytes().hex()
     # flushes past the 32 MiB stream chunk, streamed or not, aligned or odd value sizes
+    # -- with NewLeaf's copies on the default pool, on the caller's thread, on 3 threads
+    assert int(kv["default_copy_threads"]) >= 1
     for vlen in (4096, 1001):
         data = oracle.splitmix64_bytes(20000 * vlen, 0x5EED + vlen)
         want = oracle.tree_from_digests(oracle.leaf_hashes_strided(data, vlen, vlen, 20000, threads=8))
-        assert kv[f"big{vlen}_s1_root"] == kv[f"big{vlen}_s0_root"] == want[-1].tobytes().hex()
+        for t in (-1, 0, 3):
+            assert kv[f"big{vlen}_t{t}_s1_root"] == kv[f"big{vlen}_t{t}_s0_root"] == want[-1].tobytes().hex()
+    data = oracle.splitmix64_bytes(5000 * 9000, 0xBAD)
+    off = np.arange(9000, dtype=np.uint64) * 5000
+    ln = (np.arange(9000, dtype=np.uint64) * 37) % 5000
+    want = oracle.tree_from_digests(oracle.leaf_hashes(data, off, ln, threads=8))
+    for t in (-1, 0, 3):
+        assert kv[f"ragged_t{t}_root"] == want[-1].tobytes().hex()
+        assert kv[f"ragged_t{t}_leaf77"] == want[77].tobytes().hex()
     # CompactRoots over a group of one GPU (RCCL) and of device 0 twice (copy)
     from nakevaleng_amd import record
     assert kv["group1_transport"] == "1"
