@@ -341,7 +341,7 @@ int tree_from_device_values(nkv_ctx* c, const uint8_t* base, const uint64_t* off
     TRY(mark(c, 0));
     TRY(leaf_level(c, base, off, len, n, aligned, nodes, plan, g));
     TRY(mark(c, 1));
-    HIPTRY(launch_reduce(nodes, n, 0, levels_of(n) - 1, c->stream, Gate{}, ctx_ticket(c)));
+    HIPTRY(launch_reduce(nodes, n, 0, levels_of(n) - 1, c->stream));
     return mark(c, 2);
 }
 
@@ -384,7 +384,7 @@ int records_tree(nkv_ctx* c, const uint8_t* stream, uint64_t stream_len, const u
                        false, CopyWords{flags + 2, err, 1}));
     }
     TRY(mark(c, 1));
-    HIPTRY(launch_reduce(nodes, n, 0, levels_of(n) - 1, c->stream, Gate{}, ctx_ticket(c)));
+    HIPTRY(launch_reduce(nodes, n, 0, levels_of(n) - 1, c->stream));
     return mark(c, 2);
 }
 
@@ -434,8 +434,6 @@ int nkv_ctx_create(int device, nkv_ctx** out) try {
     if (rc == NKV_OK) rc = st(hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking));
     if (rc == NKV_OK) rc = st(hipHostMalloc(reinterpret_cast<void**>(&c->h_small), 64, hipHostMallocDefault));
     if (rc == NKV_OK) rc = grow(c->d_flags, 4 * 2 * kPassFlagWords);
-    if (rc == NKV_OK) rc = grow(c->d_ticket, 16);
-    if (rc == NKV_OK) rc = st(hipMemset(c->d_ticket.p, 0, 16));
     if (rc == NKV_OK) {  // both pass-flag sets start reset (each records call resets the other)
         uint32_t init[2 * kPassFlagWords] = {};
         for (uint32_t k = 0; k < 2; ++k) init[kPassFlagWords * k + 6] = init[kPassFlagWords * k + 7] = ~0u;
@@ -463,7 +461,7 @@ void nkv_ctx_destroy(nkv_ctx* c) {
     (void)hipSetDevice(c->device);
     for (DevBuf* b : {&c->d_data, &c->d_off, &c->d_len, &c->d_nodes, &c->d_img, &c->d_tmp,
                       &c->d_err, &c->d_aux, &c->d_keys, &c->d_perm, &c->d_stmp, &c->d_queue, &c->d_stats,
-                      &c->d_range, &c->d_part, &c->d_tmp2, &c->d_flags, &c->d_clk, &c->d_ticket})
+                      &c->d_range, &c->d_part, &c->d_tmp2, &c->d_flags, &c->d_clk})
         if (b->p) (void)hipFree(b->p);
     for (nkv_ctx::Pinned* blk : c->pinned) {
         if (blk->d_arena.p) (void)hipFree(blk->d_arena.p);
@@ -746,7 +744,7 @@ int nkv_tree_build(nkv_ctx* c, const uint8_t* leaf20, uint64_t n, uint8_t* root2
     TRY(grow(c->d_nodes, 20 * total_of(n)));
     uint8_t* nodes = static_cast<uint8_t*>(c->d_nodes.p);
     HIPTRY(c->stage.upload(leaf20, 20 * n, nodes, c->stream));
-    HIPTRY(launch_reduce(nodes, n, 0, levels_of(n) - 1, c->stream, Gate{}, ctx_ticket(c)));
+    HIPTRY(launch_reduce(nodes, n, 0, levels_of(n) - 1, c->stream));
     return finish_tree(c, nodes, n, root20, nodes_out, img_out);
 } NKV_CATCH
 
@@ -813,7 +811,7 @@ int nkv_tree_generic(nkv_ctx* c, const uint8_t* data, const uint64_t* off, const
     uint8_t* up = static_cast<uint8_t*>(c->d_nodes.p);
     TRY(leaf_level(c, d_base, static_cast<const uint64_t*>(c->d_off.p), static_cast<const uint64_t*>(c->d_len.p), n1,
                    aligned, up, mlen.data()));
-    if (n1 > 1) HIPTRY(launch_reduce(up, n1, 0, levels_of(n1) - 1, c->stream, Gate{}, ctx_ticket(c)));
+    if (n1 > 1) HIPTRY(launch_reduce(up, n1, 0, levels_of(n1) - 1, c->stream));
     if (upper_out) HIPTRY(c->stage.download(upper_out, up, 20 * up_total, c->stream));
     if (root20)
         HIPTRY(hipMemcpyAsync(root20, up + 20 * (up_total - 1), 20, hipMemcpyDeviceToHost,
@@ -867,7 +865,7 @@ int nkv_tree_validate(nkv_ctx* c, const uint8_t* leaf_data, const uint64_t* off,
         uint8_t* nodes = static_cast<uint8_t*>(c->d_nodes.p);
         const Segments seg{leaf_data, off, len, dst, n};
         HIPTRY(c->stage.upload(seg, NKV_DIGEST_SIZE * n, nodes, c->stream));
-        HIPTRY(launch_reduce(nodes, n, 0, levels_of(n) - 1, c->stream, Gate{}, ctx_ticket(c)));
+        HIPTRY(launch_reduce(nodes, n, 0, levels_of(n) - 1, c->stream));
         HIPTRY(hipMemcpyAsync(c->h_small, nodes + NKV_DIGEST_SIZE * (total_of(n) - 1), NKV_DIGEST_SIZE,
                               hipMemcpyDeviceToHost, c->stream));
         HIPTRY(hipStreamSynchronize(c->stream));
@@ -1036,7 +1034,7 @@ int nkv_tree_reduce_dev(nkv_ctx* c, void* d_nodes, uint64_t n) try {
     if (n > kMaxN) return NKV_ERR_INVALID;
     if (n == 0) return NKV_ERR_EMPTY;
     if (!d_nodes) return NKV_ERR_INVALID;
-    return st(launch_reduce(static_cast<uint8_t*>(d_nodes), n, 0, levels_of(n) - 1, c->stream, Gate{}, ctx_ticket(c)));
+    return st(launch_reduce(static_cast<uint8_t*>(d_nodes), n, 0, levels_of(n) - 1, c->stream));
 } NKV_CATCH
 
 int nkv_tree_from_values_dev(nkv_ctx* c, const void* d_base, const uint64_t* d_off,
@@ -1061,7 +1059,7 @@ int nkv_tree_from_strided_dev(nkv_ctx* c, const void* d_base, uint64_t stride, u
     HIPTRY(launch_leaf_strided(static_cast<const uint8_t*>(d_base), stride, len, n,
                                c->leaf_load, nodes, c->stream));
     TRY(mark(c, 1));
-    HIPTRY(launch_reduce(nodes, n, 0, top, c->stream, Gate{}, ctx_ticket(c)));
+    HIPTRY(launch_reduce(nodes, n, 0, top, c->stream));
     return mark(c, 2);
 } NKV_CATCH
 
@@ -1174,7 +1172,7 @@ int nkv_tree_verify_records_dev(nkv_ctx* c, const void* d_stream, uint64_t strea
                        false, CopyWords{flags + 4, reinterpret_cast<uint32_t*>(stats), 6}));
     }
     TRY(mark(c, 1));
-    HIPTRY(launch_reduce(nodes, n, 0, levels_of(n) - 1, c->stream, Gate{}, ctx_ticket(c)));
+    HIPTRY(launch_reduce(nodes, n, 0, levels_of(n) - 1, c->stream));
     return mark(c, 2);
 } NKV_CATCH
 

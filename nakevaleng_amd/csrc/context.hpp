@@ -138,8 +138,7 @@ struct nkv_ctx {
     hipEvent_t host_ev[2] = {nullptr, nullptr};  // host-buffer call: before the upload, after the download
     bool host_timed = false;
     nkv::DevBuf d_data, d_off, d_len, d_nodes, d_img, d_tmp, d_err, d_aux, d_keys, d_perm, d_stmp, d_queue,
-        d_stats, d_range, d_part, d_tmp2, d_flags, d_clk,
-        d_ticket;  // the tree reduce's last-workgroup ticket (launch_reduce), zero between launches
+        d_stats, d_range, d_part, d_tmp2, d_flags, d_clk;
     int flag_set = 0;  // which of the two pass-flag sets in d_flags the next records call uses
     // the length sort's bucket totals may be non-zero (a sort was cut short):
     // the next sort clears them first (internal.hpp sort_head_words)
@@ -169,9 +168,6 @@ struct nkv_ctx {
 };
 
 namespace nkv {
-
-// the context's reduce ticket (zeroed at nkv_ctx_create; launch_reduce)
-inline uint32_t* ctx_ticket(nkv_ctx* c) { return static_cast<uint32_t*>(c->d_ticket.p); }
 
 int bind(nkv_ctx* c);
 int grow_host(nkv_ctx* c, size_t bytes);

@@ -313,7 +313,7 @@ int split_top(nkv_group* grp, void* const* d_roots, uint8_t* root20) {
         TRY(grow(grp->top[r], 20 * tn));
         uint8_t* top = static_cast<uint8_t*>(grp->top[r].p);
         HIPTRY(hipMemcpyAsync(top, grp->gathered[r].p, 20 * G, hipMemcpyDeviceToDevice, c->stream));
-        if (G > 1) HIPTRY(launch_reduce(top, G, 0, levels_of(G) - 1, c->stream, Gate{}, ctx_ticket(c)));
+        if (G > 1) HIPTRY(launch_reduce(top, G, 0, levels_of(G) - 1, c->stream));
         if (d_roots && d_roots[r])
             HIPTRY(hipMemcpyAsync(d_roots[r], top + 20 * (tn - 1), 20, hipMemcpyDeviceToDevice, c->stream));
     }
@@ -348,7 +348,7 @@ int build_range(nkv_group* grp, int r, const nkv_table& t, bool aligned, const u
     }
     TRY(mark(c, 1));
     // k >= the range's natural top: the levels above it re-hash the lone node
-    HIPTRY(launch_reduce(lv, m, 0, grp->k, c->stream, Gate{}, ctx_ticket(c)));
+    HIPTRY(launch_reduce(lv, m, 0, grp->k, c->stream));
     return mark(c, 2);
 }
 

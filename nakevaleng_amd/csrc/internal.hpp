@@ -33,8 +33,6 @@ struct Gate {
         const bool narrow = hi <= lo + (lo / 16 > 1u ? lo / 16 : 1u);
         return narrow == (pol == 1);
     }
-    // host: no gate (every launch behind it runs)
-    bool always_open() const { return pol == 0; }
 };
 
 // Pass flags of the records entries' deferred plan (k_leaf_records,
@@ -86,11 +84,7 @@ struct QueueInit {
 hipError_t launch_leaf_queue(const uint8_t* base, const uint64_t* off, const uint64_t* len, const uint32_t* perm,
                              uint64_t n, uint32_t* q, uint32_t simds, uint32_t waves_per_simd, uint8_t* nodes,
                              hipStream_t s, Gate gate = Gate{});
-// ticket (nullable): a zeroed device u32 that no other launch uses at the same
-// time (the context's, ctx_ticket): the wide levels' last workgroup then builds
-// the top too (k_reduce_wide) and zeroes it again.
-hipError_t launch_reduce(uint8_t* nodes, uint64_t n, int from_level, int top, hipStream_t s, Gate gate = Gate{},
-                         uint32_t* ticket = nullptr);
+hipError_t launch_reduce(uint8_t* nodes, uint64_t n, int from_level, int top, hipStream_t s, Gate gate = Gate{});
 hipError_t launch_bfs_image(const uint8_t* nodes, const BfsLayout& lay, uint8_t* img,
                             hipStream_t s);
 // err (u32): 1 if any header points outside the stream, else 0; range

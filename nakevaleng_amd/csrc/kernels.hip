@@ -1439,14 +1439,9 @@ __global__ __launch_bounds__(kBlock) void k_reduce2(uint8_t* __restrict__ nodes,
 // level-(j0 + 2) nodes go to LDS, and subtree_reduce<1024> builds ten more
 // levels: jmax = min(j0 + 12, top).  Replaces k_reduce2 + one 1024-slab launch
 // (the slab part is a chain of one compression per level either way).
-// With a ticket (a zeroed u32 the context owns) and jtop > jmax, the workgroup
-// that finishes last also builds levels jmax + 1 .. jtop from the grid's <= 1024
-// level-jmax nodes (round 4, VERDICT r03 item 6: the tree's top without a
-// launch of its own and the gap before it), then zeroes the ticket again.
 __global__ __launch_bounds__(1024) void k_reduce_wide(uint8_t* __restrict__ nodes, uint64_t n, int j0, int jmax,
-                                                      int jtop, uint32_t* __restrict__ ticket, Gate gate) {
+                                                      Gate gate) {
     __shared__ uint32_t lds[5][1024];
-    __shared__ uint32_t s_last;
     if (!gate.open()) return;
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
@@ -1488,41 +1483,6 @@ __global__ __launch_bounds__(1024) void k_reduce_wide(uint8_t* __restrict__ node
 #pragma unroll
     for (int k = 0; k < 5; ++k) lds[k][threadIdx.x] = h[k];
     subtree_reduce<1024>(lds, n, j0 + 2, jmax, uint64_t(blockIdx.x) * 1024, nodes);
-    if (!ticket || jtop <= jmax) return;
-    // The last workgroup to get here builds the top.  Only this workgroup's
-    // level-jmax node (in lds[.][0], thread 0's own write) must reach it: thread
-    // 0 stores it again with agent-scope atomic stores (coherent across the
-    // XCDs' L2s, no L2 write-back as __threadfence would do at the end of every
-    // workgroup), waits for them, then takes its ticket.
-    if (threadIdx.x == 0) {
-#ifdef NKV_FOLD_FENCE
-        __threadfence();
-        const uint32_t last = atomicAdd(ticket, 1u) == gridDim.x - 1u ? 1u : 0u;
-        if (last) __threadfence();
-#else
-        uint32_t* p = reinterpret_cast<uint32_t*>(nodes + 20ull * (lvl_start(n, jmax) + blockIdx.x));
-#pragma unroll
-        for (int k = 0; k < 5; ++k) __hip_atomic_store(p + k, bswap32(lds[k][0]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_s_waitcnt(0);
-        const uint32_t last =
-            __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1u ? 1u : 0u;
-#endif
-        s_last = last;
-    }
-    __syncthreads();
-    if (!s_last) return;
-    if (threadIdx.x == 0) atomicExch(ticket, 0u);  // every workgroup has taken its ticket
-    const uint64_t cnt = lvl_count(n, jmax);  // <= 1024 (launch_reduce)
-    uint32_t t[5] = {0u, 0u, 0u, 0u, 0u};
-    if (threadIdx.x < cnt) {  // other workgroups' nodes: agent-scope loads, past any stale line
-        const uint32_t* p = reinterpret_cast<const uint32_t*>(nodes + 20ull * (lvl_start(n, jmax) + threadIdx.x));
-#pragma unroll
-        for (int k = 0; k < 5; ++k)
-            t[k] = bswap32(__hip_atomic_load(p + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    }
-#pragma unroll
-    for (int k = 0; k < 5; ++k) lds[k][threadIdx.x] = t[k];
-    subtree_reduce<1024>(lds, n, jmax, jtop, 0, nodes);
 }
 
 // ---------------------------------------------------------------------------
@@ -2019,8 +1979,7 @@ hipError_t launch_leaf_queue(const uint8_t* base, const uint64_t* off, const uin
 
 uint64_t queue_words(uint64_t n) { return kQueueHeader + kSimdKeys + (n + 63) / 64; }
 
-hipError_t launch_reduce(uint8_t* nodes, uint64_t n, int from_level, int top, hipStream_t s, Gate gate,
-                         uint32_t* ticket) {
+hipError_t launch_reduce(uint8_t* nodes, uint64_t n, int from_level, int top, hipStream_t s, Gate gate) {
     int j0 = from_level;
     // The widest levels two at a time at full lane use (k_reduce2, while a
     // level holds >= kReduce2Min = 512 Ki nodes: that launch is
@@ -2035,19 +1994,13 @@ hipError_t launch_reduce(uint8_t* nodes, uint64_t n, int from_level, int top, hi
     // and 2 Mi nodes: at most two 1024-thread workgroups per CU, so beyond
     // that the ten-level chains run in several rounds (at 8 Mi nodes 231 us
     // against 209 us for k_reduce2 + slabs; at 1 Mi 50.5 against 53.9 us)
-    // Round 4: with a ticket the last wide workgroup also builds the <= 10
-    // levels above its own twelve (k_reduce_wide), so a 1 Mi-leaf tree is one
-    // launch instead of two.
     for (uint64_t cnt = j0 == 0 ? n : ((n - 1) >> j0) + 1;
          top - j0 >= 12 && cnt >= kReduceWideMin && cnt <= (uint64_t(2) << 20); cnt = ((cnt - 1) >> 12) + 1) {
-        const uint64_t above = ((cnt - 1) >> 12) + 1;  // nodes at level j0 + 12
-        const bool fold = ticket && gate.always_open() && above <= 1024 && top - (j0 + 12) <= 10;
-        const int jtop = fold ? top : j0 + 12;
         hipLaunchKernelGGL(k_reduce_wide, dim3(unsigned((cnt + 4095) / 4096)), dim3(1024), 0, s, nodes, n, j0,
-                           j0 + 12, jtop, fold ? ticket : nullptr, gate);
+                           j0 + 12, gate);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
-        j0 = jtop;
+        j0 += 12;
     }
     for (uint64_t cnt = j0 == 0 ? n : ((n - 1) >> j0) + 1; top - j0 >= 2 && cnt >= kReduce2Min;
          cnt = ((cnt - 1) >> 2) + 1) {
