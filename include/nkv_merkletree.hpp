@@ -37,6 +37,7 @@
 #include <cstring>
 #include <deque>
 #include <exception>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <stdexcept>
@@ -157,6 +158,83 @@ class CopyPool {
     int busy_ = 0;
     bool stop_ = false;
     uint64_t settled_ = 0;
+};
+
+// A small persistent team of host threads for New's materialization and
+// Serialize's walk: Run(parts, fn) calls fn(0 .. parts - 1) on the team and the
+// calling thread, and returns when every part is done.
+class TaskTeam {
+   public:
+    explicit TaskTeam(int threads) {
+        for (int i = 1; i < threads; ++i) th_.emplace_back([this] { Work(); });
+    }
+    ~TaskTeam() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    TaskTeam(const TaskTeam&) = delete;
+    TaskTeam& operator=(const TaskTeam&) = delete;
+    int size() const { return int(th_.size()) + 1; }
+
+    void Run(int parts, const std::function<void(int)>& fn) {
+        if (parts <= 1 || th_.empty()) {
+            for (int k = 0; k < parts; ++k) fn(k);
+            return;
+        }
+        std::unique_lock<std::mutex> g(mu_);
+        fn_ = &fn;
+        parts_ = parts;
+        next_.store(0);
+        left_ = parts;
+        ++gen_;
+        g.unlock();
+        cv_.notify_all();
+        Claim(fn, parts);
+        g.lock();
+        // every part done and no worker still inside Claim (a late fetch_add of
+        // a finished run must not take a part of the next one)
+        done_.wait(g, [this] { return left_ == 0 && active_ == 0; });
+        fn_ = nullptr;
+    }
+
+   private:
+    void Claim(const std::function<void(int)>& fn, int parts) {  // take parts until none is left
+        for (int k; (k = next_.fetch_add(1)) < parts;) {
+            fn(k);
+            std::lock_guard<std::mutex> g(mu_);
+            if (--left_ == 0) done_.notify_all();
+        }
+    }
+    void Work() {
+        uint64_t seen = 0;
+        std::unique_lock<std::mutex> g(mu_);
+        while (true) {
+            cv_.wait(g, [&] { return stop_ || gen_ != seen; });
+            if (stop_) return;
+            seen = gen_;
+            if (!fn_) continue;  // that run already finished without this thread
+            const std::function<void(int)>* fn = fn_;
+            const int parts = parts_;
+            ++active_;
+            g.unlock();
+            Claim(*fn, parts);
+            g.lock();
+            if (--active_ == 0 && left_ == 0) done_.notify_all();
+        }
+    }
+
+    std::vector<std::thread> th_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_;
+    const std::function<void(int)>* fn_ = nullptr;
+    int parts_ = 0, left_ = 0, active_ = 0;
+    std::atomic<int> next_{0};
+    uint64_t gen_ = 0;
+    bool stop_ = false;
 };
 
 struct MerkleNode;
@@ -341,6 +419,11 @@ class Session {
     // (no per-node allocation once a flush of that size has run)
     std::vector<MerkleNode>* TakeNodes();
     void GiveNodes(std::vector<MerkleNode>* v);
+    // the host thread team (lazily: min(8, cores) threads)
+    TaskTeam& Team() {
+        if (!team_) team_.reset(new TaskTeam(int(std::min<unsigned>(8, std::max(1u, std::thread::hardware_concurrency())))));
+        return *team_;
+    }
     // New's level arrays, recycled the same way (no 20 * (2n - 1)-byte zero
     // fill and page faults per flush)
     std::vector<uint8_t> TakeLevels() {
@@ -398,6 +481,7 @@ class Session {
     int copy_threads_ = -1;  // -1: not chosen yet (Pool())
     std::vector<std::vector<MerkleNode>*> spare_;
     std::vector<uint8_t> spare_levels_;
+    std::unique_ptr<TaskTeam> team_;
 };
 
 struct MerkleNode {  // merklenode.go:15-19
@@ -483,6 +567,7 @@ inline MerkleNode NewLeaf(const std::string& v) {
 }
 
 inline Session::~Session() {
+    team_.reset();
     pool_.reset();
     for (auto* v : spare_) delete v;
     if (arena_) nkv_host_free(ctx_, arena_);
@@ -525,32 +610,89 @@ class MerkleTree {  // merkletree.go:13-15
         check(nkv_write_file(fname.c_str(), img.data(), img.size()), ("Serialize(" + fname + ")").c_str());
     }
 
-    // The queue walk (merkletree.go:75-89) in two passes: the BFS order and the
-    // image size, then every node's bytes (merklenode.go:37-63) written in place
-    // -- no per-node vector growth.
+    // The queue walk (merkletree.go:75-89).  A FIFO queue visits every node of
+    // depth d, in order, before any of depth d + 1, so the walk goes level by
+    // level: each level's children and byte counts in parallel chunks (the host
+    // team), then the image (merklenode.go:37-63) written in place, chunk by
+    // chunk, at offsets known from the counts.  The same bytes as the queue.
     std::vector<uint8_t> SerializeBytes() {
-        std::vector<MerkleNode*> q{Root};  // BFS queue: q[head..) still to visit
-        const size_t owned = leaves_.size() + (inner_ ? inner_->size() : 0);
-        if (owned) q.reserve(owned);
-        size_t bytes = 0;
-        for (size_t head = 0; head < q.size(); ++head) {
-            MerkleNode* n = q[head];
-            if (n->Left) q.push_back(n->Left);
-            if (n->Right) q.push_back(n->Right);
-            const size_t d = n->Resolve().size();
-            bytes += d ? 1 + d : 1;
-        }
-        std::vector<uint8_t> w(bytes);
-        uint8_t* o = w.data();
-        for (MerkleNode* n : q) {
-            const size_t d = n->Data.size();
-            if (!d) {
-                *o++ = MERKLE_NODE_EMPTY;
-            } else {
-                *o++ = 0;
-                std::memcpy(o, n->Data.data(), d);
-                o += d;
+        struct Level {
+            std::vector<MerkleNode*> v;
+            std::vector<uint64_t> cut, bytes;  // chunk bounds (parts + 1), chunk byte counts
+        };
+        std::vector<Level> lv(1);
+        lv[0].v.push_back(Root);
+        TaskTeam& team = Session::Default().Team();
+        for (size_t d = 0; !lv[d].v.empty(); ++d) {
+            Level& L = lv[d];
+            const uint64_t m = L.v.size();
+            const int parts = m >= (uint64_t(1) << 15) ? 4 * team.size() : 1;
+            L.cut.resize(parts + 1);
+            for (int k = 0; k <= parts; ++k) L.cut[k] = m * uint64_t(k) / parts;
+            L.bytes.assign(parts, 0);
+            std::vector<uint64_t> kids(parts, 0);
+            std::vector<char> pend(parts, 0);
+            team.Run(parts, [&](int k) {
+                uint64_t c = 0, b = 0;
+                for (uint64_t i = L.cut[k]; i < L.cut[k + 1]; ++i) {
+                    const MerkleNode* x = L.v[i];
+                    c += (x->Left != nullptr) + (x->Right != nullptr);
+                    if (x->pending()) pend[k] = 1;
+                    b += x->Data.empty() ? 1 : 1 + x->Data.size();
+                }
+                kids[k] = c;
+                L.bytes[k] = b;
+            });
+            if (std::find(pend.begin(), pend.end(), 1) != pend.end()) {
+                // deferred NewLeaf digests (a device call): resolve on this thread
+                for (int k = 0; k < parts; ++k) {
+                    uint64_t b = 0;
+                    for (uint64_t i = L.cut[k]; i < L.cut[k + 1]; ++i) {
+                        const size_t sz = L.v[i]->Resolve().size();
+                        b += sz ? 1 + sz : 1;
+                    }
+                    L.bytes[k] = b;
+                }
             }
+            std::vector<uint64_t> at(parts + 1, 0);
+            for (int k = 0; k < parts; ++k) at[k + 1] = at[k] + kids[k];
+            lv.emplace_back();
+            Level& N = lv.back();
+            Level& P = lv[d];  // (emplace_back may have moved the levels)
+            N.v.resize(at[parts]);
+            team.Run(parts, [&](int k) {
+                uint64_t o = at[k];
+                for (uint64_t i = P.cut[k]; i < P.cut[k + 1]; ++i) {
+                    MerkleNode* x = P.v[i];
+                    if (x->Left) N.v[o++] = x->Left;
+                    if (x->Right) N.v[o++] = x->Right;
+                }
+            });
+        }
+        uint64_t total = 0;
+        for (const Level& L : lv)
+            for (uint64_t b : L.bytes) total += b;
+        std::vector<uint8_t> w(total);
+        uint64_t base = 0;
+        for (const Level& L : lv) {
+            const int parts = int(L.bytes.size());
+            std::vector<uint64_t> at(parts + 1, base);
+            for (int k = 0; k < parts; ++k) at[k + 1] = at[k] + L.bytes[k];
+            team.Run(parts, [&](int k) {
+                uint8_t* o = w.data() + at[k];
+                for (uint64_t i = L.cut[k]; i < L.cut[k + 1]; ++i) {
+                    const MerkleNode* x = L.v[i];
+                    const size_t sz = x->Data.size();
+                    if (!sz) {
+                        *o++ = MERKLE_NODE_EMPTY;
+                    } else {
+                        *o++ = 0;
+                        std::memcpy(o, x->Data.data(), sz);
+                        o += sz;
+                    }
+                }
+            });
+            base = at[parts];
         }
         return w;
     }
@@ -835,11 +977,8 @@ inline std::unique_ptr<MerkleTree> New(std::vector<MerkleNode> level, std::strin
         }
     };
     const uint64_t items = n + inner;
-    const int nt = items >= (uint64_t(1) << 16) ? int(std::min<unsigned>(8, std::max(1u, std::thread::hardware_concurrency()))) : 1;
-    std::vector<std::thread> th;
-    for (int k = 1; k < nt; ++k) th.emplace_back(fill, items * k / nt, items * (k + 1) / nt);
-    fill(0, items / nt);
-    for (auto& x : th) x.join();
+    const int nt = items >= (uint64_t(1) << 16) ? 4 * S.Team().size() : 1;
+    S.Team().Run(nt, [&](int k) { fill(items * uint64_t(k) / nt, items * uint64_t(k + 1) / nt); });
     MerkleNode* root = lv == 1 ? &leaves[0] : &pool[lbase[lv - 1]];
     t->Root = root;
     t->timing_.call_ms = std::chrono::duration<double, std::milli>(c1 - c0).count();

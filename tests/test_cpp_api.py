@@ -41,6 +41,24 @@ def test_arena_copy_in_cpu(tmp_path):
     assert out.returncode == 0 and out.stdout.startswith("ok"), out.stdout + out.stderr
 
 
+@pytest.mark.parametrize("sanitize", [False, True])
+def test_task_team_cpu(tmp_path, sanitize):
+    """The mirror's host thread team (New's materialization, Serialize's walk):
+    every part of every run exactly once, runs back to back, clean shutdown;
+    also under ThreadSanitizer (host code only)."""
+    from nakevaleng_amd import build as b
+    so = b.build()
+    libdir = os.path.dirname(so)
+    exe = os.path.join(str(tmp_path), "test_task_team")
+    flags = ["-O1", "-g", "-fsanitize=thread"] if sanitize else ["-O2"]
+    subprocess.check_call(["g++", "-std=c++17", "-Wall", "-pthread", *flags, "-I", os.path.join(ROOT, "include"),
+                           os.path.join(ROOT, "tests", "cpp", "test_task_team.cpp"), "-L", libdir, "-lnkvmerkle",
+                           f"-Wl,-rpath,{libdir}", "-o", exe])
+    out = subprocess.run([exe, "3000" if sanitize else "20000"], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0 and out.stdout.startswith("ok") and "WARNING" not in out.stderr, \
+        out.stdout + out.stderr[-3000:]
+
+
 @pytest.mark.gpu
 def test_cpp_mirror_on_gpu(tmp_path, oracle):
     exe = build_binary(str(tmp_path))
