@@ -131,6 +131,19 @@ void nkvo_splitmix64_fill(uint8_t *buf, uint64_t nbytes, uint64_t seed) {
     }
 }
 
+/* the same stream from byte `first` (a multiple of 8) on: bytes [first, first + nbytes) */
+void nkvo_splitmix64_fill_at(uint8_t *buf, uint64_t nbytes, uint64_t seed, uint64_t first) {
+    const uint64_t k0 = first / 8, nw = nbytes / 8;
+    for (uint64_t k = 0; k < nw; k++) {
+        uint64_t v = splitmix64_at(seed, k0 + k);
+        memcpy(buf + 8 * k, &v, 8);
+    }
+    if (nbytes % 8) {
+        uint64_t v = splitmix64_at(seed, k0 + nw);
+        memcpy(buf + 8 * nw, &v, nbytes % 8);
+    }
+}
+
 /* ---------------- leaf hashing (NewLeaf) ---------------- */
 
 typedef struct {

@@ -34,6 +34,7 @@ def lib():
         L = ctypes.CDLL(_SO)
         L.nkvo_sha1.argtypes = [u8p, ctypes.c_uint64, u8p]
         L.nkvo_splitmix64_fill.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint64]
+        L.nkvo_splitmix64_fill_at.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64]
         L.nkvo_leaf_hashes.argtypes = [u8p, u64p, u64p, ctypes.c_uint64, u8p, ctypes.c_int]
         L.nkvo_leaf_hashes_strided.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, u8p, ctypes.c_int]
         L.nkvo_num_levels.argtypes = [ctypes.c_uint64]
@@ -79,9 +80,14 @@ def sha1(data: bytes) -> bytes:
     return out.tobytes()
 
 
-def splitmix64_bytes(nbytes: int, seed: int) -> np.ndarray:
+def splitmix64_bytes(nbytes: int, seed: int, first: int = 0) -> np.ndarray:
+    """Bytes [first, first + nbytes) of the splitmix64 stream (first: a multiple of 8)."""
+    assert first % 8 == 0
     out = np.empty(max(nbytes, 1), np.uint8)
-    lib().nkvo_splitmix64_fill(_p8(out), nbytes, seed)
+    if first:
+        lib().nkvo_splitmix64_fill_at(_p8(out), nbytes, seed, first)
+    else:
+        lib().nkvo_splitmix64_fill(_p8(out), nbytes, seed)
     return out[:nbytes]
 
 

@@ -13,7 +13,18 @@ running the oracle on the GPU box:
                    in rank order (bench.py --config one_tree, the split over N
                    GPUs), N = 1..8;
   small[r]         the same shape rule at 1 Ki values x 1 KiB (BASELINE
-                   configs[0]'s size) for the CPU tests of the verification.
+                   configs[0]'s size) for the CPU tests of the verification;
+  records[r]       bench.py --config records / records_verify: 1 Mi serialized
+                   4096-byte records (16-byte key) over splitmix64 bytes with
+                   seed 0x6e616b65 + r, leaves = the Values at +46 (the header
+                   fields the bench writes lie outside them);
+  mixed[r]         bench.py --config mixed: BASELINE configs[2]'s 4 GiB of
+                   log-uniform 64 B - 64 KiB values (bench.mixed_lengths, numpy's
+                   default_rng, seed 0x6e616b66 + r) over splitmix64 bytes of the
+                   same seed;
+  config4[r]       BASELINE configs[4]'s per-GPU table: 8 Mi values x 4 KiB (32
+                   GiB) with seed 0x6e616b65 + r, generated and hashed 1 Mi values
+                   at a time (the oracle's stream at a byte offset).
 
 Every root comes from oracle/merkle_oracle.c (the C restatement of
 ds/merkletree: leaf = SHA-1(value), merkletree.go:31-64's build), which the
@@ -21,7 +32,8 @@ CPU suite pins against the FIPS SHA-1 vectors and the literal Python
 restatement (tests/test_oracle.py).  Tree level: parity unpinned, as for every
 fixture in this directory.
 
-    python tests/golden/make_bench_roots.py [--threads 8]
+    python tests/golden/make_bench_roots.py [--threads 8] [--only config4]
+    (--only SECTION recomputes one section into the existing file)
 """
 import argparse
 import json
@@ -48,11 +60,36 @@ def digests(n, vlen, seed, threads):
     return d
 
 
+def config4(threads):
+    import numpy as np
+    n, vlen, chunk = 8 << 20, 4096, 1 << 20
+    sec = {"leaves": n, "value_bytes": vlen, "roots": {}}
+    t0 = time.time()
+    for r in range(RANKS):
+        d = np.empty((n, 20), np.uint8)
+        for c in range(0, n, chunk):
+            data = oc.splitmix64_bytes(chunk * vlen, SEED + r, first=c * vlen)
+            d[c:c + chunk] = oc.leaf_hashes_strided(data, vlen, vlen, chunk, threads=threads)
+            del data
+        sec["roots"][str(r)] = oc.tree_from_digests(d)[-1].tobytes().hex()
+        print(f"config4 rank {r}: {sec['roots'][str(r)]} ({time.time() - t0:.0f} s)", file=sys.stderr)
+    return sec
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--threads", type=int, default=os.cpu_count() or 8)
+    ap.add_argument("--only", choices=["config4"], default=None)
     args = ap.parse_args()
     oc.build()
+    if args.only:
+        with open(OUT) as f:
+            out = json.load(f)
+        out["config4"] = config4(args.threads)
+        with open(OUT, "w") as f:
+            json.dump(out, f, indent=1)
+            f.write("\n")
+        return
     n, vlen = 1 << 20, 4096
     out = {
         "generator": "tests/golden/make_bench_roots.py (oracle/merkle_oracle.c)",
@@ -78,6 +115,26 @@ def main():
     for r in range(RANKS):
         d = digests(1024, 1024, SEED + r, 1)
         out["small"]["roots"][str(r)] = oc.tree_from_digests(d)[-1].tobytes().hex()
+    rb, ks = 4096, 16
+    out["records"] = {"leaves": n, "record_bytes": rb, "key_bytes": ks, "roots": {}}
+    for r in range(RANKS):
+        stream = oc.splitmix64_bytes(n * rb, SEED + r)
+        voff = np.arange(n, dtype=np.uint64) * rb + 30 + ks
+        d = oc.leaf_hashes(stream, voff, np.full(n, rb - 30 - ks, np.uint64), threads=args.threads)
+        del stream
+        out["records"]["roots"][str(r)] = oc.tree_from_digests(d)[-1].tobytes().hex()
+        print(f"records rank {r} ({time.time() - t0:.0f} s)", file=sys.stderr)
+    import bench
+    out["mixed"] = {"payload_bytes": 4 << 30, "seed": bench.SEED_MIXED, "roots": {}, "leaves": {}}
+    for r in range(RANKS):
+        lens, off = bench.mixed_lengths(4 << 30, bench.SEED_MIXED + r)
+        data = oc.splitmix64_bytes(int(lens.sum()), bench.SEED_MIXED + r)
+        d = oc.leaf_hashes(data, off, lens, threads=args.threads)
+        del data
+        out["mixed"]["roots"][str(r)] = oc.tree_from_digests(d)[-1].tobytes().hex()
+        out["mixed"]["leaves"][str(r)] = int(len(lens))
+        print(f"mixed rank {r} ({time.time() - t0:.0f} s)", file=sys.stderr)
+    out["config4"] = config4(args.threads)
     with open(OUT, "w") as f:
         json.dump(out, f, indent=1)
         f.write("\n")

@@ -39,3 +39,34 @@ def test_full_size_roots_rank0_rank1_and_one_tree(oracle):
     assert oracle.tree_from_digests(np.concatenate(leaves))[-1].tobytes().hex() == g["one_tree"]["roots"]["2"]
     # the driver's round-3 line printed rank 0's root (BENCH_r03.json)
     assert g["sstable4k"]["roots"]["0"][0] == "ab9972ce212a49b1492b71c001341efa9dad3dcf"
+
+
+def test_records_and_mixed_roots_rank0(oracle):
+    """The records configs' and the mixed config's committed roots (rank 0),
+    re-derived as bench.build_tables lays the tables out."""
+    g = bench.golden()
+    r = g["records"]
+    n, rb, ks = r["leaves"], r["record_bytes"], r["key_bytes"]
+    stream = oracle.splitmix64_bytes(n * rb, bench.SEED)
+    voff = np.arange(n, dtype=np.uint64) * rb + 30 + ks
+    d = oracle.leaf_hashes(stream, voff, np.full(n, rb - 30 - ks, np.uint64), threads=os.cpu_count() or 8)
+    del stream
+    assert oracle.tree_from_digests(d)[-1].tobytes().hex() == r["roots"]["0"]
+    m = g["mixed"]
+    lens, off = bench.mixed_lengths(m["payload_bytes"], bench.SEED_MIXED)
+    assert len(lens) == m["leaves"]["0"]
+    data = oracle.splitmix64_bytes(int(lens.sum()), bench.SEED_MIXED)
+    d = oracle.leaf_hashes(data, off, lens, threads=os.cpu_count() or 8)
+    del data
+    assert oracle.tree_from_digests(d)[-1].tobytes().hex() == m["roots"]["0"]
+
+
+def test_stream_at_offset_matches_the_stream(oracle):
+    """configs[4]'s committed roots are generated 1 Mi values at a time from the
+    stream at a byte offset: the same bytes as the whole stream."""
+    whole = oracle.splitmix64_bytes(1 << 20, bench.SEED + 3)
+    for first in (8, 4096, 65536, (1 << 20) - 64):
+        part = oracle.splitmix64_bytes((1 << 20) - first, bench.SEED + 3, first=first)
+        assert np.array_equal(part, whole[first:])
+    assert set(bench.golden()["config4"]["roots"]) == {str(r) for r in range(8)}
+    assert bench.expected_roots("sstable4k", 8 << 20, 4096, 7, 1) == [bench.golden()["config4"]["roots"]["7"]]

@@ -268,7 +268,9 @@ def test_merged_line_shape(monkeypatch, capsys):
     assert line["verified_vs_oracle"] is True and line["verified_ranks"] == [True]
     assert line["capi_group"]["value"] == 2.0 and line["capi_one_tree"]["verified_vs_oracle"] is True
     assert line["cpu_baseline"]["cores"] == 1 and line["cpu_baseline"]["sample"] == f"{1 << 20} x 4096"
-    assert calls == [(1, ()), (1, ("--config", "one_tree", "--tables", "1"))]
+    assert calls == [(1, ()), (1, ("--config", "one_tree", "--tables", "1")),
+                     (1, ("--leaves", str(8 << 20), "--tables", "1"))]
+    assert line["capi_config4"]["n_gpus"] == 1
 
 
 def test_merged_line_at_n_gpus_keeps_cpu_baseline(monkeypatch, capsys):
@@ -354,7 +356,12 @@ def test_expected_roots_cover_the_driver_shapes():
     for N in range(1, 9):
         assert len(bench.expected_one_tree(1 << 20, 4096, N)) == 40
     assert bench.expected_roots("sstable4k", 1 << 20, 4096, 8, 1) is None
-    assert bench.expected_roots("mixed", 1 << 20, 4096, 0, 1) is None
+    # the records and mixed configs (rank r's table, one per step)
+    assert len(bench.expected_roots("records_verify", 1 << 20, 4096, 3, 1, key_bytes=16)) == 1
+    assert bench.expected_roots("records", 1 << 20, 4096, 3, 1, key_bytes=20) is None
+    assert len(bench.expected_roots("mixed", None, None, 5, 1, mixed_bytes=4 << 30)) == 1
+    assert bench.expected_roots("mixed", None, None, 5, 1, mixed_bytes=1 << 30) is None
+    assert bench.expected_roots("mixed", None, None, 5, 2) is None
     assert bench.expected_roots("sstable4k", 65536, 4096, 0, 1) is None
     assert bench.expected_one_tree(65536, 4096, 2) is None
 

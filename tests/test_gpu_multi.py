@@ -330,3 +330,5 @@ def test_bench_nccl_world_n(world):
     assert grp["n_gpus"] == world and grp["root_gather_ok"] is True and grp["verified_vs_oracle"] is True
     assert grp["backend"].endswith("RCCL")
     assert one["verified_vs_oracle"] is True and one["members_agree"] is True
+    cfg4 = line["capi_config4"]  # configs[4]'s 8 Mi x 4 KiB table on every GPU
+    assert "error" not in cfg4 and cfg4["verified_vs_oracle"] is True and cfg4["root_gather_ok"] is True
