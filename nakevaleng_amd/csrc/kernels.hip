@@ -186,20 +186,9 @@ __device__ __forceinline__ void load_digest(const uint8_t* nodes, uint64_t idx, 
 // Levels j0+1 .. jmax are computed; each level's nodes are written to the
 // global nodes buffer.  Node i of level j is SHA-1(c[2i] || c[2i+1]) when
 // 2i+1 < n_{j-1}, else SHA-1(c[2i]) (the empty pad, merkletree.go:32-34).
-//
-// Levels whose parents all fit in wave 0 (span <= 64) are a chain of one
-// compression per level on that lone wave; with `sched` (64 rows of
-// kSchedRow words of LDS, B >= 128) they run split over two waves (round 4,
-// sha1_dev.hpp): wave 1 computes each parent's schedule + K into the row of its
-// lane, one 16-word chunk ahead, while wave 0 runs the 80 rounds, reading the
-// chunk written before the last barrier.  Four barriers per level, placed 4
-// rounds before wave 0 needs the chunk, so its LDS reads are in flight while
-// it finishes the previous one.
-constexpr int kSchedRow = 68;  // 64 words + 4: 16-byte aligned rows
-
 template <int B>
 __device__ __forceinline__ void subtree_reduce(uint32_t (*lds)[B], uint64_t n, int j0, int jmax, uint64_t lo,
-                               uint8_t* nodes, uint32_t* sched = nullptr) {
+                               uint8_t* nodes) {
     const int tid = threadIdx.x;
     uint64_t nprev = lvl_count(n, j0);
     uint64_t start_cur = lvl_start(n, j0) + nprev;
@@ -211,69 +200,6 @@ __device__ __forceinline__ void subtree_reduce(uint32_t (*lds)[B], uint64_t n, i
         span >>= 1;
         const bool act = tid < span && lo_cur + tid < ncur;
         uint32_t out[5];
-        if (B >= 128 && sched && span <= 64) {
-            const int lane = tid & 63, wv = tid >> 6;
-            const bool live = lane < span && lo_cur + lane < ncur;
-            const bool mainw = wv == 0 && live, help = wv == 1 && live;
-            uint32_t* row = sched + kSchedRow * lane;
-            __syncthreads();
-            uint32_t w[16];
-            if (mainw || help) {
-                const bool lone = (2 * (lo_cur + lane) + 1) >= nprev;
-                uint32_t l[5], r[5];
-#pragma unroll
-                for (int k = 0; k < 5; ++k) {
-                    l[k] = lds[k][2 * lane];
-                    r[k] = lone ? 0u : lds[k][2 * lane + 1];
-                }
-                parent_block(l, r, lone, w);
-            }
-            uint32_t st[5], wa[16], wb[16];
-            sha1_init(st);
-            if (help) sha1_sched_chunk<1>(w, row);
-            if (mainw) sha1_rounds_regs<0, 12>(st, w);
-            __syncthreads();
-            if (help) sha1_sched_chunk<2>(w, row);
-            if (mainw) {
-                sha1_load_wk(row, 1, wa);
-                sha1_rounds_regs<12, 16>(st, w);
-                sha1_rounds_wk<16, 28, 16>(st, wa);
-            }
-            __syncthreads();
-            if (help) sha1_sched_chunk<3>(w, row);
-            if (mainw) {
-                sha1_load_wk(row, 2, wb);
-                sha1_rounds_wk<28, 32, 16>(st, wa);
-                sha1_rounds_wk<32, 44, 32>(st, wb);
-            }
-            __syncthreads();
-            if (help) sha1_sched_chunk<4>(w, row);
-            if (mainw) {
-                sha1_load_wk(row, 3, wa);
-                sha1_rounds_wk<44, 48, 32>(st, wb);
-                sha1_rounds_wk<48, 60, 48>(st, wa);
-            }
-            __syncthreads();
-            if (mainw) {
-                sha1_load_wk(row, 4, wb);
-                sha1_rounds_wk<60, 64, 48>(st, wa);
-                sha1_rounds_wk<64, 80, 64>(st, wb);
-                uint32_t h0[5];
-                sha1_init(h0);
-#pragma unroll
-                for (int k = 0; k < 5; ++k) out[k] = h0[k] + st[k];
-            }
-            __syncthreads();
-            if (mainw) {
-#pragma unroll
-                for (int k = 0; k < 5; ++k) lds[k][tid] = out[k];
-                store_digest(nodes, start_cur + lo_cur + tid, out);
-            }
-            nprev = ncur;
-            start_cur += ncur;
-            lo_prev = lo_cur;
-            continue;
-        }
         __syncthreads();
         if (act) {
             uint32_t l[5], r[5];
@@ -1444,16 +1370,9 @@ __global__ __launch_bounds__(64, kQueueRing) void k_leaf_queue(const uint8_t* __
 // min(j0 + log2 B, top) in LDS, one workgroup of B threads per slab: 8 levels
 // per launch with B = 256, 10 with B = 1024 (the narrow levels are a chain of
 // one compression per level, so fewer launches is a shorter tree).
-#ifdef NKV_NO_SPLIT
-#define NKV_SCHED nullptr
-#else
-#define NKV_SCHED sched
-#endif
-
 template <int B>
 __global__ __launch_bounds__(B) void k_reduce(uint8_t* __restrict__ nodes, uint64_t n, int j0, int jmax, Gate gate) {
     __shared__ uint32_t lds[5][B];
-    __shared__ __align__(16) uint32_t sched[64 * kSchedRow];
     if (!gate.open()) return;
     const uint64_t lo = uint64_t(blockIdx.x) * B;
     const uint64_t cnt = lvl_count(n, j0);
@@ -1462,7 +1381,7 @@ __global__ __launch_bounds__(B) void k_reduce(uint8_t* __restrict__ nodes, uint6
     if (idx < cnt) load_digest(nodes, lvl_start(n, j0) + idx, h);
 #pragma unroll
     for (int k = 0; k < 5; ++k) lds[k][threadIdx.x] = h[k];
-    subtree_reduce<B>(lds, n, j0, jmax, lo, nodes, NKV_SCHED);
+    subtree_reduce<B>(lds, n, j0, jmax, lo, nodes);
 }
 
 // K2w: the wide bottom levels at full lane use.  A wavefront takes 256 nodes
@@ -1523,7 +1442,6 @@ __global__ __launch_bounds__(kBlock) void k_reduce2(uint8_t* __restrict__ nodes,
 __global__ __launch_bounds__(1024) void k_reduce_wide(uint8_t* __restrict__ nodes, uint64_t n, int j0, int jmax,
                                                       Gate gate) {
     __shared__ uint32_t lds[5][1024];
-    __shared__ __align__(16) uint32_t sched[64 * kSchedRow];
     if (!gate.open()) return;
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
@@ -1564,7 +1482,7 @@ __global__ __launch_bounds__(1024) void k_reduce_wide(uint8_t* __restrict__ node
     // level j0 + 2 of this workgroup's 4096 nodes: 1024 nodes, node 64 wv + lane
 #pragma unroll
     for (int k = 0; k < 5; ++k) lds[k][threadIdx.x] = h[k];
-    subtree_reduce<1024>(lds, n, j0 + 2, jmax, uint64_t(blockIdx.x) * 1024, nodes, NKV_SCHED);
+    subtree_reduce<1024>(lds, n, j0 + 2, jmax, uint64_t(blockIdx.x) * 1024, nodes);
 }
 
 // ---------------------------------------------------------------------------

@@ -108,93 +108,6 @@ __device__ __forceinline__ void sha1_compress(uint32_t h[5], uint32_t w[16]) {
     h[4] += e;
 }
 
-// ---------------------------------------------------------------------------
-// A compression split over two waves (round 4): the tree's top levels are a
-// chain of one compression per level on a lone wave, which issues one
-// instruction every ~4.65 cycles whatever the work, so
-// the chain is its instruction count.  A helper wave computes the schedule
-// words W[16..79] + K into LDS while the chain wave runs only the rounds: 400
-// round instructions + 16 ds_read_b128 instead of 613.
-
-constexpr uint32_t sha1_k(int t) {
-    return t < 20 ? 0x5A827999u : t < 40 ? 0x6ED9EBA1u : t < 60 ? 0x8F1BBCDCu : 0xCA62C1D6u;
-}
-
-// One round; ewk = e + W[t] + K[t] already summed.
-template <int T>
-__device__ __forceinline__ void sha1_round(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d, uint32_t& e,
-                                           uint32_t ewk) {
-    uint32_t f;
-    if (T < 20) f = ch(b, c, d);
-    else if (T < 40 || T >= 60) f = xor3(b, c, d);
-    else f = maj(b, c, d);
-    const uint32_t tmp = add3(rotl(a, 5), f, ewk);
-    e = d;
-    d = c;
-    c = rotl(b, 30);
-    b = a;
-    a = tmp;
-}
-
-// Rounds [T0, T1) from message words in registers (T1 <= 16).
-template <int T0, int T1>
-__device__ __forceinline__ void sha1_rounds_regs(uint32_t s[5], const uint32_t w[16]) {
-#pragma unroll
-    for (int t = T0; t < T1; ++t) {
-        switch (t) {  // (compile-time t: the switch folds away)
-#define NKV_R(T)                                                                  \
-    case T:                                                                       \
-        sha1_round<T>(s[0], s[1], s[2], s[3], s[4], add3k(s[4], w[T], sha1_k(T))); \
-        break;
-            NKV_R(0) NKV_R(1) NKV_R(2) NKV_R(3) NKV_R(4) NKV_R(5) NKV_R(6) NKV_R(7)
-            NKV_R(8) NKV_R(9) NKV_R(10) NKV_R(11) NKV_R(12) NKV_R(13) NKV_R(14) NKV_R(15)
-#undef NKV_R
-        }
-    }
-}
-
-// Rounds [T0, T1) (T0 >= 16) from W + K words: wk[t - Tbase] in registers.
-template <int T0, int T1, int TB>
-__device__ __forceinline__ void sha1_rounds_wk(uint32_t s[5], const uint32_t wk[16]) {
-#pragma unroll
-    for (int t = T0; t < T1; ++t) {
-        const uint32_t ewk = s[4] + wk[t - TB];
-        if (t < 20) sha1_round<19>(s[0], s[1], s[2], s[3], s[4], ewk);
-        else if (t < 40) sha1_round<20>(s[0], s[1], s[2], s[3], s[4], ewk);
-        else if (t < 60) sha1_round<40>(s[0], s[1], s[2], s[3], s[4], ewk);
-        else sha1_round<60>(s[0], s[1], s[2], s[3], s[4], ewk);
-    }
-}
-
-// The helper's part: schedule words [16 C, 16 C + 16) of the rolling window w,
-// plus their K, stored at row[t - 16] (row: 16-byte aligned, 64 words).
-template <int C>
-__device__ __forceinline__ void sha1_sched_chunk(uint32_t w[16], uint32_t* row) {
-#pragma unroll
-    for (int q = 0; q < 16; q += 4) {
-        uint32_t v[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int t = 16 * C + q + u;
-            const uint32_t wt = rotl(xor3(w[(t - 3) & 15], w[(t - 8) & 15], w[(t - 14) & 15]) ^ w[t & 15], 1);
-            w[t & 15] = wt;
-            v[u] = wt + sha1_k(t);
-        }
-        *reinterpret_cast<uint4*>(row + 16 * (C - 1) + q) = make_uint4(v[0], v[1], v[2], v[3]);
-    }
-}
-
-__device__ __forceinline__ void sha1_load_wk(const uint32_t* row, int c, uint32_t wk[16]) {
-#pragma unroll
-    for (int q = 0; q < 16; q += 4) {
-        const uint4 v = *reinterpret_cast<const uint4*>(row + 16 * (c - 1) + q);
-        wk[q] = v.x;
-        wk[q + 1] = v.y;
-        wk[q + 2] = v.z;
-        wk[q + 3] = v.w;
-    }
-}
-
 // Parent node of the Merkle tree (ds/merkletree/merkletree.go:44-46):
 // SHA-1(left || right) for a pair (40-byte message), SHA-1(left) for a lone
 // node whose sibling is the empty pad (20-byte message).  Children are given
@@ -219,18 +132,6 @@ __device__ __forceinline__ void sha1_parent(const uint32_t l[5], const uint32_t 
     }
     sha1_init(out);
     sha1_compress(out, w);
-}
-
-// The message block of a parent (as sha1_parent builds it).
-__device__ __forceinline__ void parent_block(const uint32_t l[5], const uint32_t r[5], bool lone, uint32_t w[16]) {
-#pragma unroll
-    for (int i = 0; i < 5; ++i) w[i] = l[i];
-#pragma unroll
-    for (int i = 0; i < 5; ++i) w[5 + i] = lone ? (i == 0 ? 0x80000000u : 0u) : r[i];
-    w[10] = lone ? 0u : 0x80000000u;
-#pragma unroll
-    for (int i = 11; i < 15; ++i) w[i] = 0u;
-    w[15] = lone ? 160u : 320u;
 }
 
 }  // namespace nkv
