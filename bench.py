@@ -929,9 +929,9 @@ def main_api_flush(args):
     n, vlen = args.leaves, args.value_bytes
     runs = {}
     with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
-        for mode, threads in (("pool", -1), ("caller_thread", 0)):
+        for mode, threads, retain in (("pool", -1, 1), ("caller_thread", 0, 1), ("pool_glibc_heap", -1, 0)):
             out = subprocess.run([exe, str(n), str(vlen), str(max(2, args.api_cycles)), td, "1", hex(SEED), "1",
-                                  str(threads)], capture_output=True, text=True, timeout=900)
+                                  str(threads), str(retain)], capture_output=True, text=True, timeout=900)
             if out.returncode != 0:
                 raise SystemExit(f"api_flush failed: {out.stderr[-2000:]}")
             runs[mode] = [json.loads(x) for x in out.stdout.splitlines() if x.startswith("{")]
@@ -961,9 +961,14 @@ def main_api_flush(args):
         "dtype": "u32",
         "data": f"synthetic: splitmix64 bytes (seed {SEED:#x}) in host memory (the memtable's values)",
         "config": {"workload": f"memtable flush: {n} x {vlen} B values, sstable.go:58-74 call sequence",
-                   "leaves": n, "value_bytes": vlen, "copy_threads": b.get("copy_threads")},
+                   "leaves": n, "value_bytes": vlen, "copy_threads": b.get("copy_threads"),
+                   "heap": "retained between flushes (M_MMAP_THRESHOLD 1 GiB, no trim), as a Go GC heap"},
         "breakdown_ms": {k: b[k] for k in keys},
         "copies_on_caller_thread": {"gib_s": c0["gib_s"], **{k: c0[k] for k in keys}},
+        # the same flush with glibc's default heap policy (every freed block over
+        # 32 MiB unmapped: the next flush page-faults it again)
+        "glibc_default_heap": {"gib_s": best["pool_glibc_heap"]["gib_s"],
+                               **{k: best["pool_glibc_heap"][k] for k in keys}},
         "cycles": runs,
         "root": root,
         "verified_vs_oracle": verified,

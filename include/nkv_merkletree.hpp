@@ -108,20 +108,29 @@ class CopyPool {
     // the arena prefix whose copies are all done (caller thread only)
     uint64_t Settled() {
         std::lock_guard<std::mutex> g(mu_);
-        while (!jobs_.empty() && jobs_.front()->done.load(std::memory_order_acquire)) {
-            settled_ = jobs_.front()->end;
-            jobs_.pop_front();
-        }
+        while (!jobs_.empty() && jobs_.front()->done.load(std::memory_order_acquire)) Retire();
         return settled_;
+    }
+    // a job to fill: a retired one with its task vector's capacity (no fresh
+    // allocation, and no page faults, per job once a flush of that size ran)
+    std::unique_ptr<Job> Fresh() {
+        std::lock_guard<std::mutex> g(mu_);
+        std::unique_ptr<Job> j;
+        if (!free_.empty()) {
+            j = std::move(free_.back());
+            free_.pop_back();
+            j->tasks.clear();
+            j->done.store(false);
+        } else {
+            j.reset(new Job());
+        }
+        return j;
     }
     // wait for every submitted job (their stores are fenced by the workers)
     void Drain() {
         std::unique_lock<std::mutex> g(mu_);
         idle_.wait(g, [this] { return queue_.empty() && busy_ == 0; });
-        while (!jobs_.empty()) {
-            settled_ = jobs_.front()->end;
-            jobs_.pop_front();
-        }
+        while (!jobs_.empty()) Retire();
     }
     // a new batch starts at arena byte 0
     void Reset() {
@@ -130,6 +139,11 @@ class CopyPool {
     }
 
    private:
+    void Retire() {  // the front job is done (mu_ held)
+        settled_ = jobs_.front()->end;
+        free_.push_back(std::move(jobs_.front()));
+        jobs_.pop_front();
+    }
     void Work() {
         std::unique_lock<std::mutex> g(mu_);
         while (true) {
@@ -154,6 +168,7 @@ class CopyPool {
     std::mutex mu_;
     std::condition_variable cv_, idle_;
     std::deque<std::unique_ptr<Job>> jobs_;  // submitted, in arena order, not yet settled
+    std::vector<std::unique_ptr<Job>> free_;  // retired, for Fresh()
     std::deque<Job*> queue_;                 // not yet taken by a worker
     int busy_ = 0;
     bool stop_ = false;
@@ -296,9 +311,19 @@ class Session {
                 batch_->digests.clear();
                 batch_->resolved = false;
             } else {
-                batch_ = std::make_shared<Batch>();
-                batch_->off.reserve(hint);
-                batch_->len.reserve(hint);
+                auto nb = std::make_shared<Batch>();
+                if (batch_ && batch_->resolved) {
+                    // a sealed batch's places are never read again (its leaves
+                    // hold their digests or read them from `digests`): the new
+                    // batch takes its vectors, capacity and all
+                    nb->off.swap(batch_->off);
+                    nb->len.swap(batch_->len);
+                    nb->off.clear();
+                    nb->len.clear();
+                }
+                nb->off.reserve(hint);
+                nb->len.reserve(hint);
+                batch_ = std::move(nb);
             }
             batch_->epoch = ++epoch_;
             Settle();
@@ -313,9 +338,9 @@ class Session {
         used_ = at + n;
         if (defer && Pool()) {
             if (!job_) {
-                job_.reset(new CopyPool::Job());
+                job_ = pool_->Fresh();
                 job_->base = static_cast<uint8_t*>(arena_);
-                job_->tasks.reserve(kJobBytes / 4096 + 1);
+                if (job_->tasks.capacity() == 0) job_->tasks.reserve(kJobBytes / 4096 + 1);
             }
             if (n) job_->tasks.push_back({at, data, n});
             job_bytes_ += n;

@@ -194,6 +194,19 @@ int main(int argc, char** argv) {
         }
         nkv::merkletree::Group g1({0});
         std::printf("group1_transport %d\n", nkv_group_transport(g1.get()));
+        // every visible GPU (a multi-GPU box): ncclCommInitAll over distinct
+        // devices with /opt/rocm's RCCL, as a C++ or Go host loads it
+        int cnt = 0;
+        if (nkv_device_count(&cnt) == NKV_OK && cnt > 1) {
+            std::vector<int> all;
+            for (int d = 0; d < cnt; ++d) all.push_back(d);
+            nkv::merkletree::Group ga(all);
+            std::printf("groupall_size %d\ngroupall_transport %d\n", ga.size(), nkv_group_transport(ga.get()));
+            auto roots = nkv::merkletree::CompactRoots(ga, tabs);
+            for (size_t t = 0; t < roots.size(); ++t)
+                std::printf("compact_gall_root%zu %s\n", t,
+                            hex(std::vector<uint8_t>(roots[t].begin(), roots[t].end())).c_str());
+        }
     }
     return 0;
 }

@@ -135,3 +135,6 @@ def test_cpp_mirror_on_gpu(tmp_path, oracle):
         off, ln = record.value_spans(stream, rs)
         want = oracle.tree_from_digests(oracle.leaf_hashes(np.frombuffer(stream, np.uint8), off, ln))
         assert kv[f"compact_g1_root{t}"] == kv[f"compact_g2_root{t}"] == want[-1].tobytes().hex()
+        if "groupall_size" in kv:  # several GPUs: the group over all of them, /opt/rocm's RCCL
+            assert kv["groupall_transport"] == "1"
+            assert kv[f"compact_gall_root{t}"] == want[-1].tobytes().hex()

@@ -21,9 +21,14 @@
 //   root_ms       Root.String()
 //   walk_ms / write_ms   Serialize: BFS walk of the live tree, file write
 //
-// Usage: api_flush N VLEN CYCLES DIR [STREAMING=1] [SEED] [NONTEMPORAL=1] [COPY_THREADS=-1]
-// (COPY_THREADS -1: the mirror's default, min(16, cores) or NKV_COPY_THREADS)
+// Usage: api_flush N VLEN CYCLES DIR [STREAMING=1] [SEED] [NONTEMPORAL=1] [COPY_THREADS=-1] [RETAIN_HEAP=1]
+// (COPY_THREADS -1: the mirror's default, min(16, cores) or NKV_COPY_THREADS.
+// RETAIN_HEAP 1: the process keeps freed memory mapped between flushes, as a Go
+// process's garbage-collected heap does; glibc's default hands every block over
+// 32 MiB back to the kernel on free, so each flush would page-fault its
+// 64 MiB leaves slice and the tree's node storage afresh.  0: glibc defaults.)
 #include <fcntl.h>
+#include <malloc.h>
 #include <unistd.h>
 
 #include <chrono>
@@ -69,6 +74,11 @@ int main(int argc, char** argv) {
     const uint64_t seed = argc > 6 ? std::strtoull(argv[6], nullptr, 0) : 0x6E616B65ull;
     const bool nontemporal = argc > 7 ? std::atoi(argv[7]) != 0 : true;
     const int copy_threads = argc > 8 ? std::atoi(argv[8]) : -1;
+    const bool retain_heap = argc > 9 ? std::atoi(argv[9]) != 0 : true;
+    if (retain_heap) {
+        mallopt(M_MMAP_THRESHOLD, 1 << 30);  // large blocks from the heap, not fresh mappings
+        mallopt(M_TRIM_THRESHOLD, -1);       // and the heap is not trimmed on free
+    }
     std::vector<uint8_t> memtable(n * vlen);
     fill(memtable.data(), memtable.size(), seed, 16);
     Session& S = Session::Default();
@@ -102,12 +112,12 @@ int main(int argc, char** argv) {
         const double total = ms(t0, t5);
         std::printf(
             "{\"cycle\": %d, \"n\": %llu, \"value_bytes\": %llu, \"streaming\": %d, \"nontemporal\": %d, "
-            "\"copy_threads\": %d, \"gib_s\": %.3f, "
+            "\"copy_threads\": %d, \"retain_heap\": %d, \"gib_s\": %.3f, "
             "\"total_ms\": %.3f, \"newleaf_ms\": %.3f, \"new_call_ms\": %.3f, \"upload_ms\": %.3f, "
             "\"kernels_ms\": %.3f, \"download_ms\": %.3f, \"materialize_ms\": %.3f, \"root_ms\": %.3f, "
             "\"walk_ms\": %.3f, \"write_ms\": %.3f, \"image_bytes\": %zu, \"arena_allocs\": %llu, "
             "\"root\": \"%s\"}\n",
-            cyc, (unsigned long long)n, (unsigned long long)vlen, int(streaming), int(nontemporal), S.CopyThreads(),
+            cyc, (unsigned long long)n, (unsigned long long)vlen, int(streaming), int(nontemporal), S.CopyThreads(), int(retain_heap),
             double(n * vlen) / (total * 1e-3) / double(1ull << 30), total, ms(t0, t1),
             tree->LastNewTiming().call_ms, up, ker, down, tree->LastNewTiming().materialize_ms, ms(t2, t3),
             ms(t3, t4), ms(t4, t5), img.size(), (unsigned long long)S.arena_allocs(), root.c_str());
