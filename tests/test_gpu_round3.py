@@ -270,6 +270,35 @@ def test_group_split_tree_copy_transport(nkv, oracle, g, n):
         assert L.nkv_group_tree_dev(grp.h, arr, n, droot_bad, None) == _lib.NKV_ERR_INVALID
 
 
+def test_group_split_refusals_leave_no_tree(nkv, oracle):
+    """after any refused or failed split call -- the device form with a
+    part of the wrong length, with n = 0, or the host form with a null pointer --
+    nkv_group_tree_fetch refuses; a good call after it fetches the new tree.
+    d_roots may be NULL or hold NULL entries."""
+    _lib, _ = nkv
+    L = _lib.lib()
+    g, n, vl = 3, 1000, 64
+    data = np.frombuffer(np.random.default_rng(44).bytes(n * vl), np.uint8).copy()
+    want = oracle.tree_from_digests(oracle.leaf_hashes_strided(data, vl, vl, n))
+    nodes = np.zeros((L.nkv_total_nodes(n), 20), np.uint8)
+    with _lib.Group([0] * g) as grp:
+        parts, keep = split_parts(_lib, g, n, data, vl)
+        arr = (_lib.NkvTable * g)(*parts)
+        one = torch.zeros(20, dtype=torch.uint8, device="cuda")
+        roots = (ctypes.c_void_p * g)(None, one.data_ptr(), None)  # only member 1 wants its root
+        for bad in (lambda: L.nkv_group_tree_dev(grp.h, arr, n + 1, None, None),
+                    lambda: L.nkv_group_tree_dev(grp.h, arr, 0, None, None),
+                    lambda: L.nkv_group_tree_from_values(grp.h, None, None, None, n, None, None, None)):
+            _lib.check(L.nkv_group_tree_dev(grp.h, arr, n, roots, None))
+            grp.sync()
+            assert one.cpu().numpy().tobytes() == want[-1].tobytes()
+            assert bad() != _lib.NKV_OK
+            assert L.nkv_group_tree_fetch(grp.h, _lib.p8(nodes), None) == _lib.NKV_ERR_INVALID
+        _lib.check(L.nkv_group_tree_dev(grp.h, arr, n, None, None))
+        _lib.check(L.nkv_group_tree_fetch(grp.h, _lib.p8(nodes), None))
+        assert np.array_equal(nodes, want)
+
+
 def values_parts(_lib, g, n, base, off, ln):
     """Member r's ragged leaf range as a VALUES table: its values' bytes, offsets
     rebased to them, lengths (device tensors)."""
