@@ -951,10 +951,7 @@ __device__ __forceinline__ void sha1_blocks_any(uint8_t* wbuf, const uint8_t* p,
 // measured in rounds 1-2 (LDS-DMA stage for aligned values, direct and
 // non-temporal loads, 256-byte runs, line-pair stage, runs at each value's own
 // address, deep register prefetch) lost their A/Bs and are gone.
-#ifndef NKV_RUNS_WAVES
-#define NKV_RUNS_WAVES 4
-#endif
-constexpr int kRunsWaves = NKV_RUNS_WAVES;  // launch bound of the LOAD 4 kernel
+constexpr int kRunsWaves = 4;  // launch bound of the LOAD 4 kernel
 template <int MODE, int LOAD>
 __global__ __launch_bounds__(kBlock, LOAD == 4 ? kRunsWaves : kLeafWavesPerSimd) void k_leaf(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ off, const uint64_t* __restrict__ len,
@@ -1120,10 +1117,7 @@ struct CrcBE {
 // voff / vlen for the length-sorted leaf pass; a hashed value's voff becomes
 // kDone.  Each workgroup leaves (0, deferred ? ~0 : 0, 0) in part, folded by
 // k_locate_fold into the range whose wide Gate opens the sorted pass.
-#ifndef NKV_VERIFY_WAVES
-#define NKV_VERIFY_WAVES 4
-#endif
-constexpr int kVerifyWaves = NKV_VERIFY_WAVES;  // whole lines in registers with the CRC state: ~105 VGPRs
+constexpr int kVerifyWaves = 4;  // whole lines in registers with the CRC state: ~105 VGPRs
 __global__ __launch_bounds__(kBlock, kVerifyWaves) void k_leaf_verify(
     const uint8_t* __restrict__ stream, uint64_t stream_len, const uint64_t* __restrict__ rec_off, uint64_t n,
     int policy, uint64_t* __restrict__ voff, uint64_t* __restrict__ vlen, uint8_t* __restrict__ nodes,
@@ -1776,10 +1770,7 @@ __global__ __launch_bounds__(kBlock) void k_locate_fold(const uint32_t* __restri
 // which k_locate_fold turns into err and a range whose wide Gate opens the
 // sorted pass only when something was deferred.  A header outside the
 // stream flags bad and hashes the empty value (as k_locate).
-#ifndef NKV_RECORDS_WAVES
-#define NKV_RECORDS_WAVES 5
-#endif
-constexpr int kRecordsWaves = NKV_RECORDS_WAVES;  // narrow waves of line-aligned records take whole lines: ~86 VGPRs
+constexpr int kRecordsWaves = 5;  // narrow waves of line-aligned records take whole lines: ~86 VGPRs
 __global__ __launch_bounds__(kBlock, kRecordsWaves) void k_leaf_records(
     const uint8_t* __restrict__ stream, uint64_t stream_len, const uint64_t* __restrict__ rec_off, uint64_t n,
     int policy, uint64_t* __restrict__ voff, uint64_t* __restrict__ vlen, uint8_t* __restrict__ nodes,
