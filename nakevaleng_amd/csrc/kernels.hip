@@ -985,7 +985,10 @@ __global__ __launch_bounds__(kBlock, LOAD == 4 ? kRunsWaves : kLeafWavesPerSimd)
     if constexpr (LOAD == 4) {
         if (live) {
             sha1_blocks_runs<2>(p, uint32_t(ln >> 6), h);
-            sha1_tail<true>(p, ln, h);
+            // one length for all: a whole-block length's padding block is the
+            // same message in every lane (its schedule on the scalar unit)
+            if (MODE == 0 && (L & 63) == 0) sha1_pad_uniform(h, L);
+            else sha1_tail<true>(p, ln, h);
             store_digest(nodes, leaf, h);
         }
     } else {

@@ -108,15 +108,99 @@ __device__ __forceinline__ void sha1_compress(uint32_t h[5], uint32_t w[16]) {
     h[4] += e;
 }
 
+// rotl(x, 1) of a wave-uniform x on the scalar unit.  Written as shifts in C,
+// the compiler recognises the rotate and selects v_alignbit (vector-only) plus
+// a v_readfirstlane back; s_lshl1_add_u32 adds the carried-out bit instead.
+__device__ __forceinline__ uint32_t srotl1(uint32_t x) {
+    uint32_t r, t;
+    asm("s_lshr_b32 %1, %2, 31\n\ts_lshl1_add_u32 %0, %2, %1" : "=s"(r), "=&s"(t) : "s"(x) : "scc");
+    return r;
+}
+
+// A block whose 16 message words are the same in every lane (wave-uniform:
+// the padding block of values of one length that is a multiple of 64): the
+// schedule and W + K run on the scalar unit, which idles beside the VALU, so
+// the block costs the 400 round ops (e + W + K: one v_add with an SGPR
+// operand) instead of 613 VALU.
+__device__ __forceinline__ void sha1_compress_uniform(uint32_t h[5], uint32_t w[16]) {
+    uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4];
+#pragma unroll
+    for (int t = 0; t < 80; ++t) {
+        uint32_t wt;
+        if (t < 16) {
+            wt = w[t];
+        } else {
+            wt = srotl1(w[(t - 3) & 15] ^ w[(t - 8) & 15] ^ w[(t - 14) & 15] ^ w[t & 15]);
+            w[t & 15] = wt;
+        }
+        uint32_t f, k;
+        if (t < 20) {
+            f = ch(b, c, d);
+            k = 0x5A827999u;
+        } else if (t < 40) {
+            f = xor3(b, c, d);
+            k = 0x6ED9EBA1u;
+        } else if (t < 60) {
+            f = maj(b, c, d);
+            k = 0x8F1BBCDCu;
+        } else {
+            f = xor3(b, c, d);
+            k = 0xCA62C1D6u;
+        }
+        uint32_t wk, ewk;  // W + K on the scalar unit, + e in one v_add with an SGPR operand
+        asm("s_add_u32 %0, %1, %2" : "=s"(wk) : "s"(wt), "s"(k) : "scc");
+        asm("v_add_u32 %0, %1, %2" : "=v"(ewk) : "s"(wk), "v"(e));
+        const uint32_t tmp = add3(rotl(a, 5), f, ewk);
+        e = d;
+        d = c;
+        c = rotl(b, 30);
+        b = a;
+        a = tmp;
+    }
+    h[0] += a;
+    h[1] += b;
+    h[2] += c;
+    h[3] += d;
+    h[4] += e;
+}
+
+// The padding block of a value whose length L (wave-uniform) is a multiple of
+// 64: 0x80, zeros, the 64-bit big-endian bit length (FIPS 180-4 5.1.1).
+__device__ __forceinline__ void sha1_pad_uniform(uint32_t h[5], uint64_t L) {
+    const uint64_t bits = L << 3;
+    uint32_t w[16];
+    w[0] = 0x80000000u;
+#pragma unroll
+    for (int j = 1; j < 14; ++j) w[j] = 0u;
+    w[14] = uint32_t(bits >> 32);
+    w[15] = uint32_t(bits);
+    sha1_compress_uniform(h, w);
+}
+
 // Parent node of the Merkle tree (ds/merkletree/merkletree.go:44-46):
 // SHA-1(left || right) for a pair (40-byte message), SHA-1(left) for a lone
 // node whose sibling is the empty pad (20-byte message).  Children are given
 // as their SHA-1 state words, which are exactly the big-endian message words.
+// A wave with no lone node (all but at most one wave of a level) takes the
+// pair form with its padding words as constants, which the compiler folds
+// into the schedule; only a wave holding the level's lone node selects the
+// message words per lane.
 __device__ __forceinline__ void sha1_parent(const uint32_t l[5], const uint32_t r[5], bool lone,
                                             uint32_t out[5]) {
     uint32_t w[16];
 #pragma unroll
     for (int i = 0; i < 5; ++i) w[i] = l[i];
+    sha1_init(out);
+    if (!__any(lone)) {
+#pragma unroll
+        for (int i = 0; i < 5; ++i) w[5 + i] = r[i];
+        w[10] = 0x80000000u;
+#pragma unroll
+        for (int i = 11; i < 15; ++i) w[i] = 0u;
+        w[15] = 320u;
+        sha1_compress(out, w);
+        return;
+    }
     if (lone) {
         w[5] = 0x80000000u;
 #pragma unroll
@@ -130,7 +214,6 @@ __device__ __forceinline__ void sha1_parent(const uint32_t l[5], const uint32_t 
         for (int i = 11; i < 15; ++i) w[i] = 0u;
         w[15] = 320u;
     }
-    sha1_init(out);
     sha1_compress(out, w);
 }
 
