@@ -32,13 +32,14 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.
 # v_add3 / v_alignbit / v_perm set the cadence, profiles/r01_valu_rate.txt),
 # VALU_PER_WAVE_BLOCK instructions per wave per 64-byte block (PMC
 # SQ_INSTS_VALU per launch / wave-blocks of payload: leaf from the register-run
-# kernel, profiles/r03_leaf_valu_pmc.json; records (k_leaf_records) and verify
+# kernel with its padding block's schedule on the scalar unit,
+# profiles/r04_pad_valu_pmc.json (39,689 per wave / 64; 623.0 before); records (k_leaf_records) and verify
 # (k_leaf_verify) per 64 bytes of Value, profiles/r03_records_pmc.json), 4096 bytes per
 # wave-block (64 lanes x 64 B):
 #   ceiling = SIMDS x f / (VALU_PER_WAVE_BLOCK x VALU_CYCLES) x 4096 B.
 SIMDS = 1024  # 256 CUs x 4
 VALU_CYCLES = 4.0
-VALU_PER_WAVE_BLOCK = {"leaf": 623.0, "records": 631.7, "verify": 737.9}
+VALU_PER_WAVE_BLOCK = {"leaf": 620.1, "records": 631.7, "verify": 737.9}
 SHA1_VALU_CEILING_GBS = 4100.0  # fallback without a clock reading: tools/sha1_rate.hip at 2.37 GHz
 # The mixed config's floor is its longest value: one lane's chain of dependent
 # compressions, on a wave that issues one instruction every ~4.65 cycles when

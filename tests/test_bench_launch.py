@@ -237,8 +237,8 @@ def test_valu_ceiling_prices_each_kernel_at_its_own_count():
     for c in ("cfg2", "mixed", "runs4", "one_tree"):
         assert bench.valu_kind(c) == "leaf"
     assert bench.valu_ceiling(None, "leaf") is None
-    # 1024 SIMDs at 2.2 GHz, one VALU per 4 cycles, 623 per 4 KiB wave-block
-    assert abs(bench.valu_ceiling(2200.0, "leaf") - 1024 * 2.2e9 / (623.0 * 4) * 4096 / 1e9) < 1e-6
+    # 1024 SIMDs at 2.2 GHz, one VALU per 4 cycles, 620.1 per 4 KiB wave-block
+    assert abs(bench.valu_ceiling(2200.0, "leaf") - 1024 * 2.2e9 / (620.1 * 4) * 4096 / 1e9) < 1e-6
     assert bench.valu_ceiling(2200.0, "verify") < bench.valu_ceiling(2200.0, "records") < bench.valu_ceiling(2200.0, "leaf")
 
 

@@ -270,6 +270,27 @@ def test_strided_device_path(nkv, oracle, base_off, stride, vlen):
     assert np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("vlen,stride", [(0, 16), (64, 64), (128, 128), (192, 208), (4096, 4096), (8192, 8192)])
+@pytest.mark.parametrize("n", [1, 1000, 4097])
+def test_strided_whole_block_lengths(nkv, oracle, vlen, stride, n):
+    """Lengths that are multiples of 64: the padding block is the same message in
+    every lane and k_leaf<0, 4> runs its schedule on the scalar unit
+    (sha1_pad_uniform); dead lanes in the last wave, and the empty value."""
+    torch = _torch()
+    _lib, ctx = nkv
+    _bind(torch, ctx)
+    L = _lib.lib()
+    nbytes = stride * n
+    d = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    _lib.check(L.nkv_fill_splitmix64_dev(ctx.h, d.data_ptr(), nbytes, SEED + vlen))
+    d_nodes = torch.zeros(L.nkv_total_nodes(n) * 20, dtype=torch.uint8, device="cuda")
+    _lib.check(L.nkv_tree_from_strided_dev(ctx.h, d.data_ptr(), stride, vlen, n, d_nodes.data_ptr()))
+    torch.cuda.synchronize()
+    host = oracle.splitmix64_bytes(nbytes, SEED + vlen)
+    want = oracle.tree_from_digests(oracle.leaf_hashes_strided(host, stride, vlen, n, threads=8))
+    assert np.array_equal(d_nodes.cpu().numpy().reshape(-1, 20), want)
+
+
 @pytest.mark.parametrize("load", [4, 11])
 def test_strided_every_load_path(nkv, oracle, load):
     torch = _torch()
