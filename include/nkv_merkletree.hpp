@@ -196,8 +196,16 @@ class TaskTeam {
     int size() const { return int(th_.size()) + 1; }
 
     void Run(int parts, const std::function<void(int)>& fn) {
-        if (parts <= 1 || th_.empty()) {
-            for (int k = 0; k < parts; ++k) fn(k);
+        if (parts <= 1 || th_.empty()) {  // every part runs, as on the team
+            std::exception_ptr e;
+            for (int k = 0; k < parts; ++k) {
+                try {
+                    fn(k);
+                } catch (...) {
+                    if (!e) e = std::current_exception();
+                }
+            }
+            if (e) std::rethrow_exception(e);
             return;
         }
         std::unique_lock<std::mutex> g(mu_);
@@ -214,13 +222,27 @@ class TaskTeam {
         // a finished run must not take a part of the next one)
         done_.wait(g, [this] { return left_ == 0 && active_ == 0; });
         fn_ = nullptr;
+        // a part that threw (on any thread): rethrown here, once every thread
+        // has left fn, which lives in the caller's frame
+        if (err_) {
+            std::exception_ptr e = err_;
+            err_ = nullptr;
+            g.unlock();
+            std::rethrow_exception(e);
+        }
     }
 
    private:
     void Claim(const std::function<void(int)>& fn, int parts) {  // take parts until none is left
         for (int k; (k = next_.fetch_add(1)) < parts;) {
-            fn(k);
+            std::exception_ptr e;
+            try {
+                fn(k);
+            } catch (...) {
+                e = std::current_exception();
+            }
             std::lock_guard<std::mutex> g(mu_);
+            if (e && !err_) err_ = e;
             if (--left_ == 0) done_.notify_all();
         }
     }
@@ -250,6 +272,7 @@ class TaskTeam {
     std::atomic<int> next_{0};
     uint64_t gen_ = 0;
     bool stop_ = false;
+    std::exception_ptr err_;  // the first part that threw in the current run
 };
 
 struct MerkleNode;
