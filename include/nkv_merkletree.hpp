@@ -652,18 +652,44 @@ class MerkleTree {  // merkletree.go:13-15
     MerkleTree(const MerkleTree&) = delete;
     MerkleTree& operator=(const MerkleTree&) = delete;
 
-    // merkletree.go:67-92: write the BFS image; O_WRONLY|O_CREAT without O_TRUNC
+    // merkletree.go:67-92: write the BFS image; O_WRONLY|O_CREAT without O_TRUNC.
+    // The image is built in a per-thread buffer kept across calls (no 44 MB
+    // zero fill and page faults per flush at 1 Mi leaves) and written by
+    // nkv_write_file (parallel positioned writes for large images).
     void Serialize(const std::string& fname) {
-        std::vector<uint8_t> img = SerializeBytes();
-        check(nkv_write_file(fname.c_str(), img.data(), img.size()), ("Serialize(" + fname + ")").c_str());
+        thread_local std::vector<uint8_t> buf;
+        const auto t0 = std::chrono::steady_clock::now();
+        const uint64_t total = WalkInto(buf);
+        const auto t1 = std::chrono::steady_clock::now();
+        check(nkv_write_file(fname.c_str(), buf.data(), total), ("Serialize(" + fname + ")").c_str());
+        const auto t2 = std::chrono::steady_clock::now();
+        ser_timing_.walk_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+        ser_timing_.write_ms = std::chrono::duration<double, std::milli>(t2 - t1).count();
+        ser_timing_.bytes = total;
+    }
+    // where the last Serialize's time went (bench.py --config api_flush)
+    struct SerializeTiming {
+        double walk_ms = 0, write_ms = 0;
+        uint64_t bytes = 0;
+    };
+    const SerializeTiming& LastSerializeTiming() const { return ser_timing_; }
+
+    // The image as bytes (the same walk into a fresh vector).
+    std::vector<uint8_t> SerializeBytes() {
+        std::vector<uint8_t> w;
+        w.resize(WalkInto(w));
+        return w;
     }
 
+   private:
     // The queue walk (merkletree.go:75-89).  A FIFO queue visits every node of
     // depth d, in order, before any of depth d + 1, so the walk goes level by
     // level: each level's children and byte counts in parallel chunks (the host
     // team), then the image (merklenode.go:37-63) written in place, chunk by
     // chunk, at offsets known from the counts.  The same bytes as the queue.
-    std::vector<uint8_t> SerializeBytes() {
+    // Writes the image to w[0, total) (w grows if it is smaller, and is never
+    // shrunk or cleared) and returns total.
+    uint64_t WalkInto(std::vector<uint8_t>& w) {
         struct Level {
             std::vector<MerkleNode*> v;
             std::vector<uint64_t> cut, bytes;  // chunk bounds (parts + 1), chunk byte counts
@@ -720,7 +746,7 @@ class MerkleTree {  // merkletree.go:13-15
         uint64_t total = 0;
         for (const Level& L : lv)
             for (uint64_t b : L.bytes) total += b;
-        std::vector<uint8_t> w(total);
+        if (w.size() < total) w.resize(total);
         uint64_t base = 0;
         for (const Level& L : lv) {
             const int parts = int(L.bytes.size());
@@ -742,9 +768,10 @@ class MerkleTree {  // merkletree.go:13-15
             });
             base = at[parts];
         }
-        return w;
+        return total;
     }
 
+   public:
     // merkletree.go:97-157, including its quirk: the loop compares the node
     // counter against the just-emptied queue and stops, so only the root is
     // linked into the tree.
@@ -893,6 +920,7 @@ class MerkleTree {  // merkletree.go:13-15
     std::vector<uint8_t> levels_;
     uint64_t n_ = 0;  // leaves New built the tree from
     NewTiming timing_;
+    SerializeTiming ser_timing_;
 };
 
 inline std::vector<std::vector<uint8_t>> Sha1Many(const std::vector<std::vector<uint8_t>>& msgs) {

@@ -97,6 +97,26 @@ def test_write_file_has_no_truncate(lib, tmp_path):
     assert L.nkv_write_file(str(tmp_path / "no/such/dir/x").encode(), lib.p8(b), 20) == lib.NKV_ERR_IO
 
 
+def test_write_file_parallel_pieces(lib, tmp_path):
+    """Images of 8 MiB and more are written by several threads at their own
+    offsets: the file holds exactly the bytes of one sequential write, a longer
+    stale file keeps its tail (no O_TRUNC), and odd lengths split cleanly."""
+    L = lib.lib()
+    f = str(tmp_path / "big-1-0-metadata.db")
+    rng = np.random.default_rng(7)
+    old = rng.integers(0, 256, (70 << 20) + 13, dtype=np.uint8)
+    assert L.nkv_write_file(f.encode(), lib.p8(old), old.size) == 0
+    assert open(f, "rb").read() == old.tobytes()
+    for n in [(8 << 20) - 1, 8 << 20, (44 << 20) + 40040171 % 997, (64 << 20) + 5]:
+        new = rng.integers(0, 256, n, dtype=np.uint8)
+        assert L.nkv_write_file(f.encode(), lib.p8(new), n) == 0
+        got = open(f, "rb").read()
+        assert len(got) == old.size
+        assert got[:n] == new.tobytes()
+        assert got[n:] == old.tobytes()[n:]
+        old = np.frombuffer(got, np.uint8).copy()
+
+
 def test_no_cpu_fallback_without_device(lib):
     """With no HIP device the product path fails loudly instead of hashing on the CPU."""
     if lib.device_count() > 0:

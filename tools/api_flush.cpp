@@ -19,7 +19,8 @@
 //     upload_ms / kernels_ms / download_ms   its HIP-event split
 //   materialize_ms  New's pointer tree (2n - 1 nodes + pads)
 //   root_ms       Root.String()
-//   walk_ms / write_ms   Serialize: BFS walk of the live tree, file write
+//   walk_ms / write_ms   Serialize(file): BFS walk of the live tree into the
+//                 reused image buffer, the file write (parallel pwrite)
 //
 // Usage: api_flush N VLEN CYCLES DIR [STREAMING=1] [SEED] [NONTEMPORAL=1] [COPY_THREADS=-1] [RETAIN_HEAP=1]
 // (COPY_THREADS -1: the mirror's default, min(16, cores) or NKV_COPY_THREADS.
@@ -103,10 +104,9 @@ int main(int argc, char** argv) {
         const auto t2 = clk::now();
         const std::string root = tree->Root->String();
         const auto t3 = clk::now();
-        const std::vector<uint8_t> img = tree->SerializeBytes();  // Serialize = this walk + the write
-        const auto t4 = clk::now();
-        check(nkv_write_file(fname.c_str(), img.data(), img.size()), "Serialize");
+        tree->Serialize(fname);  // the walk of the live tree + the file write
         const auto t5 = clk::now();
+        const auto& st = tree->LastSerializeTiming();
         float up = -1, ker = -1, down = -1;
         if (nkv_ctx_last_host_timing(S.ctx(), &up, &ker, &down) != NKV_OK) up = ker = down = -1;
         const double total = ms(t0, t5);
@@ -120,7 +120,7 @@ int main(int argc, char** argv) {
             cyc, (unsigned long long)n, (unsigned long long)vlen, int(streaming), int(nontemporal), S.CopyThreads(), int(retain_heap),
             double(n * vlen) / (total * 1e-3) / double(1ull << 30), total, ms(t0, t1),
             tree->LastNewTiming().call_ms, up, ker, down, tree->LastNewTiming().materialize_ms, ms(t2, t3),
-            ms(t3, t4), ms(t4, t5), img.size(), (unsigned long long)S.arena_allocs(), root.c_str());
+            st.walk_ms, st.write_ms, size_t(st.bytes), (unsigned long long)S.arena_allocs(), root.c_str());
         std::fflush(stdout);
     }
     return 0;
