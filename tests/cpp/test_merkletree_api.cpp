@@ -77,6 +77,19 @@ int main(int argc, char** argv) {
             std::fwrite(img.data(), 1, img.size(), f);
             std::fclose(f);
         }
+        // Serialize(file) walks into a reused per-thread buffer (larger after the
+        // bigger trees): the file must hold exactly this tree's image
+        {
+            const std::string fn = dir + "/tree" + std::to_string(n) + "-1-0-metadata.db";
+            std::remove(fn.c_str());
+            t->Serialize(fn);
+            FILE* f = std::fopen(fn.c_str(), "rb");
+            std::vector<uint8_t> got(img.size() + 1);
+            const size_t k = f ? std::fread(got.data(), 1, got.size(), f) : 0;
+            if (f) std::fclose(f);
+            got.resize(k);
+            std::printf("tree%llu_file_eq %d\n", (unsigned long long)n, int(got == img));
+        }
         if (n == 1000) {
             // corrupt one leaf of the materialized tree: Validate must fail
             MerkleNode* leaf = t->Root;
@@ -129,7 +142,19 @@ int main(int argc, char** argv) {
         while (leaf->Left) leaf = leaf->Left;
         leaf->Data.assign(20, 0xAB);
         t->Root->Right->Data[0] ^= 0xFF;
-        std::printf("mut_img %s\n", hex(t->SerializeBytes()).c_str());
+        const auto mimg = t->SerializeBytes();
+        std::printf("mut_img %s\n", hex(mimg).c_str());
+        // Serialize(file) after the 70001-leaf tree: the reused buffer is larger
+        // than this image, the file holds only this image's bytes
+        const std::string fn = dir + "/mut-1-0-metadata.db";
+        std::remove(fn.c_str());
+        t->Serialize(fn);
+        FILE* f = std::fopen(fn.c_str(), "rb");
+        std::vector<uint8_t> got(mimg.size() + 64);
+        const size_t k = f ? std::fread(got.data(), 1, got.size(), f) : 0;
+        if (f) std::fclose(f);
+        got.resize(k);
+        std::printf("mut_file_eq %d\n", int(got == mimg));
     }
     // flushes larger than the arena's stream chunk (32 MiB): settled chunks are
     // copied to the device during the NewLeaf loop; odd value sizes land at

@@ -79,6 +79,9 @@ def test_cpp_mirror_on_gpu(tmp_path, oracle):
         assert int(kv[f"tree{n}_bfs_len"]) == c["bfs_len"]
         assert kv[f"tree{n}_bfs_head"] == c["bfs_head_hex"]
         assert kv[f"tree{n}_validate"] == "1"
+    for n in (1, 2, 3, 255, 256, 257, 1000, 1025, 70001):
+        assert kv[f"tree{n}_file_eq"] == "1"  # Serialize(file) == SerializeBytes()
+    assert kv["mut_file_eq"] == "1"  # a smaller image after a larger one
     assert kv["tree1000_corrupt_validate"] == "0"
     # a tree New materializes on several threads (70001 leaves of 64 bytes)
     data = oracle.splitmix64_bytes(70001 * 64, 0x6E616B65 + 70001)
