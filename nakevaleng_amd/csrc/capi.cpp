@@ -12,7 +12,6 @@
 #include <algorithm>
 #include <cmath>
 #include <new>
-#include <thread>
 #include <vector>
 
 #include "context.hpp"
@@ -993,46 +992,22 @@ int nkv_bloom_from_records(nkv_ctx* c, const uint8_t* stream, uint64_t stream_le
     return st(hipStreamSynchronize(c->stream));
 } NKV_CATCH
 
-// bytes [lo, hi) of data at file offset lo
-static bool write_range(int fd, const uint8_t* data, uint64_t lo, uint64_t hi) {
-    while (lo < hi) {
-        const ssize_t w = pwrite(fd, data + lo, size_t(std::min<uint64_t>(hi - lo, 1ull << 30)), off_t(lo));
-        if (w <= 0) return false;
-        lo += uint64_t(w);
-    }
-    return true;
-}
-
 int nkv_write_file(const char* fname, const uint8_t* data, uint64_t len) try {
     if (!fname || (!data && len)) return NKV_ERR_INVALID;
     int fd = open(fname, O_WRONLY | O_CREAT, 0666);  // no O_TRUNC: merkletree.go:68
     if (fd < 0) return NKV_ERR_IO;
-    // A large image is written by several threads at their own offsets (the
-    // copy into the page cache is what a single write() spends its time on);
-    // the bytes and offsets are those of one sequential write.
-    constexpr uint64_t kPiece = uint64_t(8) << 20;
-    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    const int parts = int(std::min<uint64_t>(std::min<unsigned>(8, hw), len / kPiece));
-    bool ok = true;
-    if (parts <= 1) {
-        ok = write_range(fd, data, 0, len);
-    } else {
-        std::vector<char> good(parts, 0);
-        std::vector<std::thread> th;
-        th.reserve(parts);
-        auto part = [&](int k) { good[k] = write_range(fd, data, len * k / parts, len * (k + 1) / parts); };
-        int started = 1;  // parts 1 .. started - 1 run on threads
-        try {
-            for (int k = 1; k < parts; ++k, ++started) th.emplace_back(part, k);
-        } catch (...) {  // no thread: the rest on this one
+    // one sequential write (positioned writes from several threads measured no
+    // faster: buffered writes to one file serialise on its inode lock)
+    uint64_t done = 0;
+    while (done < len) {
+        ssize_t w = write(fd, data + done, size_t(std::min<uint64_t>(len - done, 1ull << 30)));
+        if (w <= 0) {
+            close(fd);
+            return NKV_ERR_IO;
         }
-        for (int k = started; k < parts; ++k) part(k);
-        part(0);
-        for (auto& t : th) t.join();
-        for (char g : good) ok = ok && g;
+        done += uint64_t(w);
     }
-    const bool closed = close(fd) == 0;
-    return ok && closed ? NKV_OK : NKV_ERR_IO;
+    return close(fd) == 0 ? NKV_OK : NKV_ERR_IO;
 } NKV_CATCH
 
 // ---- device-resident API ----

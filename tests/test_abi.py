@@ -97,10 +97,9 @@ def test_write_file_has_no_truncate(lib, tmp_path):
     assert L.nkv_write_file(str(tmp_path / "no/such/dir/x").encode(), lib.p8(b), 20) == lib.NKV_ERR_IO
 
 
-def test_write_file_parallel_pieces(lib, tmp_path):
-    """Images of 8 MiB and more are written by several threads at their own
-    offsets: the file holds exactly the bytes of one sequential write, a longer
-    stale file keeps its tail (no O_TRUNC), and odd lengths split cleanly."""
+def test_write_file_large(lib, tmp_path):
+    """Images of tens of MiB: the file holds exactly the bytes written, and a
+    longer stale file keeps its tail (no O_TRUNC)."""
     L = lib.lib()
     f = str(tmp_path / "big-1-0-metadata.db")
     rng = np.random.default_rng(7)

@@ -19,8 +19,8 @@
 //     upload_ms / kernels_ms / download_ms   its HIP-event split
 //   materialize_ms  New's pointer tree (2n - 1 nodes + pads)
 //   root_ms       Root.String()
-//   walk_ms / write_ms   Serialize(file): BFS walk of the live tree into the
-//                 reused image buffer, the file write (parallel pwrite)
+//   walk_ms / write_ms   Serialize(file): BFS walk of the live tree, the file
+//                 write (MerkleTree::LastSerializeTiming)
 //
 // Usage: api_flush N VLEN CYCLES DIR [STREAMING=1] [SEED] [NONTEMPORAL=1] [COPY_THREADS=-1] [RETAIN_HEAP=1]
 // (COPY_THREADS -1: the mirror's default, min(16, cores) or NKV_COPY_THREADS.
