@@ -189,6 +189,9 @@ def parse(argv=None):
                          "per table, pipelined behind the next table (step)")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="do not record per-kernel HIP events inside the timed loop")
+    ap.add_argument("--timing-every", type=int, default=1,
+                    help="record the kernel-timing events on every k-th step of the timed loop only "
+                         "(NKV_OPT_TIMING_EVERY; each record is a packet between two kernels)")
     ap.add_argument("--no-capi", action="store_true",
                     help="no capi_group / capi_one_tree sub-records (by default rank 0 runs the one-process C-ABI "
                          "group over the same N GPUs in a fresh child process once the ranks are done)")
@@ -755,6 +758,7 @@ def run_ranks(args, T):
     if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
+    ctx.set_option(_lib.NKV_OPT_TIMING_EVERY, max(1, args.timing_every))
     ctx.set_timing(not args.no_kernel_timing, clock=not args.no_clock)
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -1047,6 +1051,7 @@ def main_capi(args, T):
     for _ in range(args.warmup):
         step()
     grp.sync()
+    ctxs[0].set_option(_lib.NKV_OPT_TIMING_EVERY, max(1, args.timing_every))
     ctxs[0].set_timing(not args.no_kernel_timing, clock=not args.no_clock)
     t0 = time.perf_counter()
     for _ in range(args.steps):

@@ -133,6 +133,11 @@ int nkv_ctx_sync(nkv_ctx *ctx);
 #define NKV_OPT_TABLE_LANES 12 /* nkv_trees_dev: streams the tables of one call are spread
                                   over (1..8, default 2), so one table's leaf kernel runs
                                   while the previous one finishes and reduces */
+#define NKV_OPT_TIMING_EVERY 13 /* NKV_TIMING_EVENTS on every k-th tree call only (1..10^6,
+                                   default 1; counted from nkv_ctx_set_timing): each event
+                                   record is a packet on the stream between two kernels,
+                                   so a timed loop samples its kernel times instead of
+                                   carrying three records per call */
 int nkv_ctx_set_option(nkv_ctx *ctx, int key, int64_t value);
 /* Timing (nkv_ctx_set_timing flags).  NKV_TIMING_EVENTS: the tree calls record
  * HIP events around the leaf kernel and the tree reduce on the context's

@@ -30,6 +30,7 @@ NKV_OPT_STAGE_CHUNK = 8
 NKV_OPT_BLOOM_PATH = 10
 NKV_OPT_RECORDS_FUSED = 11
 NKV_OPT_TABLE_LANES = 12
+NKV_OPT_TIMING_EVERY = 13
 NKV_TIMING_EVENTS = 1
 NKV_TIMING_CLOCK = 2
 NKV_TABLE_STRIDED = 0

@@ -219,6 +219,8 @@ int finish_tree(nkv_ctx* c, uint8_t* nodes, uint64_t n, uint8_t* root20, uint8_t
 // call (no host sync) so a timed loop can be summarised afterwards.
 int mark(nkv_ctx* c, int which) {
     if (!c->timing) return NKV_OK;
+    if (which == 0) c->sampled = c->timing_calls++ % uint64_t(c->timing_every) == 0;
+    if (!c->sampled) return NKV_OK;
     if (which == 0) {
         if (c->ring_used + 3 > nkv_ctx::kTimingRing) c->ring_used = 0;  // restart the window
         if (c->ring_used + 3 > c->ring.size()) {
@@ -242,6 +244,13 @@ int mark(nkv_ctx* c, int which) {
 // split it into upload, kernels and download (nkv_ctx_last_host_timing).
 int host_mark(nkv_ctx* c, int which) {
     if (!c->timing) return NKV_OK;
+    // which 0 comes before the call's mark(0): the call is sampled when the
+    // count it is about to take is
+    const bool sampled = which == 0 ? c->timing_calls % uint64_t(c->timing_every) == 0 : c->sampled;
+    if (!sampled) {
+        c->host_timed = false;
+        return NKV_OK;
+    }
     if (!c->host_ev[which]) HIPTRY(hipEventCreate(&c->host_ev[which]));
     HIPTRY(hipEventRecord(c->host_ev[which], c->stream));
     if (which == 1) c->host_timed = c->timed;
@@ -547,6 +556,11 @@ int nkv_ctx_set_option(nkv_ctx* c, int key, int64_t value) try {
             if (value < 1 || value > 8) return NKV_ERR_INVALID;
             c->table_lanes = int(value);
             return NKV_OK;
+        case NKV_OPT_TIMING_EVERY:
+            if (value < 1 || value > 1000000) return NKV_ERR_INVALID;
+            c->timing_every = int(value);
+            c->timing_calls = 0;
+            return NKV_OK;
         default:
             return NKV_ERR_INVALID;
     }
@@ -563,10 +577,12 @@ int nkv_ctx_set_timing(nkv_ctx* c, int enable) try {
     c->timing = (enable & NKV_TIMING_EVENTS) != 0;
     c->timed = false;
     c->ring_used = 0;
+    c->timing_calls = 0;
     for (nkv_ctx* l : c->lanes) {
         l->timing = c->timing;
         l->timed = false;
         l->ring_used = 0;
+        l->timing_calls = 0;
     }
     if (enable & NKV_TIMING_CLOCK) {
         TRY(grow(c->d_clk, kClockWords * sizeof(unsigned long long)));

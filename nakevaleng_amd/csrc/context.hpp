@@ -130,6 +130,11 @@ struct nkv_ctx {
     int table_lanes = 2;    // NKV_OPT_TABLE_LANES
     bool timing = false;
     bool timed = false;
+    // NKV_OPT_TIMING_EVERY: the tree calls record their events on every k-th
+    // call only (counted from nkv_ctx_set_timing); sampled: the current call
+    int timing_every = 1;
+    uint64_t timing_calls = 0;
+    bool sampled = true;
     // per-call event triples (leaf start, leaf end / reduce start, reduce end),
     // the latest kTimingRing / 3 calls
     static constexpr size_t kTimingRing = 3 * 65536;

@@ -39,10 +39,12 @@ void copy_options(const nkv_ctx* from, nkv_ctx* to) {
     to->queue_waves = from->queue_waves;
     to->crc_load = from->crc_load;
     to->records_fused = from->records_fused;
-    if (to->timing != from->timing) {
+    if (to->timing != from->timing || to->timing_every != from->timing_every) {
         to->timing = from->timing;
+        to->timing_every = from->timing_every;
         to->timed = false;
         to->ring_used = 0;
+        to->timing_calls = 0;
     }
 }
 

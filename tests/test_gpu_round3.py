@@ -520,6 +520,45 @@ def test_host_call_timing_and_clock_probe(nkv, oracle):
     assert nb[-20:].cpu().numpy().tobytes() == want[-1].tobytes()
 
 
+def test_timing_every_kth_call(nkv, oracle):
+    """NKV_OPT_TIMING_EVERY k: only calls 0, k, 2k, ... since set_timing record
+    events (the timed loop's sampling); out-of-range k refused; results unchanged."""
+    _lib, ctx = nkv
+    L = _lib.lib()
+    n, vl = 20000, 256
+    d = torch.empty(n * vl, dtype=torch.uint8, device="cuda")
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    _lib.check(L.nkv_fill_splitmix64_dev(ctx.h, d.data_ptr(), n * vl, 11))
+    nb = nodes_buf(L, n)
+    assert L.nkv_ctx_set_option(ctx.h, _lib.NKV_OPT_TIMING_EVERY, 0) == _lib.NKV_ERR_INVALID
+    try:
+        for k, calls, want_sampled in ((3, 7, 3), (1, 4, 4), (8, 20, 3)):
+            ctx.set_option(_lib.NKV_OPT_TIMING_EVERY, k)
+            ctx.set_timing(True)
+            for _ in range(calls):
+                _lib.check(L.nkv_tree_from_strided_dev(ctx.h, d.data_ptr(), vl, vl, n, nb.data_ptr()))
+            got, leaf_ms, reduce_ms = ctx.timing_summary()
+            assert got == want_sampled, (k, got)
+            assert leaf_ms > 0 and reduce_ms > 0
+            # a host call that is not sampled has no host timing; a sampled one has
+            ctx.set_option(_lib.NKV_OPT_TIMING_EVERY, 2)
+            ctx.set_timing(True)
+            base, off, ln = ragged(3000, 4)
+            root = np.zeros(20, np.uint8)
+            a, b, c = ctypes.c_float(), ctypes.c_float(), ctypes.c_float()
+            for i in range(3):
+                _lib.check(L.nkv_tree_from_values(ctx.h, _lib.p8(base), _lib.p64(off), _lib.p64(ln), 3000,
+                                                  _lib.p8(root), None, None))
+                rc = L.nkv_ctx_last_host_timing(ctx.h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
+                assert rc == (_lib.NKV_OK if i % 2 == 0 else _lib.NKV_ERR_INVALID), (i, rc)
+            assert root.tobytes() == want_tree(oracle, base, off, ln)[-1].tobytes()
+    finally:
+        ctx.set_timing(False)
+        ctx.set_option(_lib.NKV_OPT_TIMING_EVERY, 1)
+    want = oracle.tree_from_digests(oracle.leaf_hashes_strided(d.cpu().numpy(), vl, vl, n, threads=8))
+    assert nb[-20:].cpu().numpy().tobytes() == want[-1].tobytes()
+
+
 def test_python_mirror_serialize_reads_the_live_tree(nkv, oracle):
     """merkletree.go:75-89 walks the live tree: after New, a leaf's and an
     interior node's Data changed through Root show in the image exactly as the
