@@ -149,9 +149,12 @@ int nkv_ctx_set_option(nkv_ctx *ctx, int key, int64_t value);
 #define NKV_TIMING_EVENTS 1
 #define NKV_TIMING_CLOCK 2
 int nkv_ctx_set_timing(nkv_ctx *ctx, int flags);
+/* the latest tree call that recorded events (every call, or every k-th under
+ * NKV_OPT_TIMING_EVERY) */
 int nkv_ctx_last_timing(nkv_ctx *ctx, float *leaf_ms, float *reduce_ms);
 /* the latest nkv_tree_from_values under NKV_TIMING_EVENTS: upload (host values ->
- * HBM), kernels (leaf + tree), download (outputs -> host) */
+ * HBM), kernels (leaf + tree), download (outputs -> host); NKV_ERR_INVALID when
+ * that call was not sampled (NKV_OPT_TIMING_EVERY) */
 int nkv_ctx_last_host_timing(nkv_ctx *ctx, float *upload_ms, float *kernels_ms, float *download_ms);
 /* NKV_TIMING_CLOCK: the lifetime-weighted mean shader clock of the leaf-kernel
  * waves since the flag was set, and how many waves reported (synchronizes). */
