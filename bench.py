@@ -482,8 +482,9 @@ def valu_ceiling(mhz, kind):
 
 def pmc_traffic(args, n, vlen, nbytes):
     """PMC-measured HBM bytes of this config's leaf kernel, per launch (separate
-    rocprofv3 passes: tools/pmc_sizes.sh for cfg2, tools/pmc_config.sh for the others)."""
-    cfg2_pmc = {0: "pmc_traffic_cfg2_runs.json", 4: "pmc_traffic_cfg2_runs.json",
+    rocprofv3 passes, tools/pmc_config.sh; cfg2 on round 4's build,
+    tools/r04_pmc_cfg2.sh)."""
+    cfg2_pmc = {0: "pmc_traffic_cfg2_r04.json", 4: "pmc_traffic_cfg2_r04.json",
                 1: "pmc_traffic.json"}.get(args.leaf_load)
     pmc_name = {"sstable4k": cfg2_pmc, "runs4": cfg2_pmc, "records": "pmc_traffic_records.json",
                 "mixed": "pmc_traffic_mixed.json", "records_verify": "pmc_traffic_records_verify.json"}.get(args.config)
