@@ -144,7 +144,7 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", choices=["sstable4k", "mixed", "records", "records_verify", "one_tree", "runs4",
-                                         "api_flush"],
+                                         "api_flush", "small_flush"],
                     default="sstable4k",
                     help="sstable4k = BASELINE configs[1] (the metric); mixed = configs[2]; records = the "
                          "compaction form: 1 Mi serialized 4 KiB records in a Data table, values located "
@@ -152,7 +152,10 @@ def parse(argv=None):
                          "record's Crc checked (nkv_tree_verify_records_dev); runs4 = configs[3] per GPU: "
                          "lsm_run_max = 4 tables of 1 Mi x 4 KiB per step (sstable4k with --tables 4); "
                          "api_flush = the host-inclusive flush through the C++ Go-API mirror: NewLeaf x n "
-                         "from host memory, New, Root, Serialize to a fresh file (tools/api_flush.cpp)")
+                         "from host memory, New, Root, Serialize to a fresh file (tools/api_flush.cpp); "
+                         "small_flush = microseconds per flush at the reference's default sizes (10 values "
+                         "<= 200 B) up to configs[0], GPU paths beside one host core (tools/small_flush.cpp)")
+    ap.add_argument("--small-reps", type=int, default=300, help="small_flush: flushes per shape and mode")
     ap.add_argument("--api-cycles", type=int, default=4, help="api_flush: flushes per mode (the first allocates "
                                                               "the pinned arena)")
     ap.add_argument("--tables", type=int, default=0,
@@ -198,46 +201,133 @@ def parse(argv=None):
     ap.add_argument("--capi-timeout", type=int, default=150,
                     help="seconds per C-ABI group child (a healthy 8-GPU child takes well under a minute; a hung "
                          "one must not cost the run its line)")
+    ap.add_argument("--no-subconfigs", action="store_true",
+                    help="no config2_mixed / config1_records sub-records (by default the N = 1 configs[1] line "
+                         "runs both in fresh children, each with its own roofline and CPU baseline)")
+    ap.add_argument("--child-budget-s", type=int, default=360,
+                    help="seconds after the ranks finish within which the sub-config children must start")
     return ap.parse_args(argv)
 
 
-def cpu_baseline(n_leaves: int, vlen: int) -> dict:
-    """The oracle (C restatement of ds/merkletree, one thread, like the Go reference)."""
+_T0 = time.perf_counter()
+
+
+def progress(msg: str) -> None:
+    """One progress line on stderr (a long run shows it is alive)."""
+    print(f"bench.py [{time.perf_counter() - _T0:7.1f} s] {msg}", file=sys.stderr, flush=True)
+
+
+def host_threads() -> int:
+    """Host threads this process may use: its affinity set, capped by
+    OMP_NUM_THREADS (the GPU box gives a one-GPU job 16 of its cores)."""
+    return max(1, min(int(os.environ.get("OMP_NUM_THREADS", "16") or 16), len(os.sched_getaffinity(0))))
+
+
+def cpu_model() -> str:
+    """The host CPU's model name (/proc/cpuinfo, what lscpu prints)."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def cpu_sample(args, rank: int = 0) -> dict:
+    """The host-memory form of the workload the GPU line measured (rank `rank`'s
+    first table, same seeds and layout as build_tables), bounded to
+    --cpu-sample-leaves values (the mixed batch whole: its leaves are ragged,
+    so a prefix would be a different workload).  Keys: data, n, nbytes and
+    either (stride, L) or (off, lens); `text` says what it is."""
     import numpy as np
     from oracle import oracle_c as oc
+    cfg = args.config
+    if cfg == "mixed":
+        lens, off = mixed_lengths(args.mixed_bytes, SEED_MIXED + rank)
+        nbytes = int(lens.sum())
+        return {"data": oc.splitmix64_bytes(nbytes, SEED_MIXED + rank), "off": off, "lens": lens, "n": len(lens),
+                "nbytes": nbytes, "text": f"BASELINE configs[2]'s batch: {len(lens)} values of 64 B - 64 KiB "
+                                          f"({nbytes} B, splitmix64 seed {SEED_MIXED + rank:#x})"}
+    n = min(args.cpu_sample_leaves, args.leaves)
+    if cfg in ("records", "records_verify"):
+        rb, ks = args.value_bytes, args.key_bytes
+        vlen = rb - 30 - ks
+        # the Values sit at rec + 30 + KeySize (record.go:191-199); the header
+        # words build_tables writes do not overlap them
+        off = np.arange(n, dtype=np.uint64) * rb + 30 + ks
+        return {"data": oc.splitmix64_bytes(n * rb, SEED + rank), "off": off, "lens": np.full(n, vlen, np.uint64),
+                "n": n, "nbytes": n * vlen,
+                "text": f"{n} serialized {rb}-B records ({ks}-B key, {vlen}-B value; splitmix64 seed "
+                        f"{SEED + rank:#x}), the values hashed in place"}
+    vlen = args.value_bytes
+    return {"data": oc.splitmix64_bytes(n * vlen, SEED + rank), "stride": vlen, "L": vlen, "n": n,
+            "nbytes": n * vlen, "text": f"{n} x {vlen} B values (splitmix64 seed {SEED + rank:#x})"}
+
+
+# The four CPU variants of SURVEY.md 8(d): the portable C restatement
+# (oracle/merkle_oracle.c, the reference's statements) and OpenSSL's SHA-1
+# (oracle/merkle_openssl.c, libcrypto: SHA-NI where the host has it, the
+# stand-in for Go's assembly crypto/sha1), each on one thread (the reference
+# is single-threaded) and on every host thread this process may use.
+CPU_VARIANTS = (("port_1core", "port", False), ("openssl_1core", "openssl", False),
+                ("port_all_cores", "port", True), ("all_cores_openssl", "openssl", True))
+
+
+def cpu_baseline(args, rank: int = 0) -> dict:
+    """Leaf hash + full tree of cpu_sample() on the host, every variant of
+    CPU_VARIANTS timed on the same bytes.  `value` is the STRONGEST figure
+    (`best` names it), so every GPU/CPU ratio is against the best CPU; the
+    one-core port is the reference-shaped figure.  Every variant's root must
+    agree."""
+    from oracle import oracle_c as oc
     oc.build()
-    data = oc.splitmix64_bytes(n_leaves * vlen, SEED)
-    t0 = time.perf_counter()
-    leaves = oc.leaf_hashes_strided(data, vlen, vlen, n_leaves, threads=1)
-    nodes = oc.tree_from_digests(leaves)
-    dt = time.perf_counter() - t0
-    # SURVEY 8(d) variant 2: the same port with the leaves spread over the host
-    # cores this process may use (the box caps a GPU job's share at 16)
-    threads = max(1, min(int(os.environ.get("OMP_NUM_THREADS", "16") or 16), len(os.sched_getaffinity(0))))
-    t3 = time.perf_counter()
-    leaves_mt = oc.leaf_hashes_strided(data, vlen, vlen, n_leaves, threads=threads)
-    nodes_mt = oc.tree_from_digests(leaves_mt)
-    dt3 = time.perf_counter() - t3
-    assert nodes_mt[-1].tobytes() == nodes[-1].tobytes()
-    # informational: OpenSSL SHA-1 (hashlib) on one core over a 256 MiB slice
-    k = min(n_leaves, (256 << 20) // vlen)
-    t1 = time.perf_counter()
-    for i in range(k):
-        hashlib.sha1(memoryview(data)[i * vlen:(i + 1) * vlen]).digest()
-    dt2 = time.perf_counter() - t1
-    del data
+    s = cpu_sample(args, rank)
+    data, n, nbytes = s["data"], s["n"], s["nbytes"]
+    threads = host_threads()
+    out, roots = {}, set()
+    for name, impl, allc in CPU_VARIANTS:
+        t = threads if allc else 1
+        t0 = time.perf_counter()
+        if impl == "port":
+            leaves = (oc.leaf_hashes_strided(data, s["stride"], s["L"], n, threads=t) if "stride" in s
+                      else oc.leaf_hashes(data, s["off"], s["lens"], threads=t))
+            nodes = oc.tree_from_digests(leaves, threads=t)
+        else:
+            leaves = (oc.ossl_leaf_hashes_strided(data, s["stride"], s["L"], n, threads=t) if "stride" in s
+                      else oc.ossl_leaf_hashes(data, s["off"], s["lens"], threads=t))
+            nodes = oc.ossl_tree_from_digests(leaves, threads=t)
+        dt = time.perf_counter() - t0
+        roots.add(nodes[-1].tobytes().hex())
+        out[name] = {"value": round(nbytes / dt / 2**30, 4), "cores": t, "seconds": round(dt, 3)}
+        progress(f"cpu_baseline {args.config} {name}: {out[name]['value']} GiB/s")
+        del leaves, nodes
+    if len(roots) != 1:
+        raise SystemExit(f"bench.py: the CPU variants disagree on the root ({sorted(roots)})")
+    best = max(out, key=lambda k: out[k]["value"])
     return {
-        "value": round(n_leaves * vlen / dt / 2**30, 4),
+        "value": out[best]["value"],
         "unit": "GiB/s",
-        "cores": 1,
+        "cores": out[best]["cores"],
         "kind": "port",
-        "sample": f"{n_leaves} x {vlen} B values (splitmix64 seed {SEED:#x}), leaf hash + full tree, "
-                  f"oracle/merkle_oracle.c single thread, {dt:.2f} s",
-        "root": nodes[-1].tobytes().hex(),
-        "openssl_leaf_hash_1core_GiBps": round(k * vlen / dt2 / 2**30, 4),
-        "all_cores": {"value": round(n_leaves * vlen / dt3 / 2**30, 4), "unit": "GiB/s", "cores": threads,
-                      "sample": "the same sample, leaves over pthreads, tree on one thread"},
+        "best": best,
+        "sample": s["text"] + ", leaf hash + full tree",
+        "cpu_model": cpu_model(),
+        "host_threads": threads,
+        "root": roots.pop(),
+        **out,
     }
+
+
+def vs_cpu(value, cpu) -> dict:
+    """GPU/CPU ratios of a line: against the strongest CPU figure and the
+    reference-shaped one (one core, portable SHA-1)."""
+    if not cpu or not value:
+        return {}
+    return {"vs_cpu_best": round(value / cpu["value"], 2),
+            "vs_cpu_port_1core": round(value / cpu["port_1core"]["value"], 2)}
 
 
 def launcher_cmd(argv, n: int, port: int):
@@ -579,12 +669,15 @@ def main():
         return main_capi(args, T)
     if args.config == "api_flush":
         return main_api_flush(args)
+    if args.config == "small_flush":
+        return main_small_flush(args)
     rc = ensure_ranks(args, sys.argv[1:])
     if rc is not None:
         sys.exit(rc)
     out = run_ranks(args, T)
     if out is None:  # not rank 0: done
         return
+    progress(f"{args.config}: ranks done, {out.get('value')} GiB/s")
     import gc
     import torch
     gc.collect()  # the tables and their closures hold this run's device buffers
@@ -593,8 +686,13 @@ def main():
     # the same N GPUs (SURVEY 8e's process model, what the Go drop-in would use;
     # VERDICT r03 item 1), each in a fresh child process, then the CPU baseline.
     world = out["n_gpus"]
+    t_start = time.perf_counter()
+
+    def budget_left():  # the driver allows the whole run 600 s; keep the children well inside it
+        return args.child_budget_s - (time.perf_counter() - t_start)
     if not args.no_capi and args.config in ("sstable4k", "runs4"):
         out["capi_group"] = capi_child(args, world, [], args.capi_timeout)
+        progress("capi_group child done")
         if args.config == "sstable4k":
             if "error" in out["capi_group"]:  # the same group would fail again: no second wait
                 out["capi_one_tree"] = {"error": "skipped: the group child failed"}
@@ -606,11 +704,55 @@ def main():
                     # BASELINE configs[4]'s per-GPU table: 8 Mi x 4 KiB = 32 GiB on each GPU
                     out["capi_config4"] = capi_child(args, world, ["--leaves", str(8 << 20), "--tables", "1"],
                                                      args.capi_timeout)
-    if not args.no_cpu_baseline and args.config in ("sstable4k", "runs4"):
+    if not args.no_subconfigs and args.config == "sstable4k" and world == 1 and T == 1 \
+            and (args.leaves, args.value_bytes) == (1 << 20, 4096):
+        # The other single-GPU BASELINE workloads, each a
+        # fresh child with its own roofline, verification and CPU baseline on
+        # the same sample: configs[2] (mixed) and the serialized-record form of
+        # configs[1] (the literal sstable.go:58-74 / lsmtree.go:210-211 input).
+        for key, cfg in SUBCONFIGS:
+            left = budget_left()
+            if left < 60:
+                out[key] = {"error": f"skipped: {args.child_budget_s} s child budget spent"}
+                continue
+            out[key] = sub_child(args, cfg, int(min(args.capi_timeout, left)))
+            progress(f"{key} child done: {out[key].get('value', out[key].get('error'))}")
+    if not args.no_cpu_baseline:
         # at every N, on rank 0 once the ranks are done (the Go reference is
         # one process on the same host)
-        out["cpu_baseline"] = cpu_baseline(min(args.cpu_sample_leaves, args.leaves), args.value_bytes)
+        out["cpu_baseline"] = cpu_baseline(args)
+        out.update(vs_cpu(out.get("value"), out["cpu_baseline"]))
     print(json.dumps(out), flush=True)
+
+
+# sub-record key -> the child's --config (bench.py --gpus 1 only)
+SUBCONFIGS = (("config2_mixed", "mixed"), ("config1_records", "records"))
+SUB_KEYS = ("value", "unit", "n_gpus", "steps", "ms_per_step", "sclk_mhz", "roofline", "kernel_ms",
+            "verified_vs_oracle", "verified_basis", "root", "cpu_baseline", "vs_cpu_best", "vs_cpu_port_1core")
+
+
+def sub_child(args, config, timeout, run=None):
+    """Run `bench.py --config <config> --gpus 1` (this run's step flags) in a
+    fresh child and return the keys of its line that go into the parent's line
+    (or {"error": ...}: a failed child never costs the parent its line)."""
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in CHILD_ENV_DROP}
+    env["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    cmd = [sys.executable, os.path.abspath(__file__)] + list(sys.argv[1:]) + [
+        "--config", config, "--gpus", "1", "--tables", "1", "--no-capi", "--no-subconfigs"]
+    t0 = time.perf_counter()
+    try:
+        p = (run or subprocess.run)(cmd, stdout=subprocess.PIPE, text=True, timeout=timeout, env=env)
+    except subprocess.TimeoutExpired:
+        return {"error": f"timed out after {timeout} s", "cmd": " ".join(cmd[1:])}
+    lines = [x for x in (p.stdout or "").splitlines() if x.startswith("{")]
+    if p.returncode != 0 or not lines:
+        return {"error": f"exit status {p.returncode}", "cmd": " ".join(cmd[1:])}
+    d = json.loads(lines[-1])
+    sub = {k: d[k] for k in SUB_KEYS if k in d}
+    sub["workload"] = d.get("config", {}).get("workload")
+    sub["wall_s"] = round(time.perf_counter() - t0, 1)
+    return sub
 
 
 CHILD_ENV_DROP = ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE",
@@ -935,13 +1077,20 @@ def main_api_flush(args):
     n, vlen = args.leaves, args.value_bytes
     runs = {}
     with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
-        for mode, threads, retain in (("pool", -1, 1), ("caller_thread", 0, 1), ("pool_glibc_heap", -1, 0)):
-            out = subprocess.run([exe, str(n), str(vlen), str(max(2, args.api_cycles)), td, "1", hex(SEED), "1",
-                                  str(threads), str(retain)], capture_output=True, text=True, timeout=900)
+        for mode, threads, retain, reserve in (("pool", -1, 1, 1), ("caller_thread", 0, 1, 1),
+                                               ("pool_glibc_heap", -1, 0, 1), ("pool_no_reserve", -1, 1, 0)):
+            out = subprocess.run([exe, str(n), str(vlen), str(max(3, args.api_cycles)), td, "1", hex(SEED), "1",
+                                  str(threads), str(retain), str(reserve)], capture_output=True, text=True,
+                                 timeout=900)
             if out.returncode != 0:
                 raise SystemExit(f"api_flush failed: {out.stderr[-2000:]}")
             runs[mode] = [json.loads(x) for x in out.stdout.splitlines() if x.startswith("{")]
-    best = {m: max(r[1:], key=lambda c: c["gib_s"]) for m, r in runs.items()}
+    # the steady state is the MEDIAN of the cycles after the first (VERDICT r04
+    # item 3), reported beside the first (cold) and the best cycle
+    def median_cycle(r):
+        rest = sorted(r[1:], key=lambda c: c["gib_s"])
+        return rest[(len(rest) - 1) // 2]
+    best = {m: median_cycle(r) for m, r in runs.items()}
     root = best["pool"]["root"]
     # every cycle's root against the committed oracle root (1 Mi x 4 KiB), else
     # the oracle at run time under --verify
@@ -952,8 +1101,9 @@ def main_api_flush(args):
         want = oc.tree_from_digests(oc.leaf_hashes_strided(host, vlen, vlen, n, threads=16))[-1].tobytes().hex()
         del host
     verified = None if want is None else all(c["root"] == want for r in runs.values() for c in r)
-    cpu = None if args.no_cpu_baseline else cpu_baseline(n, vlen)
+    cpu = None if args.no_cpu_baseline else cpu_baseline(args)
     b, c0 = best["pool"], best["caller_thread"]
+    first, top = runs["pool"][0], max(runs["pool"][1:], key=lambda c: c["gib_s"])
     keys = ("newleaf_ms", "new_call_ms", "upload_ms", "kernels_ms", "download_ms", "materialize_ms", "root_ms",
             "walk_ms", "write_ms", "total_ms")
     out = {
@@ -969,7 +1119,19 @@ def main_api_flush(args):
         "config": {"workload": f"memtable flush: {n} x {vlen} B values, sstable.go:58-74 call sequence",
                    "leaves": n, "value_bytes": vlen, "copy_threads": b.get("copy_threads"),
                    "heap": "retained between flushes (M_MMAP_THRESHOLD 1 GiB, no trim), as a Go GC heap"},
+        "value_basis": "median of the flushes after the first (steady state)",
         "breakdown_ms": {k: b[k] for k in keys},
+        # the first flush of the process (arena and node storage allocated,
+        # pages faulted in) and the best steady one
+        "first_flush": {"gib_s": first["gib_s"], "arena_allocs": first.get("arena_allocs"),
+                        **{k: first[k] for k in keys}},
+        "first_over_steady_time": round(first["total_ms"] / b["total_ms"], 3),
+        "reserve_ms": first.get("reserve_ms"),
+        # the same without Session::Reserve: the first flush grows the arena
+        "first_flush_no_reserve": {"gib_s": runs["pool_no_reserve"][0]["gib_s"],
+                                   "arena_allocs": runs["pool_no_reserve"][0].get("arena_allocs"),
+                                   **{k: runs["pool_no_reserve"][0][k] for k in keys}},
+        "best_flush": {"gib_s": top["gib_s"], **{k: top[k] for k in keys}},
         "copies_on_caller_thread": {"gib_s": c0["gib_s"], **{k: c0[k] for k in keys}},
         # the same flush with glibc's default heap policy (every freed block over
         # 32 MiB unmapped: the next flush page-faults it again)
@@ -980,9 +1142,114 @@ def main_api_flush(args):
         "verified_vs_oracle": verified,
         "cpu_baseline": cpu,
     }
-    if cpu:
-        out["vs_cpu_all_cores"] = round(b["gib_s"] / cpu["all_cores"]["value"], 3)
-        out["vs_cpu_one_core"] = round(b["gib_s"] / cpu["value"], 3)
+    out.update(vs_cpu(b["gib_s"], cpu))
+    print(json.dumps(out), flush=True)
+
+
+# --config small_flush: (name, n, min value length, max value length); lengths
+# uniform in [min, max], seed SMALL_SEED (tools/small_flush.cpp's generator)
+SMALL_SEED = 0x6E616B67
+SMALL_SHAPES = (
+    ("flush_default", 10, 1, 200),     # MEMTABLE_CAPACITY = 10 under the 2 KB threshold (coreconf.go:33-34)
+    ("compaction_default", 40, 1, 200),  # LSM_RUN_MAX = 4 such runs merged (coreconf.go:39)
+    ("n100", 100, 1, 200),
+    ("n256", 256, 1, 200),
+    ("n1024", 1024, 1, 200),
+    ("config0", 1024, 1024, 1024),     # BASELINE configs[0]: 1 Ki x 1 KiB
+    ("n256_4k", 256, 4096, 4096),
+    ("n1024_4k", 1024, 4096, 4096),    # 4 MiB: above the small path's 1 MiB bound
+)
+
+
+def small_shape_values(n, lo, hi, seed=SMALL_SEED):
+    """tools/small_flush.cpp's memtable: len[i] = lo + splitmix(i) % (hi - lo + 1),
+    then the bytes from the same stateful splitmix64 stream (host arrays)."""
+    import numpy as np
+    from oracle import oracle_c as oc
+    used = 0
+    if hi > lo:
+        w = oc.splitmix64_bytes(8 * n, seed).view(np.uint64)
+        lens = (lo + w % np.uint64(hi - lo + 1)).astype(np.uint64)
+        used = n
+    else:
+        lens = np.full(n, lo, np.uint64)
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum(lens[:-1])
+    total = int(lens.sum())
+    data = oc.splitmix64_bytes(total, seed, first=8 * used) if total else np.zeros(0, np.uint8)
+    return data, off, lens
+
+
+def main_small_flush(args):
+    """--config small_flush: microseconds per flush at the reference engine's own
+    default sizes and up to configs[0]'s 1 Ki x 1 KiB,
+    through the C++ Go-API mirror (tools/small_flush.cpp: NewLeaf x n, New,
+    Root.String(), the image; with the file write as well; and the bare C-ABI
+    call), for each NKV_OPT_SMALL_PATH mode: 1 = the one-launch kernel over
+    pinned host memory (default), 2 = the one launch through HBM, 0 = the grid
+    path.  Beside each shape: the same flush in memory on one host core with the
+    portable SHA-1 and with OpenSSL's (oracle/, nkvo_flush_reps), whose root every
+    GPU run must reproduce."""
+    import subprocess
+    import tempfile
+    from nakevaleng_amd import build as nb
+    from oracle import oracle_c as oc
+    exe = nb.build_small_flush()
+    spec = [f"{n}:{lo}:{hi}:{SMALL_SEED:x}" for _, n, lo, hi in SMALL_SHAPES]
+    gpu = {}
+    with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
+        for mode in (1, 2, 0):
+            p = subprocess.run([exe, str(mode), str(args.small_reps), td] + spec, capture_output=True, text=True,
+                               timeout=600)
+            if p.returncode != 0:
+                raise SystemExit(f"small_flush mode {mode} failed: {p.stderr[-2000:]}")
+            gpu[mode] = [json.loads(x) for x in p.stdout.splitlines() if x.startswith("{")]
+    shapes, verified = [], True
+    for k, (name, n, lo, hi) in enumerate(SMALL_SHAPES):
+        data, off, lens = small_shape_values(n, lo, hi)
+        cpu = {}
+        root = None
+        for impl in ("port", "openssl"):
+            est, root = oc.flush_us(data, off, lens, 3, openssl=impl == "openssl")
+            reps = max(5, min(200000, int(0.25e6 / max(est, 0.05))))  # ~0.25 s per figure
+            us_, r2 = oc.flush_us(data, off, lens, reps, openssl=impl == "openssl")
+            assert r2 == root
+            cpu[f"{impl}_1core_us"] = round(us_, 3)
+        best_cpu = min(cpu.values())
+        row = {"shape": name, "n": n, "value_bytes": [lo, hi], "payload_bytes": int(lens.sum()), "cpu": cpu,
+               "root": root}
+        for mode, key in ((1, "small_pinned"), (2, "small_hbm"), (0, "grid")):
+            g = gpu[mode][k]
+            ok = g["root"] == root
+            verified = verified and ok
+            row[key] = {"path": "small" if g["path"] == 1 else "grid", "mirror_us": g["mirror_us"],
+                        "mirror_us_p10_p90": [g["mirror_us_p10"], g["mirror_us_p90"]], "file_us": g["file_us"],
+                        "abi_us": g["abi_us"], "root_ok": ok}
+        best_gpu = min(row[m]["mirror_us"] for m in ("small_pinned", "small_hbm", "grid"))
+        row["gpu_over_cpu_time"] = round(best_gpu / best_cpu, 2)
+        shapes.append(row)
+    # the smallest payload of the sweep at which the best GPU flush is at least as
+    # fast as the best one-core CPU flush
+    cross = next((r["payload_bytes"] for r in sorted(shapes, key=lambda r: r["payload_bytes"])
+                  if r["gpu_over_cpu_time"] <= 1.0), None)
+    head = shapes[0]
+    out = {
+        "metric": "microseconds per default-size flush (NewLeaf x 10 values <= 200 B, New, Root, image) "
+                  "through the Go-API mirror",
+        "value": head["small_pinned"]["mirror_us"],
+        "unit": "us",
+        "n_gpus": 1,
+        "higher_is_better": False,
+        "dtype": "u32",
+        "data": f"synthetic: splitmix64 values (seed {SMALL_SEED:#x}) in host memory",
+        "config": {"workload": "the reference engine's default flush (coreconf.go:33-34) and compaction (:39) "
+                               "sizes, up to configs[0] and beyond the small path's bound",
+                   "reps": args.small_reps},
+        "shapes": shapes,
+        "crossover_payload_bytes": cross,
+        "verified_vs_oracle": verified,
+        "cpu_model": cpu_model(),
+    }
     print(json.dumps(out), flush=True)
 
 

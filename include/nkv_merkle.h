@@ -79,6 +79,19 @@ typedef enum nkv_status {
 
 typedef struct nkv_ctx nkv_ctx;
 
+/* ---- ABI version ----
+ * NKV_ABI_VERSION is the version this header describes; nkv_abi_version()
+ * the one the loaded library implements.  A caller built against version V
+ * checks nkv_abi_version() == V at start (the Go shim does).
+ * The version goes up whenever an existing entry point changes its meaning or
+ * signature; adding entry points or option values does not change it.
+ *   1: nkv_group_tree_dev takes d_roots as an array of g device pointers
+ *      (void *const *; before: one device pointer), and the options
+ *      NKV_OPT_DEEP_PREFETCH / NKV_OPT_QUEUE_RING accept only their one
+ *      remaining value. */
+#define NKV_ABI_VERSION 1
+int nkv_abi_version(void);
+
 /* ---- errors, devices, contexts ---- */
 const char *nkv_strerror(int status);
 /* "nkv-src-sha256:<64 hex>": SHA-256 of the sources and build flags this
@@ -107,6 +120,8 @@ int nkv_ctx_sync(nkv_ctx *ctx);
                                counts of a batch of >= 4096 values lie within max(1, min/16)
                                of each other, else sorted (decided on the device, no
                                read-back) */
+#define NKV_OPT_DEEP_PREFETCH 3 /* retired (ABI version 1): 3 is the only value accepted */
+#define NKV_OPT_QUEUE_RING 9    /* retired (ABI version 1): 13 is the only value accepted */
 #define NKV_OPT_QUEUE_SPLIT 4 /* work-queue kernel: groups whose longest value has at most
                                  this many 64-B blocks may go to the non-priority waves
                                  when the longest value bounds the batch (default 32) */
@@ -138,7 +153,21 @@ int nkv_ctx_sync(nkv_ctx *ctx);
                                    record is a packet on the stream between two kernels,
                                    so a timed loop samples its kernel times instead of
                                    carrying three records per call */
+#define NKV_OPT_SMALL_PATH 14 /* host-buffer tree calls (nkv_tree_from_values, nkv_tree_from_records)
+                                 of at most NKV_OPT_SMALL_MAX_N values and NKV_OPT_SMALL_MAX_BYTES
+                                 of payload: the whole tree and its image in ONE launch, one
+                                 synchronize.  1 (default) = the kernel reads the packed values
+                                 and writes its results across PCIe (host-coherent pinned
+                                 buffers, no DMA); 2 = one copy to HBM, the launch, one copy
+                                 back; 0 = off (the grid path for every size) */
+#define NKV_OPT_SMALL_MAX_N 15     /* 0..1024 (default 1024) */
+#define NKV_OPT_SMALL_MAX_BYTES 16 /* payload bound of the small path (default 1 MiB; the values
+                                      16-byte aligned; for records the whole stream) */
 int nkv_ctx_set_option(nkv_ctx *ctx, int key, int64_t value);
+/* Which path the latest host-buffer tree call of the context took */
+#define NKV_PATH_GRID 0  /* copies + leaf kernel + per-level reduce launches */
+#define NKV_PATH_SMALL 1 /* the one-launch small tree (NKV_OPT_SMALL_PATH) */
+int nkv_ctx_last_path(nkv_ctx *ctx, int *path);
 /* Timing (nkv_ctx_set_timing flags).  NKV_TIMING_EVENTS: the tree calls record
  * HIP events around the leaf kernel and the tree reduce on the context's
  * stream (and, for nkv_tree_from_values, around the upload and the download).
@@ -180,7 +209,10 @@ uint64_t nkv_bfs_size(uint64_t n); /* Serialize() bytes for 20-byte leaves */
  * overlaps the caller's NewLeaf loop; the next call over the block moves only
  * the rest.  Those bytes must not change until that call returns.  A call over
  * the block ends the batch; an upto below the previous one starts a new batch.
- * nkv_host_free waits for copies from the block. */
+ * nkv_host_free waits for copies from the block.  nkv_host_alloc also
+ * allocates the block's device mirror (as many bytes of HBM), so a block
+ * reserved once (e.g. at engine start, from the memtable's capacity) costs
+ * the flushes that use it no allocation. */
 int nkv_host_alloc(nkv_ctx *ctx, uint64_t bytes, void **out);
 int nkv_host_free(nkv_ctx *ctx, void *p);
 int nkv_host_stream(nkv_ctx *ctx, const void *block, uint64_t upto);
@@ -378,6 +410,16 @@ int nkv_group_create(const int *devices, int g, nkv_group **out);
 void nkv_group_destroy(nkv_group *grp);
 int nkv_group_size(const nkv_group *grp);
 int nkv_group_transport(const nkv_group *grp);
+/* Peer access between member i's GPU and member j's: nkv_group_create enables
+ * xGMI peer mappings for every pair of distinct GPUs that supports them
+ * (hipDeviceEnablePeerAccess; a pair already enabled counts), so GPU-to-GPU
+ * copies (nkv_group_tree_fetch, the copy transport) go over xGMI.  *state:
+ * NKV_PEER_ENABLED, NKV_PEER_SAME (both members on one GPU), or NKV_PEER_NONE
+ * (not mappable: copies take the runtime's staged path). */
+#define NKV_PEER_NONE 0
+#define NKV_PEER_ENABLED 1
+#define NKV_PEER_SAME 2
+int nkv_group_peer_access(const nkv_group *grp, int i, int j, int *state);
 /* member i's context (owned by the group): options, streams, *_dev calls */
 int nkv_group_ctx(nkv_group *grp, int i, nkv_ctx **out);
 int nkv_group_sync(nkv_group *grp);

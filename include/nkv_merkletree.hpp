@@ -126,6 +126,14 @@ class CopyPool {
         }
         return j;
     }
+    // a job that was filled but copied by its owner instead (Session::Settle)
+    void Recycle(std::unique_ptr<Job> j) {
+        if (!j) return;
+        std::lock_guard<std::mutex> g(mu_);
+        j->tasks.clear();
+        free_.push_back(std::move(j));
+    }
+    CopyFn copy_fn() const { return copy_; }
     // wait for every submitted job (their stores are fenced by the workers)
     void Drain() {
         std::unique_lock<std::mutex> g(mu_);
@@ -195,8 +203,20 @@ class TaskTeam {
     TaskTeam& operator=(const TaskTeam&) = delete;
     int size() const { return int(th_.size()) + 1; }
 
+    // Safe from several threads at once: one run holds the team, and a caller
+    // that finds it busy (another thread's Serialize or New) runs its parts
+    // itself (two trees serialized or destroyed on two threads, as
+    // Go allows).
     void Run(int parts, const std::function<void(int)>& fn) {
-        if (parts <= 1 || th_.empty()) {  // every part runs, as on the team
+        struct Hold {  // the team for this run, released however the run ends
+            std::atomic<bool>* f;
+            bool own;
+            ~Hold() {
+                if (own) f->store(false, std::memory_order_release);
+            }
+        } held{&busy_, false};
+        if (parts > 1 && !th_.empty()) held.own = !busy_.exchange(true, std::memory_order_acq_rel);
+        if (!held.own) {  // every part runs, as on the team
             std::exception_ptr e;
             for (int k = 0; k < parts; ++k) {
                 try {
@@ -265,6 +285,7 @@ class TaskTeam {
     }
 
     std::vector<std::thread> th_;
+    std::atomic<bool> busy_{false};  // a run owns the team
     std::mutex mu_;
     std::condition_variable cv_, done_;
     const std::function<void(int)>* fn_ = nullptr;
@@ -278,22 +299,39 @@ class TaskTeam {
 struct MerkleNode;
 
 // One device context + the pinned arena that deferred NewLeaf values go to.
+//
+// Threads: NewLeaf and New of one session are one thread at a time (the
+// caller's flush or compaction loop; the Go shim holds a mutex).  Serialize,
+// Deserialize and the destruction of finished trees may run on several threads
+// at once: the recycled node storage is locked and the host team runs one
+// caller's parts at a time.
 class Session {
    public:
-    explicit Session(int device = 0) {
-        check(nkv_ctx_create(device, &ctx_), "nkv_ctx_create");
-    }
+    // The device context is created on first use (ctx()), so trees that never
+    // hash (Deserialize, Serialize of a read tree) need no GPU.
+    explicit Session(int device = 0) : device_(device) {}
     ~Session();  // below MerkleNode (it frees the recycled node storage)
     Session(const Session&) = delete;
     Session& operator=(const Session&) = delete;
 
-    nkv_ctx* ctx() const { return ctx_; }
+    nkv_ctx* ctx() {
+        std::call_once(ctx_once_, [this] { check(nkv_ctx_create(device_, &ctx_), "nkv_ctx_create"); });
+        return ctx_;
+    }
 
     // The process-wide default session on device 0 (Go's package-level state).
+    // Never destroyed: a tree with static storage may outlive any other static,
+    // and its destructor recycles into this session.
     static Session& Default() {
-        static Session s(0);
-        return s;
+        static Session* s = new Session(0);
+        return *s;
     }
+
+    // Size the pinned arena for a flush of up to `bytes` of values (plus their
+    // 16-byte alignment) before the first NewLeaf, e.g. from the memtable's
+    // threshold at engine start (coreconf MEMTABLE_THRESHOLD): the first flush
+    // then neither grows nor copies the arena.
+    void Reserve(uint64_t bytes) { Grow(bytes, false); }
 
     // ---- deferred leaves ----
     struct Batch {
@@ -355,7 +393,7 @@ class Session {
             if (pool_) pool_->Reset();
         }
         const uint64_t at = (used_ + 15) & ~uint64_t(15);
-        Reserve(at + n);
+        Grow(at + n, true);
         batch_->off.push_back(at);
         batch_->len.push_back(n);
         used_ = at + n;
@@ -374,7 +412,7 @@ class Session {
                     if (s >= streamed_ + kStreamChunk) {
                         streamed_ = s - s % kStreamChunk;
                         Fence();  // values this thread copied itself (the std::string forms)
-                        check(nkv_host_stream(ctx_, arena_, streamed_), "nkv_host_stream");
+                        check(nkv_host_stream(ctx(), arena_, streamed_), "nkv_host_stream");
                     }
                 }
             }
@@ -384,7 +422,7 @@ class Session {
             if (!pool_ && stream_ && used_ >= streamed_ + kStreamChunk) {
                 streamed_ = used_ - used_ % kStreamChunk;
                 Fence();
-                check(nkv_host_stream(ctx_, arena_, streamed_), "nkv_host_stream");
+                check(nkv_host_stream(ctx(), arena_, streamed_), "nkv_host_stream");
             }
         }
         return batch_->off.size() - 1;
@@ -392,9 +430,22 @@ class Session {
     const std::shared_ptr<Batch>& batch() const { return batch_; }
     // Every queued arena copy done (New and every other reader of the arena
     // call this first).
+    // A job of at most kInlineJob bytes still being filled (a small flush's
+    // whole batch, or the tail of a large one) is copied here instead: handing
+    // it to a pool thread and waiting for it costs two thread wake-ups, more
+    // than the copy (the reference's default flush is ~2 KB).
+    static constexpr uint64_t kInlineJob = uint64_t(256) << 10;
     void Settle() {
         if (!pool_) return;
-        SubmitJob();
+        if (job_ && job_bytes_ <= kInlineJob) {
+            const CopyPool::CopyFn copy = pool_->copy_fn();
+            for (const CopyPool::Task& t : job_->tasks) copy(job_->base + t.at, t.src, t.n);
+            pool_->Recycle(std::move(job_));
+            job_.reset();
+            job_bytes_ = 0;
+        } else {
+            SubmitJob();
+        }
         pool_->Drain();
     }
     // NewLeaf's copy threads: 0 = copy on the caller's thread; default
@@ -426,7 +477,7 @@ class Session {
         b.digests.assign(20 * n, 0);
         Settle();
         Fence();
-        check(nkv_leaf_hash(ctx_, arena(), b.off.data(), b.len.data(), n, b.digests.data()), "NewLeaf");
+        check(nkv_leaf_hash(ctx(), arena(), b.off.data(), b.len.data(), n, b.digests.data()), "NewLeaf");
         b.resolved = true;
     }
 
@@ -469,19 +520,25 @@ class Session {
     void GiveNodes(std::vector<MerkleNode>* v);
     // the host thread team (lazily: min(8, cores) threads)
     TaskTeam& Team() {
-        if (!team_) team_.reset(new TaskTeam(int(std::min<unsigned>(8, std::max(1u, std::thread::hardware_concurrency())))));
+        std::call_once(team_once_, [this] {
+            team_.reset(new TaskTeam(int(std::min<unsigned>(8, std::max(1u, std::thread::hardware_concurrency())))));
+        });
         return *team_;
     }
     // New's level arrays, recycled the same way (no 20 * (2n - 1)-byte zero
     // fill and page faults per flush)
     std::vector<uint8_t> TakeLevels() {
         std::vector<uint8_t> v;
+        std::lock_guard<std::mutex> g(spare_mu_);
         v.swap(spare_levels_);
         return v;
     }
     void GiveLevels(std::vector<uint8_t>&& v) {
+        std::lock_guard<std::mutex> g(spare_mu_);
         if (v.capacity() > spare_levels_.capacity()) spare_levels_.swap(v);
     }
+    // the host team (Team()) is created once even when two threads ask at once
+    std::once_flag team_once_;
 
    private:
     CopyPool* Pool() {
@@ -500,25 +557,35 @@ class Session {
         job_.reset();
         job_bytes_ = 0;
     }
-    void Reserve(uint64_t bytes) {
+    // A block of at least `bytes`: exactly that for Reserve, else (NewLeaf
+    // outgrowing the block) twice the old size, from kFirstArena.  The open
+    // batch's values move with it.
+    static constexpr uint64_t kFirstArena = uint64_t(64) << 20;
+    void Grow(uint64_t bytes, bool doubling) {
         if (bytes <= cap_) return;
         Settle();  // no queued copy may land in the old block
-        uint64_t want = cap_ ? cap_ * 2 : (uint64_t(1) << 20);
-        while (want < bytes) want *= 2;
+        uint64_t want = bytes;
+        if (doubling) {
+            want = cap_ ? cap_ * 2 : kFirstArena;
+            while (want < bytes) want *= 2;
+        }
         void* p = nullptr;
-        check(nkv_host_alloc(ctx_, want, &p), "nkv_host_alloc");
+        check(nkv_host_alloc(ctx(), want, &p), "nkv_host_alloc");
         ++allocs_;
         if (arena_) {
             Fence();
-            std::memcpy(p, arena_, used_);
-            nkv_host_free(ctx_, arena_);
+            if (used_) std::memcpy(p, arena_, used_);
+            nkv_host_free(ctx(), arena_);
         }
         arena_ = p;
         cap_ = want;
         streamed_ = 0;  // a new block: its device copy starts from byte 0
     }
 
+    int device_ = 0;
+    std::once_flag ctx_once_;
     nkv_ctx* ctx_ = nullptr;
+    std::mutex spare_mu_;  // spare_ and spare_levels_ (trees end on any thread)
     void* arena_ = nullptr;
     uint64_t cap_ = 0, used_ = 0, epoch_ = 0, allocs_ = 0, streamed_ = 0;
     bool stream_ = true, nt_ = true;
@@ -619,10 +686,11 @@ inline Session::~Session() {
     pool_.reset();
     for (auto* v : spare_) delete v;
     if (arena_) nkv_host_free(ctx_, arena_);
-    nkv_ctx_destroy(ctx_);
+    if (ctx_) nkv_ctx_destroy(ctx_);
 }
 
 inline std::vector<MerkleNode>* Session::TakeNodes() {
+    std::lock_guard<std::mutex> g(spare_mu_);
     if (spare_.empty()) return new std::vector<MerkleNode>();
     auto* v = spare_.back();
     spare_.pop_back();
@@ -631,7 +699,9 @@ inline std::vector<MerkleNode>* Session::TakeNodes() {
 
 inline void Session::GiveNodes(std::vector<MerkleNode>* v) {
     if (!v) return;
+    std::unique_lock<std::mutex> g(spare_mu_);
     if (spare_.size() >= 2) {  // two trees' worth (a flush and the one before)
+        g.unlock();
         delete v;
         return;
     }
@@ -955,7 +1025,7 @@ inline std::unique_ptr<MerkleTree> New(std::vector<MerkleNode> level, std::strin
     const uint64_t total = nkv_total_nodes(n);
     Session& S = Session::Default();
     t->levels_ = S.TakeLevels();
-    t->levels_.resize(20 * total);  // every byte is written below
+    t->levels_.resize(20 * total);  // recycled: every byte is written below (level 0 zeroed for generic leaves)
     uint8_t* nodes = t->levels_.data();
 
     // the flush / compaction pattern: n NewLeaf calls of one batch, in order
@@ -988,6 +1058,9 @@ inline std::unique_ptr<MerkleTree> New(std::vector<MerkleNode> level, std::strin
                 flat.insert(flat.end(), x.Data.begin(), x.Data.end());
             }
             flat.push_back(0);
+            // leaves of any length have no 20-byte level 0: zero it, as a fresh
+            // array was (a recycled one holds the last tree's digests)
+            std::memset(nodes, 0, 20 * n);
             check(nkv_tree_generic(ctx, flat.data(), off.data(), len.data(), n, nullptr, nodes + 20 * n,
                                    nullptr),
                   "New");

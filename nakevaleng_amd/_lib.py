@@ -31,6 +31,14 @@ NKV_OPT_BLOOM_PATH = 10
 NKV_OPT_RECORDS_FUSED = 11
 NKV_OPT_TABLE_LANES = 12
 NKV_OPT_TIMING_EVERY = 13
+NKV_OPT_SMALL_PATH = 14
+NKV_OPT_SMALL_MAX_N = 15
+NKV_OPT_SMALL_MAX_BYTES = 16
+NKV_PATH_GRID = 0
+NKV_PATH_SMALL = 1
+NKV_OPT_DEEP_PREFETCH = 3  # retired: accepts only 3
+NKV_OPT_QUEUE_RING = 9  # retired: accepts only 13
+NKV_ABI_VERSION = 1  # include/nkv_merkle.h
 NKV_TIMING_EVENTS = 1
 NKV_TIMING_CLOCK = 2
 NKV_TABLE_STRIDED = 0
@@ -39,6 +47,9 @@ NKV_TABLE_RECORDS = 2
 NKV_TABLE_VERIFY = 3
 NKV_TRANSPORT_RCCL = 1
 NKV_TRANSPORT_COPY = 2
+NKV_PEER_NONE = 0
+NKV_PEER_ENABLED = 1
+NKV_PEER_SAME = 2
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)
 _u64p = ctypes.POINTER(ctypes.c_uint64)
@@ -63,6 +74,7 @@ _tabp = ctypes.POINTER(NkvTable)
 
 # name -> (restype, argtypes); every symbol include/nkv_merkle.h declares
 SIGNATURES = {
+    "nkv_abi_version": (_int, []),
     "nkv_strerror": (ctypes.c_char_p, [_int]),
     "nkv_build_id": (ctypes.c_char_p, []),
     "nkv_device_count": (_int, [ctypes.POINTER(_int)]),
@@ -71,6 +83,7 @@ SIGNATURES = {
     "nkv_ctx_set_stream": (_int, [_vp, _vp]),
     "nkv_ctx_use_own_stream": (_int, [_vp]),
     "nkv_ctx_sync": (_int, [_vp]),
+    "nkv_ctx_last_path": (_int, [_vp, ctypes.POINTER(_int)]),
     "nkv_ctx_set_option": (_int, [_vp, _int, ctypes.c_int64]),
     "nkv_ctx_set_timing": (_int, [_vp, _int]),
     "nkv_ctx_last_timing": (_int, [_vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
@@ -126,6 +139,7 @@ SIGNATURES = {
     "nkv_group_destroy": (None, [_vp]),
     "nkv_group_size": (_int, [_vp]),
     "nkv_group_transport": (_int, [_vp]),
+    "nkv_group_peer_access": (_int, [_vp, _int, _int, ctypes.POINTER(_int)]),
     "nkv_group_ctx": (_int, [_vp, _int, ctypes.POINTER(_vp)]),
     "nkv_group_sync": (_int, [_vp]),
     "nkv_group_roots_allgather": (_int, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(_vp), _u8p]),
@@ -169,6 +183,9 @@ def lib():
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
+        if L.nkv_abi_version() != NKV_ABI_VERSION:
+            raise ImportError(f"{SO_PATH} implements C-ABI version {L.nkv_abi_version()}, "
+                              f"this binding needs {NKV_ABI_VERSION}")
         _lib = L
     return _lib
 
@@ -262,6 +279,12 @@ class Context:
     def sync(self) -> None:
         check(lib().nkv_ctx_sync(self.h))
 
+    def last_path(self) -> int:
+        """NKV_PATH_* of the latest host-buffer tree call (small one-launch or grid)."""
+        p = _int()
+        check(lib().nkv_ctx_last_path(self.h, ctypes.byref(p)))
+        return p.value
+
     def set_timing(self, on, clock: bool = False) -> None:
         """Events around the leaf kernel / reduce (on) and the leaf kernels' clock probe (clock)."""
         flags = (NKV_TIMING_EVENTS if on else 0) | (NKV_TIMING_CLOCK if clock else 0)
@@ -315,6 +338,12 @@ class Group:
     @property
     def transport(self) -> int:
         return lib().nkv_group_transport(self.h)
+
+    def peer_access(self, i: int, j: int) -> int:
+        """NKV_PEER_* between member i's GPU and member j's."""
+        s = _int()
+        check(lib().nkv_group_peer_access(self.h, i, j, ctypes.byref(s)))
+        return s.value
 
     def ctx_handle(self, i: int):
         out = _vp()

@@ -88,17 +88,32 @@ API_FLUSH_SRC = os.path.join(ROOT, "tools", "api_flush.cpp")
 API_FLUSH = os.path.join(ROOT, "build", "api_flush")
 
 
-def build_api_flush() -> str:
-    """The end-to-end flush driver (tools/api_flush.cpp) over the C++ Go-API mirror
-    (bench.py --config api_flush); g++, linked to the in-tree library."""
+def build_tool(name: str) -> str:
+    """tools/<name>.cpp over the C++ Go-API mirror -> build/<name> (g++, linked
+    to the in-tree library; rebuilt when the source, the headers or the library
+    are newer)."""
     build(quiet=True)
-    os.makedirs(os.path.dirname(API_FLUSH), exist_ok=True)
-    tmp = f"{API_FLUSH}.tmp{os.getpid()}"
+    src = os.path.join(ROOT, "tools", f"{name}.cpp")
+    exe = os.path.join(ROOT, "build", name)
+    deps = [src, SO] + [os.path.join(ROOT, "include", h) for h in ("nkv_merkle.h", "nkv_merkletree.hpp")]
+    if os.path.exists(exe) and os.path.getmtime(exe) >= max(os.path.getmtime(d) for d in deps):
+        return exe
+    os.makedirs(os.path.dirname(exe), exist_ok=True)
+    tmp = f"{exe}.tmp{os.getpid()}"
     subprocess.check_call(["g++", "-O2", "-std=c++17", "-pthread", "-I", os.path.join(ROOT, "include"),
-                           API_FLUSH_SRC, "-L", PKG, "-lnkvmerkle", "-Wl,-rpath,$ORIGIN/../nakevaleng_amd",
-                           "-o", tmp])
-    os.replace(tmp, API_FLUSH)
-    return API_FLUSH
+                           src, "-L", PKG, "-lnkvmerkle", "-Wl,-rpath,$ORIGIN/../nakevaleng_amd", "-o", tmp])
+    os.replace(tmp, exe)
+    return exe
+
+
+def build_api_flush() -> str:
+    """The end-to-end flush driver (tools/api_flush.cpp, bench.py --config api_flush)."""
+    return build_tool("api_flush")
+
+
+def build_small_flush() -> str:
+    """The default-size flush driver (tools/small_flush.cpp, bench.py --config small_flush)."""
+    return build_tool("small_flush")
 
 
 if __name__ == "__main__":

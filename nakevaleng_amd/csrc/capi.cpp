@@ -199,6 +199,91 @@ int stage_stream(nkv_ctx* c, const uint8_t* src, uint64_t bytes, DevBuf& d, cons
     return NKV_OK;
 }
 
+// A host-coherent pinned buffer of at least `bytes` (contents not kept): the
+// small-tree kernel reads / writes it across PCIe, uncached on the GPU side.
+int grow_coherent(uint8_t** p, size_t* cap, size_t bytes) {
+    if (*cap >= bytes) return NKV_OK;
+    if (*p) (void)hipHostFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    const size_t want = std::max(bytes, size_t(64) << 10);
+    if (hipHostMalloc(reinterpret_cast<void**>(p), want, hipHostMallocCoherent) != hipSuccess) {
+        (void)hipGetLastError();
+        *p = nullptr;
+        return NKV_ERR_NOMEM;
+    }
+    *cap = want;
+    return NKV_OK;
+}
+
+// The reference engine's own flush and compaction sizes (coreconf.go:33-34,
+// :39: 10-record memtables, 4 runs) hash a few KiB per call, where the grid
+// path's copies and per-level launches cost far more than the work.  A batch
+// of at most small_max_n values and small_max_bytes of (16-byte aligned)
+// payload instead goes as ONE launch (k_small_tree): the values are packed into
+// a host-coherent pinned buffer that the kernel reads across PCIe
+// (NKV_OPT_SMALL_PATH 1) or that is copied to HBM first (2), the kernel writes
+// nodes + image into a pinned output buffer (or HBM, then one copy back), and
+// the call synchronizes once.  *taken = false: not eligible, nothing done.
+int small_tree(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint64_t* len, uint64_t n,
+               uint8_t* root20, uint8_t* nodes_out, uint8_t* img_out, bool* taken) {
+    *taken = false;
+    if (c->small_path == 0 || n == 0 || n > c->small_max_n || n > kSmallMaxN) return NKV_OK;
+    uint64_t vbytes = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        if (len[i] > c->small_max_bytes) return NKV_OK;
+        vbytes += align16(len[i]);
+        if (vbytes > c->small_max_bytes) return NKV_OK;
+    }
+    const uint64_t tot = total_of(n);
+    const uint64_t img_len = layout_of(counts_of(n)).total;
+    const uint64_t img_at = align16(20 * tot);
+    const uint64_t in_bytes = 16 * n + vbytes, out_bytes = img_at + align16(img_len);
+    const uint32_t lds = small_lds_bytes(n, tot, img_len);
+    if (lds > kSmallMaxLds) return NKV_OK;
+    uint64_t lo = 0, hi = 0;  // a call over a pinned block ends its batch (nkv_host_stream)
+    if (nkv_ctx::Pinned* blk = pinned_extent(c, base, off, len, n, &lo, &hi)) blk->streamed = 0;
+    TRY(grow_coherent(&c->h_sin, &c->h_sin_cap, in_bytes));
+    TRY(grow_coherent(&c->h_sout, &c->h_sout_cap, out_bytes));
+    const size_t small_cap = c->d_small.cap;
+    TRY(grow(c->d_small, 64 + 20 * kSmallMaxN));
+    if (c->d_small.cap != small_cap) HIPTRY(hipMemsetAsync(c->d_small.p, 0, 64, c->stream));  // the ticket
+    uint64_t* desc = reinterpret_cast<uint64_t*>(c->h_sin);
+    uint8_t* vals = c->h_sin + 16 * n;
+    uint64_t p = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        desc[2 * i] = p;
+        desc[2 * i + 1] = len[i];
+        if (len[i]) memcpy(vals + p, base + off[i], len[i]);
+        p += align16(len[i]);
+    }
+    uint8_t* scratch = static_cast<uint8_t*>(c->d_small.p) + 64;
+    unsigned int* ticket = static_cast<unsigned int*>(c->d_small.p);
+    if (c->small_path == 2) {  // through HBM: one copy in, one launch, one copy out
+        TRY(grow(c->d_sin, in_bytes));
+        TRY(grow(c->d_sout, out_bytes));
+        HIPTRY(hipMemcpyAsync(c->d_sin.p, c->h_sin, in_bytes, hipMemcpyHostToDevice, c->stream));
+        HIPTRY(launch_small_tree(static_cast<const uint8_t*>(c->d_sin.p), uint32_t(n),
+                                 static_cast<uint8_t*>(c->d_sout.p), uint32_t(img_at), lds, scratch, ticket,
+                                 c->stream));
+        HIPTRY(hipMemcpyAsync(c->h_sout, c->d_sout.p, out_bytes, hipMemcpyDeviceToHost, c->stream));
+    } else {  // the kernel reads the values and writes its results across PCIe
+        void *din = nullptr, *dout = nullptr;
+        HIPTRY(hipHostGetDevicePointer(&din, c->h_sin, 0));
+        HIPTRY(hipHostGetDevicePointer(&dout, c->h_sout, 0));
+        HIPTRY(launch_small_tree(static_cast<const uint8_t*>(din), uint32_t(n), static_cast<uint8_t*>(dout),
+                                 uint32_t(img_at), lds, scratch, ticket, c->stream));
+    }
+    HIPTRY(hipStreamSynchronize(c->stream));
+    if (nodes_out) memcpy(nodes_out, c->h_sout, 20 * tot);
+    if (root20) memcpy(root20, c->h_sout + 20 * (tot - 1), 20);
+    if (img_out) memcpy(img_out, c->h_sout + img_at, img_len);
+    c->last_path = NKV_PATH_SMALL;
+    c->host_timed = false;
+    *taken = true;
+    return NKV_OK;
+}
+
 int finish_tree(nkv_ctx* c, uint8_t* nodes, uint64_t n, uint8_t* root20, uint8_t* nodes_out,
                 uint8_t* img_out) {
     const uint64_t tot = total_of(n);
@@ -407,6 +492,8 @@ extern "C" {
 
 const char* nkv_build_id(void) { return "nkv-src-sha256:" NKV_SRC_HASH; }
 
+int nkv_abi_version(void) { return NKV_ABI_VERSION; }
+
 const char* nkv_strerror(int s) {
     switch (s) {
         case NKV_OK: return "ok";
@@ -470,7 +557,8 @@ void nkv_ctx_destroy(nkv_ctx* c) {
     (void)hipSetDevice(c->device);
     for (DevBuf* b : {&c->d_data, &c->d_off, &c->d_len, &c->d_nodes, &c->d_img, &c->d_tmp,
                       &c->d_err, &c->d_aux, &c->d_keys, &c->d_perm, &c->d_stmp, &c->d_queue, &c->d_stats,
-                      &c->d_range, &c->d_part, &c->d_tmp2, &c->d_flags, &c->d_clk})
+                      &c->d_range, &c->d_part, &c->d_tmp2, &c->d_flags, &c->d_clk, &c->d_sin, &c->d_sout,
+                      &c->d_small})
         if (b->p) (void)hipFree(b->p);
     for (nkv_ctx::Pinned* blk : c->pinned) {
         if (blk->d_arena.p) (void)hipFree(blk->d_arena.p);
@@ -479,6 +567,8 @@ void nkv_ctx_destroy(nkv_ctx* c) {
     }
     if (c->h_stage) (void)hipHostFree(c->h_stage);
     if (c->h_small) (void)hipHostFree(c->h_small);
+    if (c->h_sin) (void)hipHostFree(c->h_sin);
+    if (c->h_sout) (void)hipHostFree(c->h_sout);
     for (hipEvent_t e : c->ring) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->join_ev) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->host_ev)
@@ -561,9 +651,31 @@ int nkv_ctx_set_option(nkv_ctx* c, int key, int64_t value) try {
             c->timing_every = int(value);
             c->timing_calls = 0;
             return NKV_OK;
+        case NKV_OPT_SMALL_PATH:
+            if (value < 0 || value > 2) return NKV_ERR_INVALID;
+            c->small_path = int(value);
+            return NKV_OK;
+        case NKV_OPT_SMALL_MAX_N:
+            if (value < 0 || value > int64_t(kSmallMaxN)) return NKV_ERR_INVALID;
+            c->small_max_n = uint64_t(value);
+            return NKV_OK;
+        case NKV_OPT_SMALL_MAX_BYTES:
+            if (value < 0 || value > (int64_t(1) << 30)) return NKV_ERR_INVALID;
+            c->small_max_bytes = uint64_t(value);
+            return NKV_OK;
+        case NKV_OPT_DEEP_PREFETCH:  // retired: the one path left (ABI version 1)
+            return value == 3 ? NKV_OK : NKV_ERR_INVALID;
+        case NKV_OPT_QUEUE_RING:  // retired: the 3-slot ring (ABI version 1)
+            return value == 13 ? NKV_OK : NKV_ERR_INVALID;
         default:
             return NKV_ERR_INVALID;
     }
+} NKV_CATCH
+
+int nkv_ctx_last_path(nkv_ctx* c, int* path) try {
+    if (!c || !path) return NKV_ERR_INVALID;
+    *path = c->last_path;
+    return NKV_OK;
 } NKV_CATCH
 
 int nkv_ctx_sync(nkv_ctx* c) try {
@@ -698,6 +810,13 @@ int nkv_host_alloc(nkv_ctx* c, uint64_t bytes, void** out) try {
         (void)hipHostFree(p);
         return NKV_ERR_NOMEM;
     }
+    // the block's device mirror now, not inside the first flush that streams
+    // into it (an arena reserved at engine start costs a flush nothing)
+    if (grow(blk->d_arena, blk->bytes) != NKV_OK) {
+        (void)hipHostFree(p);
+        delete blk;
+        return NKV_ERR_NOMEM;
+    }
     c->pinned.push_back(blk);
     *out = p;
     return NKV_OK;
@@ -770,6 +889,10 @@ int nkv_tree_from_values(nkv_ctx* c, const uint8_t* base, const uint64_t* off, c
     if (n > kMaxN) return NKV_ERR_INVALID;
     if (n == 0) return NKV_ERR_EMPTY;
     if (!base || !off || !len) return NKV_ERR_INVALID;
+    bool small = false;
+    TRY(small_tree(c, base, off, len, n, root20, nodes_out, img_out, &small));
+    if (small) return NKV_OK;
+    c->last_path = NKV_PATH_GRID;
     TRY(host_mark(c, 0));
     const uint8_t* d_base = nullptr;
     bool aligned = true;
@@ -901,6 +1024,27 @@ int nkv_tree_from_records(nkv_ctx* c, const uint8_t* stream, uint64_t stream_len
     if (n == 0) return NKV_ERR_EMPTY;
     if (!stream || !rec_size) return NKV_ERR_INVALID;
     if (!records_fit(rec_size, n, stream_len)) return NKV_ERR_INVALID;
+    if (c->small_path != 0 && n <= c->small_max_n && n <= kSmallMaxN && stream_len <= c->small_max_bytes) {
+        // a small table (one lsm_run_max compaction at the default sizes): the
+        // values' places from the headers here (record.go:191-199, the same
+        // bounds k_locate applies), then the one-launch path
+        std::vector<uint64_t> voff(n), vlen(n);
+        uint64_t r = 0;
+        for (uint64_t i = 0; i < n; ++i) {
+            if (!header_in(r, stream_len)) return NKV_ERR_INVALID;
+            uint64_t ks = 0, vs = 0;
+            memcpy(&ks, stream + r + 14, 8);
+            memcpy(&vs, stream + r + 22, 8);
+            if (ks > stream_len || vs > stream_len || r + 30 + ks + vs > stream_len) return NKV_ERR_INVALID;
+            voff[i] = r + 30 + ks;
+            vlen[i] = vs;
+            r += rec_size[i];
+        }
+        bool small = false;
+        TRY(small_tree(c, stream, voff.data(), vlen.data(), n, root20, nodes_out, img_out, &small));
+        if (small) return NKV_OK;
+    }
+    c->last_path = NKV_PATH_GRID;
     TRY(stage_stream(c, stream, stream_len, c->d_data, rec_size, n, c->d_aux));
     // record offsets in their own scratch (records_tree uses d_off / d_len)
     TRY(grow(c->d_tmp2, 8 * n));

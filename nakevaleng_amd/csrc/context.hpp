@@ -170,6 +170,18 @@ struct nkv_ctx {
         nkv::DevBuf d_arena;  // device mirror of the block
     };
     std::vector<Pinned*> pinned;
+    // the one-launch small-tree path of the host-buffer calls (NKV_OPT_SMALL_*):
+    // host-coherent pinned in / out buffers the kernel reads and writes across
+    // PCIe (or device copies of them, small_path 2), and its device scratch
+    // (the ticket word + 20 n leaf digests)
+    int small_path = 1;
+    uint64_t small_max_n = 1024;
+    uint64_t small_max_bytes = uint64_t(1) << 20;
+    uint8_t* h_sin = nullptr;
+    uint8_t* h_sout = nullptr;
+    size_t h_sin_cap = 0, h_sout_cap = 0;
+    nkv::DevBuf d_sin, d_sout, d_small;
+    int last_path = 0;  // NKV_PATH_* of the latest host-buffer tree call
 };
 
 namespace nkv {

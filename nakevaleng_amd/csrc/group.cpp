@@ -180,11 +180,45 @@ struct nkv_group {
     std::vector<DevBuf> levels;    // per member: levels 0..k of its range, level-major
     std::vector<DevBuf> top;       // per member: the top tree over the G sub-roots
     DevBuf full, img;              // member 0: the whole tree, its image
+    std::vector<int> peer;         // g x g: NKV_PEER_* of member i's device to member j's
 };
 
 namespace {
 
 int member_bind(nkv_group* grp, int i) { return st(hipSetDevice(grp->dev[i])); }
+
+// xGMI peer mappings between every pair of the members' GPUs (VERDICT r04 item
+// 5): nkv_group_tree_fetch and the copy transport move bytes GPU to GPU with
+// hipMemcpyPeerAsync, which without a mapping takes whatever path the runtime
+// picks (staged through the host).  A pair already enabled (by another group,
+// or by torch in the same process) counts as enabled; a pair the hardware
+// cannot map stays NKV_PEER_NONE and its copies still work.  Mappings are
+// process-wide and are left in place when the group is destroyed (another
+// group of the process may use them).
+int enable_peers(nkv_group* grp) {
+    const int g = grp->g;
+    grp->peer.assign(size_t(g) * g, NKV_PEER_NONE);
+    for (int i = 0; i < g; ++i) {
+        for (int j = 0; j < g; ++j) {
+            int& s = grp->peer[size_t(i) * g + j];
+            if (grp->dev[i] == grp->dev[j]) {
+                s = NKV_PEER_SAME;
+                continue;
+            }
+            int can = 0;
+            if (hipDeviceCanAccessPeer(&can, grp->dev[i], grp->dev[j]) != hipSuccess) {
+                (void)hipGetLastError();
+                continue;
+            }
+            if (!can) continue;
+            TRY(member_bind(grp, i));
+            const hipError_t e = hipDeviceEnablePeerAccess(grp->dev[j], 0);
+            if (e == hipSuccess || e == hipErrorPeerAccessAlreadyEnabled) s = NKV_PEER_ENABLED;
+            (void)hipGetLastError();  // an already-enabled pair leaves its error behind
+        }
+    }
+    return NKV_OK;
+}
 
 // bytes from member j's device memory to member i's, on member i's stream (a
 // plain device copy when both are the same GPU, else a peer copy over xGMI)
@@ -395,6 +429,7 @@ int nkv_group_create(const int* devices, int g, nkv_group** out) try {
         if (rc != NKV_OK) grp->comm.clear();
         grp->transport = NKV_TRANSPORT_RCCL;
     }
+    if (rc == NKV_OK) rc = enable_peers(grp);  // after RCCL's own setup (it may have enabled them)
     if (rc != NKV_OK) {
         nkv_group_destroy(grp);
         return rc;
@@ -427,6 +462,12 @@ void nkv_group_destroy(nkv_group* grp) {
     for (nkv_ctx* c : grp->ctx) nkv_ctx_destroy(c);
     delete grp;
 }
+
+int nkv_group_peer_access(const nkv_group* grp, int i, int j, int* state) try {
+    if (!grp || !state || i < 0 || j < 0 || i >= grp->g || j >= grp->g) return NKV_ERR_INVALID;
+    *state = grp->peer[size_t(i) * grp->g + j];
+    return NKV_OK;
+} NKV_CATCH
 
 int nkv_group_size(const nkv_group* grp) { return grp ? grp->g : 0; }
 

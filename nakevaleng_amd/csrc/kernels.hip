@@ -12,6 +12,7 @@
 //                     merklenode.go:37-63) at closed-form offsets.
 //   K0  k_locate      value offset/length of each serialized core/record
 //                     (record.go:191-199): value = rec + 30 + KeySize.
+//   Ks  k_small_tree  a whole small tree (n <= 1024) and its image in one launch.
 //       k_fill        splitmix64 synthetic bytes (bench/test input only).
 //
 // Node storage ("nodes" buffer): every level, bottom-up, level-major; level L
@@ -23,6 +24,7 @@
 
 #include "crc_dev.hpp"
 #include "internal.hpp"
+#include "nkv_merkle.h"
 #include "sha1_dev.hpp"
 
 namespace nkv {
@@ -1922,7 +1924,159 @@ __global__ __launch_bounds__(kBlock) void k_fill(uint8_t* __restrict__ buf, uint
 }
 
 // ---------------------------------------------------------------------------
+// Ks: a whole small tree in ONE launch -- the sizes the reference engine runs at
+// by default (coreconf.go:33-34: a flush of MEMTABLE_CAPACITY = 10 records;
+// :39: a compaction of lsm_run_max = 4 such runs), where a launch per level
+// and copies per buffer would cost more than the hashing.
+//
+// Input `in` (16-byte aligned): n (offset, length) u64 pairs, then the values
+// at in + 16 n + offset (16-byte aligned offsets).  The host packs it into
+// host-coherent pinned memory that the kernel reads across PCIe (no DMA), or
+// copies it to HBM first (NKV_OPT_SMALL_PATH).  One lane per leaf and one
+// 256-lane workgroup per 256 leaves, so each wave runs alone on its SIMD (a
+// leaf's SHA-1 is a serial chain: DESIGN.md section 4, lone-wave cadence); the
+// last workgroup to finish (a ticket) takes every leaf digest, builds all levels
+// (merkletree.go:31-64) and the Serialize image (merkletree.go:67-92,
+// merklenode.go:37-63) in LDS, and stores nodes (level-major, 20 B each) at out
+// and the image at out + img_at with 16-byte stores.  Dynamic LDS:
+// small_lds_bytes(n).
+
+constexpr uint32_t kSmallBlock = 256;
+
+// SHA-1 of p[0, len), p 16-byte aligned, one block of register lookahead
+__device__ __forceinline__ void sha1_value_aligned(const uint8_t* p, uint64_t len, uint32_t h[5]) {
+    sha1_init(h);
+    const uint64_t nfull = len >> 6;
+    const uint4* q = reinterpret_cast<const uint4*>(p);
+    uint4 cur[4], nxt[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        cur[k] = nfull ? q[k] : make_uint4(0u, 0u, 0u, 0u);
+        nxt[k] = make_uint4(0u, 0u, 0u, 0u);
+    }
+    for (uint64_t b = 0; b < nfull; ++b) {
+        if (b + 1 < nfull) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) nxt[k] = q[4 * (b + 1) + k];
+        }
+        uint32_t w[16];
+        be16_from_raw(cur, w);
+        sha1_compress(h, w);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) cur[k] = nxt[k];
+    }
+    sha1_tail<true>(p, len, h);
+}
+
+// bytes [0, bytes) of LDS src to dst (16-byte aligned both), 16 per store
+__device__ __forceinline__ void small_copy_out(const uint8_t* src, uint8_t* dst, uint32_t bytes) {
+    const uint32_t whole = bytes & ~15u;
+    for (uint32_t b = 16 * threadIdx.x; b < whole; b += 16 * kSmallBlock)
+        *reinterpret_cast<uint4*>(dst + b) = *reinterpret_cast<const uint4*>(src + b);
+    for (uint32_t b = whole + threadIdx.x; b < bytes; b += kSmallBlock) dst[b] = src[b];
+}
+
+__global__ __launch_bounds__(kSmallBlock) void k_small_tree(const uint8_t* __restrict__ in, uint32_t n,
+                                                            uint8_t* __restrict__ out, uint32_t img_at,
+                                                            uint8_t* __restrict__ scratch,
+                                                            unsigned int* __restrict__ ticket) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
+    __shared__ uint32_t is_last;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t i = blockIdx.x * kSmallBlock + tid;
+    const uint64_t* desc = reinterpret_cast<const uint64_t*>(in);
+    uint32_t h[5] = {0u, 0u, 0u, 0u, 0u};
+    if (i < n) sha1_value_aligned(in + 16ull * n + desc[2 * i], desc[2 * i + 1], h);  // NewLeaf, merklenode.go:27-34
+    if (gridDim.x > 1) {
+        if (i < n) store_digest(scratch, i, h);
+        __threadfence();
+        __syncthreads();
+        if (tid == 0) is_last = atomicAdd(ticket, 1u) == gridDim.x - 1 ? 1u : 0u;
+        __syncthreads();
+        if (!is_last) return;
+        __threadfence();
+        if (tid == 0) atomicExch(ticket, 0u);  // the next launch counts from 0
+        for (uint32_t j = tid; j < n; j += kSmallBlock) {
+            const uint32_t* s = reinterpret_cast<const uint32_t*>(scratch + 20u * j);
+            uint32_t* d = reinterpret_cast<uint32_t*>(sm + 20u * j);
+#pragma unroll
+            for (int k = 0; k < 5; ++k) d[k] = __atomic_load_n(s + k, __ATOMIC_RELAXED);
+        }
+    } else if (i < n) {
+        store_digest(sm, i, h);
+    }
+    __syncthreads();
+    // every level above the leaves (at least one): a lone last node is hashed
+    // alone, its sibling being the empty pad (merkletree.go:32-34, :44-46)
+    uint32_t cnt = n, base = 0;
+    int lv = 1;
+    do {
+        const uint32_t pc = (cnt + 1) >> 1;
+        for (uint32_t j = tid; j < pc; j += kSmallBlock) {
+            const bool lone = 2 * j + 1 >= cnt;
+            uint32_t l[5], r[5] = {0u, 0u, 0u, 0u, 0u}, o[5];
+            load_digest(sm, base + 2 * j, l);
+            if (!lone) load_digest(sm, base + 2 * j + 1, r);
+            sha1_parent(l, r, lone, o);
+            store_digest(sm, base + cnt + j, o);
+        }
+        __syncthreads();
+        base += cnt;
+        cnt = pc;
+        ++lv;
+    } while (cnt > 1);
+    const uint32_t total = base + 1;
+    // the image, top level first: 0x00 + digest per node, one 0x01 after each
+    // odd level below the top (merklenode.go:37-63, MERKLE_NODE_EMPTY :11)
+    uint8_t* img = sm + ((20u * total + 15u) & ~15u);
+    uint32_t p = 0;
+    for (int L = lv - 1; L >= 0; --L) {
+        const uint32_t c = L == 0 ? n : ((n - 1) >> L) + 1;
+        uint32_t s = 0;
+        for (int j = 0; j < L; ++j) s += j == 0 ? n : ((n - 1) >> j) + 1;
+        for (uint32_t k = tid; k < c; k += kSmallBlock) {
+            uint8_t* o = img + p + 21u * k;
+            const uint8_t* d = sm + 20u * (s + k);
+            o[0] = 0u;
+#pragma unroll
+            for (int b = 0; b < 20; ++b) o[1 + b] = d[b];
+        }
+        p += 21u * c;
+        if (L < lv - 1 && (c & 1u)) {
+            if (tid == 0) img[p] = NKV_MERKLE_NODE_EMPTY;
+            ++p;
+        }
+    }
+    __syncthreads();
+    small_copy_out(sm, out, 20u * total);
+    small_copy_out(img, out + img_at, p);
+}
+
+// ---------------------------------------------------------------------------
 // host-side launchers
+
+uint32_t small_lds_bytes(uint64_t n, uint64_t total_nodes, uint64_t img_bytes) {
+    (void)n;
+    return uint32_t(((20 * total_nodes + 15) & ~uint64_t(15)) + ((img_bytes + 15) & ~uint64_t(15)));
+}
+
+hipError_t launch_small_tree(const uint8_t* in, uint32_t n, uint8_t* out, uint32_t img_at, uint32_t lds_bytes,
+                             uint8_t* scratch, unsigned int* ticket, hipStream_t s) {
+    if (n == 0 || n > kSmallMaxN || lds_bytes > kSmallMaxLds) return hipErrorInvalidValue;
+    static thread_local int attr_device = -1;  // the attribute is per device
+    int dev = -1;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (attr_device != dev) {
+        e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_small_tree),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, int(kSmallMaxLds));
+        if (e != hipSuccess) return e;
+        attr_device = dev;
+    }
+    const unsigned grid = unsigned((n + kSmallBlock - 1) / kSmallBlock);
+    hipLaunchKernelGGL(k_small_tree, dim3(grid), dim3(kSmallBlock), lds_bytes, s, in, n, out, img_at, scratch, ticket);
+    return hipGetLastError();
+}
 
 static inline unsigned grid_for(uint64_t n) { return unsigned((n + kBlock - 1) / kBlock); }
 

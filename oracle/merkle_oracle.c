@@ -33,6 +33,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <pthread.h>
+#include <time.h>
 
 /* ---------------- portable FIPS 180-4 SHA-1 ---------------- */
 
@@ -253,6 +254,49 @@ int nkvo_tree_from_digests(uint8_t *nodes, uint64_t n) {
     return lv;
 }
 
+/* The same tree with each level of at least 4096 parents split over `threads`
+ * (the all-cores CPU baseline, SURVEY.md 8(d) variant 2: "std::thread over
+ * leaf ranges + parallel levels").  Same bytes as nkvo_tree_from_digests. */
+typedef struct {
+    const uint8_t *prev;
+    uint8_t *cur;
+    uint64_t pc, lo, hi;
+} level_job;
+
+static void *level_worker(void *p) {
+    level_job *j = (level_job *)p;
+    for (uint64_t i = j->lo; i < j->hi; i++)
+        parent20(j->prev + 40 * i, (2 * i + 1 < j->pc) ? j->prev + 40 * i + 20 : NULL, j->cur + 20 * i);
+    return NULL;
+}
+
+int nkvo_tree_from_digests_mt(uint8_t *nodes, uint64_t n, int threads) {
+    uint64_t counts[72];
+    int lv = nkvo_level_counts(n, counts, 72);
+    if (lv <= 0) return -1;
+    if (threads < 1) threads = 1;
+    pthread_t *tid = calloc((size_t)threads, sizeof *tid);
+    level_job *jobs = calloc((size_t)threads, sizeof *jobs);
+    uint64_t base = 0;
+    for (int L = 1; L < lv; L++) {
+        const uint64_t pc = counts[L - 1], cc = counts[L];
+        uint8_t *prev = nodes + 20 * base;
+        const int t = cc >= 4096 ? threads : 1;
+        for (int k = 0; k < t; k++) {
+            jobs[k] = (level_job){prev, prev + 20 * pc, pc, cc * (uint64_t)k / (uint64_t)t,
+                                  cc * (uint64_t)(k + 1) / (uint64_t)t};
+            if (t == 1) level_worker(&jobs[k]);
+            else pthread_create(&tid[k], NULL, level_worker, &jobs[k]);
+        }
+        if (t > 1)
+            for (int k = 0; k < t; k++) pthread_join(tid[k], NULL);
+        base += pc;
+    }
+    free(tid);
+    free(jobs);
+    return lv;
+}
+
 /* New() with leaves of arbitrary Data: leaf i = data[off[i] .. +len[i]).
  * upper: levels 1..top (20 bytes each), level-major bottom-up. */
 int nkvo_tree_generic(const uint8_t *data, const uint64_t *off, const uint64_t *len, uint64_t n,
@@ -294,6 +338,43 @@ uint64_t nkvo_bfs_size(uint64_t n) {
         if (L < lv - 1 && (counts[L] & 1)) s += 1;
     }
     return s;
+}
+
+/* ---------------- CPU timing of one small flush (bench.py small_flush) ----------------
+ * `reps` flushes of the n values on the calling thread, each the whole Merkle
+ * step of sstable.makeMetadata (core/sstable/sstable.go:58-74) in memory:
+ * NewLeaf per value, New/build, the Serialize image -- fresh buffers per
+ * flush, as Go allocates them.  fn: the SHA-1 to use (NULL: this file's
+ * portable one; bench.py passes OpenSSL's from liboracle_ossl.so).  Returns the
+ * total seconds; root20: the last flush's root. */
+typedef void (*nkvo_sha1_fn)(const uint8_t *, uint64_t, uint8_t *);
+uint64_t nkvo_bfs_image(const uint8_t *nodes, uint64_t n, uint8_t *img);
+
+double nkvo_flush_reps(const uint8_t *base, const uint64_t *off, const uint64_t *len, uint64_t n, int reps,
+                       nkvo_sha1_fn fn, uint8_t *root20) {
+    if (n == 0 || reps < 1) return 0.0;
+    if (!fn) fn = nkvo_sha1;
+    const uint64_t total = nkvo_total_nodes(n), isz = nkvo_bfs_size(n);
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int r = 0; r < reps; r++) {
+        uint8_t *nodes = malloc(20 * total), *img = malloc(isz);
+        for (uint64_t i = 0; i < n; i++) fn(base + off[i], len[i], nodes + 20 * i);
+        uint64_t b = 0, pc = n;
+        do {
+            const uint64_t cc = (pc + 1) / 2;
+            uint8_t *prev = nodes + 20 * b, *cur = prev + 20 * pc;
+            for (uint64_t i = 0; i < cc; i++) fn(prev + 40 * i, 2 * i + 1 < pc ? 40 : 20, cur + 20 * i);
+            b += pc;
+            pc = cc;
+        } while (pc > 1);
+        nkvo_bfs_image(nodes, n, img);
+        if (r == reps - 1 && root20) memcpy(root20, nodes + 20 * (total - 1), 20);
+        free(nodes);
+        free(img);
+    }
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
 }
 
 /* BFS image from level-major nodes (20-byte leaves).  Returns bytes written. */

@@ -20,11 +20,37 @@ u8p = ctypes.POINTER(ctypes.c_uint8)
 u64p = ctypes.POINTER(ctypes.c_uint64)
 
 
+_SO_OSSL = os.path.join(_HERE, "liboracle_ossl.so")
+_ossl = None
+
+
+def _make(so: str, srcs) -> None:
+    srcs = [os.path.join(_HERE, f) for f in srcs] + [os.path.join(_HERE, "Makefile")]
+    if not os.path.exists(so) or os.path.getmtime(so) < max(os.path.getmtime(s) for s in srcs):
+        subprocess.check_call(["make", "-s", "-C", _HERE, os.path.basename(so)])
+
+
 def build() -> str:
-    srcs = [os.path.join(_HERE, f) for f in ("merkle_oracle.c", "record_crc_oracle.c", "bloom_oracle.c")]
-    if not os.path.exists(_SO) or os.path.getmtime(_SO) < max(os.path.getmtime(s) for s in srcs):
-        subprocess.check_call(["make", "-s", "-C", _HERE, "liboracle.so"])
+    _make(_SO, ("merkle_oracle.c", "record_crc_oracle.c", "bloom_oracle.c"))
+    _make(_SO_OSSL, ("merkle_openssl.c",))
     return _SO
+
+
+def ossl():
+    """liboracle_ossl.so: the leaf hash + tree with OpenSSL's SHA-1 (libcrypto),
+    the strongest CPU baseline (bench.py cpu_baseline)."""
+    global _ossl
+    if _ossl is None:
+        build()
+        L = ctypes.CDLL(_SO_OSSL)
+        L.nkvo_ossl_sha1.argtypes = [u8p, ctypes.c_uint64, u8p]
+        L.nkvo_ossl_leaf_hashes.argtypes = [u8p, u64p, u64p, ctypes.c_uint64, u8p, ctypes.c_int]
+        L.nkvo_ossl_leaf_hashes_strided.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, u8p,
+                                                    ctypes.c_int]
+        L.nkvo_ossl_tree_from_digests.argtypes = [u8p, ctypes.c_uint64, ctypes.c_int]
+        L.nkvo_ossl_tree_from_digests.restype = ctypes.c_int
+        _ossl = L
+    return _ossl
 
 
 def lib():
@@ -43,6 +69,10 @@ def lib():
         L.nkvo_total_nodes.restype = ctypes.c_uint64
         L.nkvo_tree_from_digests.argtypes = [u8p, ctypes.c_uint64]
         L.nkvo_tree_from_digests.restype = ctypes.c_int
+        L.nkvo_flush_reps.argtypes = [u8p, u64p, u64p, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p, u8p]
+        L.nkvo_flush_reps.restype = ctypes.c_double
+        L.nkvo_tree_from_digests_mt.argtypes = [u8p, ctypes.c_uint64, ctypes.c_int]
+        L.nkvo_tree_from_digests_mt.restype = ctypes.c_int
         L.nkvo_tree_generic.argtypes = [u8p, u64p, u64p, ctypes.c_uint64, u8p]
         L.nkvo_tree_generic.restype = ctypes.c_int
         L.nkvo_bfs_size.argtypes = [ctypes.c_uint64]
@@ -110,6 +140,58 @@ def leaf_hashes_strided(base: np.ndarray, stride: int, L: int, n: int, threads: 
     return out[:n]
 
 
+def ossl_sha1(data: bytes) -> bytes:
+    a = np.frombuffer(bytes(data) + b"\0", dtype=np.uint8)
+    out = np.zeros(20, np.uint8)
+    ossl().nkvo_ossl_sha1(_p8(a), len(data), _p8(out))
+    return out.tobytes()
+
+
+def ossl_leaf_hashes(base: np.ndarray, off: np.ndarray, ln: np.ndarray, threads: int = 1) -> np.ndarray:
+    base = np.ascontiguousarray(base, np.uint8)
+    if base.size == 0:
+        base = np.zeros(1, np.uint8)
+    off = np.ascontiguousarray(off, np.uint64)
+    ln = np.ascontiguousarray(ln, np.uint64)
+    n = off.size
+    out = np.zeros((max(n, 1), 20), np.uint8)
+    ossl().nkvo_ossl_leaf_hashes(_p8(base), _p64(off), _p64(ln), n, _p8(out), threads)
+    return out[:n]
+
+
+def ossl_leaf_hashes_strided(base: np.ndarray, stride: int, L: int, n: int, threads: int = 1) -> np.ndarray:
+    base = np.ascontiguousarray(base, np.uint8)
+    out = np.zeros((max(n, 1), 20), np.uint8)
+    ossl().nkvo_ossl_leaf_hashes_strided(_p8(base), stride, L, n, _p8(out), threads)
+    return out[:n]
+
+
+def ossl_tree_from_digests(leaf20: np.ndarray, threads: int = 1) -> np.ndarray:
+    """tree_from_digests with OpenSSL's SHA-1, wide levels over `threads`."""
+    leaf20 = np.ascontiguousarray(leaf20, np.uint8).reshape(-1, 20)
+    n = leaf20.shape[0]
+    nodes = np.zeros((total_nodes(n), 20), np.uint8)
+    nodes[:n] = leaf20
+    if ossl().nkvo_ossl_tree_from_digests(_p8(nodes), n, threads) < 0:
+        raise ValueError("cannot build Merkle Tree from 0 nodes")
+    return nodes
+
+
+def flush_us(base: np.ndarray, off: np.ndarray, ln: np.ndarray, reps: int, openssl: bool = False):
+    """(microseconds per flush, root hex) of `reps` in-memory flushes on this
+    thread (leaf hashes + tree + image, nkvo_flush_reps), with the portable
+    SHA-1 or OpenSSL's."""
+    base = np.ascontiguousarray(base, np.uint8)
+    if base.size == 0:
+        base = np.zeros(1, np.uint8)
+    off = np.ascontiguousarray(off, np.uint64)
+    ln = np.ascontiguousarray(ln, np.uint64)
+    fn = ctypes.cast(ossl().nkvo_ossl_sha1, ctypes.c_void_p) if openssl else None
+    root = np.zeros(20, np.uint8)
+    s = lib().nkvo_flush_reps(_p8(base), _p64(off), _p64(ln), off.size, reps, fn, _p8(root))
+    return s / reps * 1e6, root.tobytes().hex()
+
+
 def num_levels(n: int) -> int:
     return lib().nkvo_num_levels(n)
 
@@ -118,13 +200,16 @@ def total_nodes(n: int) -> int:
     return lib().nkvo_total_nodes(n)
 
 
-def tree_from_digests(leaf20: np.ndarray) -> np.ndarray:
-    """All levels, level-major bottom-up, shape (total_nodes, 20).  Root is the last row."""
+def tree_from_digests(leaf20: np.ndarray, threads: int = 1) -> np.ndarray:
+    """All levels, level-major bottom-up, shape (total_nodes, 20).  Root is the last row.
+    threads > 1: wide levels split over that many threads (same bytes)."""
     leaf20 = np.ascontiguousarray(leaf20, np.uint8).reshape(-1, 20)
     n = leaf20.shape[0]
     nodes = np.zeros((total_nodes(n), 20), np.uint8)
     nodes[:n] = leaf20
-    if lib().nkvo_tree_from_digests(_p8(nodes), n) < 0:
+    rc = (lib().nkvo_tree_from_digests_mt(_p8(nodes), n, threads) if threads > 1
+          else lib().nkvo_tree_from_digests(_p8(nodes), n))
+    if rc < 0:
         raise ValueError("cannot build Merkle Tree from 0 nodes")
     return nodes
 

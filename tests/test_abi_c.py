@@ -1,0 +1,78 @@
+"""The C-ABI from plain C, as cgo compiles it.
+
+include/nkv_merkle.h is built under gcc -std=c99 -pedantic -Werror with a small
+C program (tests/c/abi_c99.c) that calls the flush's entry points
+(nkv_tree_from_values, the shape functions) and prints the results; on CPU it
+must build, link and fail cleanly without a device; on the GPU its root and
+image must equal the oracle's on the same bytes, on the one-launch small path
+(n <= 1024) and on the grid path.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "tests", "c", "abi_c99.c")
+
+
+def build_c(tmpdir):
+    from nakevaleng_amd import build as b
+    so = b.build(quiet=True)
+    libdir = os.path.dirname(so)
+    exe = os.path.join(str(tmpdir), "abi_c99")
+    subprocess.check_call(["gcc", "-std=c99", "-pedantic", "-Werror", "-Wall", "-Wextra", "-O1",
+                           "-I", os.path.join(ROOT, "include"), SRC, "-L", libdir, "-lnkvmerkle",
+                           f"-Wl,-rpath,{libdir}", "-o", exe])
+    return exe
+
+
+def run(exe, n):
+    out = subprocess.run([exe, str(n)], capture_output=True, text=True, timeout=120)
+    return out.returncode, dict(line.split(" ", 1) for line in out.stdout.strip().splitlines()), out.stderr
+
+
+def inputs(n):
+    ln = (np.arange(n, dtype=np.uint64) * 37) % 301
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum(ln[:-1])
+    total = int(ln.sum())
+    base = ((np.arange(total + 1, dtype=np.uint64) * 131 + 7) & 255).astype(np.uint8)
+    return base, off, ln
+
+
+def fnv1a64(b: bytes) -> str:
+    h = 14695981039346656037
+    for x in b:
+        h = ((h ^ x) * 1099511628211) & 0xFFFFFFFFFFFFFFFF
+    return f"{h:016x}"
+
+
+def test_header_is_c99_and_shapes_without_device(tmp_path, oracle):
+    """Compiles as C99 -pedantic -Werror, links, and on a machine without a GPU
+    prints the pure shape functions and fails the context cleanly."""
+    exe = build_c(tmp_path)
+    if os.environ.get("HIP_VISIBLE_DEVICES") is None and os.path.exists("/dev/kfd"):
+        pytest.skip("a GPU is visible: the device half runs in test_c_caller_on_gpu")
+    rc, kv, err = run(exe, 1000)
+    assert rc == 0, err
+    assert kv["abi"] == "1"
+    assert int(kv["levels"]) == oracle.num_levels(1000)
+    assert int(kv["total"]) == oracle.total_nodes(1000)
+    assert int(kv["bfs"]) == oracle.bfs_size(1000)
+    assert kv["device"].startswith("none")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 10, 1000, 1024, 1025, 5000])
+def test_c_caller_on_gpu(tmp_path, oracle, n):
+    exe = build_c(tmp_path)
+    rc, kv, err = run(exe, n)
+    assert rc == 0, err
+    base, off, ln = inputs(n)
+    nodes = oracle.tree_from_digests(oracle.leaf_hashes(base, off, ln))
+    assert kv["root"] == nodes[-1].tobytes().hex()
+    assert kv["img_fnv"] == fnv1a64(oracle.bfs_image(nodes, n))
+    assert kv["path"] == ("1" if n <= 1024 else "0")
+    assert kv["empty"] == "1 cannot build Merkle Tree from 0 nodes"

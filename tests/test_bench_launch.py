@@ -261,16 +261,31 @@ def test_merged_line_shape(monkeypatch, capsys):
         calls.append((world, tuple(extra)))
         return {"value": 2.0, "verified_vs_oracle": True, "n_gpus": world}
     monkeypatch.setattr(bench, "capi_child", fake_child)
-    monkeypatch.setattr(bench, "cpu_baseline", lambda n, v: {"value": 1.25, "unit": "GiB/s", "cores": 1,
-                                                              "kind": "port", "sample": f"{n} x {v}"})
+    subs = []
+
+    def fake_sub(args, config, timeout, run=None):
+        subs.append(config)
+        return {"value": 3.0 if config == "mixed" else 4.0, "verified_vs_oracle": True,
+                "roofline": {"frac": 0.4}, "cpu_baseline": {"value": 20.0, "best": "all_cores_openssl"}}
+    monkeypatch.setattr(bench, "sub_child", fake_sub)
+    monkeypatch.setattr(bench, "cpu_baseline", lambda a: {"value": 1.25, "unit": "GiB/s", "cores": 1,
+                                                           "kind": "port", "port_1core": {"value": 0.5},
+                                                           "sample": f"{a.leaves} x {a.value_bytes}"})
     bench.main()
     line = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
     assert line["verified_vs_oracle"] is True and line["verified_ranks"] == [True]
     assert line["capi_group"]["value"] == 2.0 and line["capi_one_tree"]["verified_vs_oracle"] is True
     assert line["cpu_baseline"]["cores"] == 1 and line["cpu_baseline"]["sample"] == f"{1 << 20} x 4096"
+    assert line["vs_cpu_best"] == 0.8 and line["vs_cpu_port_1core"] == 2.0
     assert calls == [(1, ()), (1, ("--config", "one_tree", "--tables", "1")),
                      (1, ("--leaves", str(8 << 20), "--tables", "1"))]
     assert line["capi_config4"]["n_gpus"] == 1
+    # configs[2] and the records form of configs[1] as
+    # fresh-child sub-records, each with its own roofline and CPU baseline
+    assert subs == ["mixed", "records"]
+    assert line["config2_mixed"]["value"] == 3.0 and line["config1_records"]["value"] == 4.0
+    for k in ("config2_mixed", "config1_records"):
+        assert line[k]["verified_vs_oracle"] is True and "roofline" in line[k] and "cpu_baseline" in line[k]
 
 
 def test_merged_line_at_n_gpus_keeps_cpu_baseline(monkeypatch, capsys):
@@ -280,10 +295,12 @@ def test_merged_line_at_n_gpus_keeps_cpu_baseline(monkeypatch, capsys):
     monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "8", "--config", "runs4", "--no-capi"])
     monkeypatch.setattr(bench, "run_ranks", lambda args, T: {"n_gpus": 8, "value": 8.0})
     monkeypatch.setattr(bench, "capi_child", lambda *a, **k: pytest.fail("--no-capi"))
-    monkeypatch.setattr(bench, "cpu_baseline", lambda n, v: {"value": 1.0, "cores": 1})
+    monkeypatch.setattr(bench, "cpu_baseline", lambda a: {"value": 1.0, "cores": 1, "port_1core": {"value": 1.0}})
+    monkeypatch.setattr(bench, "sub_child", lambda *a, **k: pytest.fail("sub-configs are N = 1 only"))
     bench.main()
     line = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
-    assert line["cpu_baseline"] == {"value": 1.0, "cores": 1} and "capi_group" not in line
+    assert line["cpu_baseline"]["value"] == 1.0 and "capi_group" not in line
+    assert "config2_mixed" not in line and line["vs_cpu_best"] == 8.0
 
 
 def test_other_ranks_print_nothing(monkeypatch, capsys):
@@ -400,3 +417,73 @@ def test_rank_verification_world2(oracle, bad_rank):
         p.join(timeout=60)
     want_codes = [1, 1] if bad_rank < 0 else [1, 0]
     assert res[0] == res[1] == (want_codes, bad_rank < 0)
+
+
+def test_sub_child_command_env_and_errors(monkeypatch):
+    """The sub-config child: this run's flags + --config C --gpus 1 --no-capi
+    --no-subconfigs (no recursion), outside any launcher; its line's keys kept;
+    a failing or hung child gives {"error": ...}."""
+    import subprocess
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--steps", "7", "--warmup", "2"])
+    monkeypatch.setenv("WORLD_SIZE", "1")
+    args = bench.parse(["--steps", "7", "--warmup", "2"])
+    seen = {}
+
+    class P:
+        returncode = 0
+        stdout = json.dumps({"value": 2700.0, "n_gpus": 1, "roofline": {"frac": 0.37, "chain_frac": 0.9},
+                             "verified_vs_oracle": True, "cpu_baseline": {"value": 25.0},
+                             "vs_cpu_best": 108.0, "config": {"workload": "mixed"}, "other": 1}) + "\n"
+
+    def run(cmd, **kw):
+        seen["cmd"], seen["env"] = cmd, kw["env"]
+        return P()
+    sub = bench.sub_child(args, "mixed", 100, run=run)
+    cmd = seen["cmd"]
+    child = bench.parse(cmd[2:])
+    assert child.config == "mixed" and child.gpus == 1 and child.no_capi and child.no_subconfigs
+    assert child.steps == 7 and child.warmup == 2 and child.tables == 1
+    assert "WORLD_SIZE" not in seen["env"] and seen["env"]["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+    assert sub["value"] == 2700.0 and sub["roofline"]["chain_frac"] == 0.9 and sub["cpu_baseline"]["value"] == 25.0
+    assert sub["workload"] == "mixed" and "other" not in sub
+
+    class Bad:
+        returncode = 1
+        stdout = ""
+    assert "error" in bench.sub_child(args, "records", 100, run=lambda cmd, **kw: Bad())
+
+    def hang(cmd, **kw):
+        raise subprocess.TimeoutExpired(cmd, 100)
+    assert "timed out" in bench.sub_child(args, "records", 100, run=hang)["error"]
+
+
+def test_cpu_baseline_variants_small(oracle, monkeypatch):
+    """cpu_baseline times the four SURVEY 8(d) variants on the same sample (the
+    portable port and OpenSSL, one core and every core), they agree on the root,
+    and `value` is the strongest; for every config kind."""
+    monkeypatch.setenv("OMP_NUM_THREADS", "2")
+    for argv, n in ((["--leaves", "64", "--value-bytes", "4096", "--cpu-sample-leaves", "64"], 64),
+                    (["--config", "records", "--leaves", "48", "--cpu-sample-leaves", "48"], 48),
+                    (["--config", "mixed", "--mixed-bytes", str(1 << 20)], None)):
+        a = bench.parse(argv)
+        cb = bench.cpu_baseline(a)
+        vals = {k: cb[k]["value"] for k, _, _ in bench.CPU_VARIANTS}
+        assert cb["value"] == max(vals.values()) and cb["best"] in vals
+        assert cb["port_1core"]["cores"] == 1 and cb["all_cores_openssl"]["cores"] == 2
+        assert cb["cpu_model"] and cb["host_threads"] == 2
+        s = bench.cpu_sample(a)
+        if n:
+            assert s["n"] == n
+        want = (oracle.tree_from_digests(oracle.leaf_hashes_strided(s["data"], s["stride"], s["L"], s["n"]))
+                if "stride" in s else oracle.tree_from_digests(oracle.leaf_hashes(s["data"], s["off"], s["lens"])))
+        assert cb["root"] == want[-1].tobytes().hex()
+
+
+def test_records_cpu_sample_layout():
+    """The records CPU sample hashes each record's Value where the GPU line's
+    table has it: record r at r x record size, its Value at +30 + KeySize
+    (record.go:191-199), ValueSize = record size - 30 - KeySize."""
+    a = bench.parse(["--config", "records", "--leaves", "1024", "--cpu-sample-leaves", "1024",
+                     "--value-bytes", "1024"])
+    s = bench.cpu_sample(a)
+    assert s["n"] == 1024 and int(s["lens"][0]) == 1024 - 30 - 16 and int(s["off"][1]) == 1024 + 46

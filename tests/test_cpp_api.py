@@ -59,6 +59,26 @@ def test_task_team_cpu(tmp_path, sanitize):
         out.stdout + out.stderr[-3000:]
 
 
+@pytest.mark.parametrize("sanitize", [False, True])
+def test_session_shared_by_threads_cpu(tmp_path, sanitize):
+    """trees serialized and destroyed on several threads at once
+    (the session's recycled storage is locked; the host team runs one caller's
+    run at a time, the others inline), no GPU needed; also under
+    ThreadSanitizer (host code only)."""
+    from nakevaleng_amd import build as b
+    so = b.build()
+    libdir = os.path.dirname(so)
+    exe = os.path.join(str(tmp_path), "test_session_threads")
+    flags = ["-O1", "-g", "-fsanitize=thread"] if sanitize else ["-O2"]
+    subprocess.check_call(["g++", "-std=c++17", "-Wall", "-pthread", *flags, "-I", os.path.join(ROOT, "include"),
+                           os.path.join(ROOT, "tests", "cpp", "test_session_threads.cpp"), "-L", libdir,
+                           "-lnkvmerkle", f"-Wl,-rpath,{libdir}", "-o", exe])
+    out = subprocess.run([exe, str(tmp_path), "300" if sanitize else "3000"], capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode == 0 and out.stdout.startswith("ok") and "WARNING" not in out.stderr, \
+        out.stdout + out.stderr[-3000:]
+
+
 @pytest.mark.gpu
 def test_cpp_mirror_on_gpu(tmp_path, oracle):
     exe = build_binary(str(tmp_path))

@@ -276,6 +276,45 @@ def test_group_refuses_pointers_on_another_device(nkv, oracle, devs):
             assert np.array_equal(keep[4 * t + 3].cpu().numpy().reshape(-1, 20), w), t
 
 
+@pytest.mark.parametrize("devs", device_sets(COUNT))
+def test_group_peer_access(nkv, oracle, devs):
+    """nkv_group_create enables xGMI peer access for every
+    pair of distinct member GPUs (hipDeviceEnablePeerAccess; a pair already
+    enabled counts), and nkv_group_tree_fetch's copies over those mappings
+    return the whole split tree bit-exact.  Every pair the runtime reports as
+    mappable (hipDeviceCanAccessPeer, through torch) must read
+    NKV_PEER_ENABLED; a member with itself reads NKV_PEER_SAME."""
+    _lib, _ = nkv
+    L = _lib.lib()
+    g = len(devs)
+    with _lib.Group(devs) as grp:
+        for i in range(g):
+            for j in range(g):
+                st = grp.peer_access(i, j)
+                if devs[i] == devs[j]:
+                    assert st == _lib.NKV_PEER_SAME
+                elif torch.cuda.can_device_access_peer(devs[i], devs[j]):
+                    assert st == _lib.NKV_PEER_ENABLED, (i, j)
+                else:
+                    assert st == _lib.NKV_PEER_NONE
+        s = ctypes.c_int()
+        assert L.nkv_group_peer_access(grp.h, g, 0, ctypes.byref(s)) == _lib.NKV_ERR_INVALID
+        assert L.nkv_group_peer_access(grp.h, 0, -1, ctypes.byref(s)) == _lib.NKV_ERR_INVALID
+        assert L.nkv_group_peer_access(grp.h, 0, 0, None) == _lib.NKV_ERR_INVALID
+        # the split tree's nodes and image fetched to the host across the members
+        n, vl = 65537, 64
+        data = np.frombuffer(np.random.default_rng(11).bytes(n * vl), np.uint8).copy()
+        want = oracle.tree_from_digests(oracle.leaf_hashes_strided(data, vl, vl, n))
+        parts, pk = split_parts_on(_lib, devs, n, data, vl)
+        check_split(_lib, L, oracle, grp, devs, parts, n, want)
+    # a second group over the same devices: the mappings are already there
+    with _lib.Group(devs) as grp2:
+        for i in range(g):
+            for j in range(g):
+                if devs[i] != devs[j] and torch.cuda.can_device_access_peer(devs[i], devs[j]):
+                    assert grp2.peer_access(i, j) == _lib.NKV_PEER_ENABLED
+
+
 @pytest.mark.parametrize("devs", mixed_sets(COUNT))
 def test_group_mixed_copy_transport(nkv, oracle, devs):
     """[0, 0, 1]: device 0 twice, so the copy transport -- across two GPUs:
@@ -285,6 +324,9 @@ def test_group_mixed_copy_transport(nkv, oracle, devs):
     L = _lib.lib()
     with _lib.Group(devs) as grp:
         assert grp.transport == _lib.NKV_TRANSPORT_COPY
+        assert grp.peer_access(0, 1) == grp.peer_access(1, 0) == _lib.NKV_PEER_SAME
+        if torch.cuda.can_device_access_peer(0, 1):
+            assert grp.peer_access(0, 2) == grp.peer_access(2, 1) == _lib.NKV_PEER_ENABLED
         tabs, wants, keep = member_tables(_lib, L, oracle, devs)
         k = len(tabs)
         roots = np.zeros(20 * k, np.uint8)

@@ -590,9 +590,12 @@ def test_pruned_variants_are_refused(nkv):
         assert L.nkv_ctx_set_option(ctx.h, _lib.NKV_OPT_LEAF_LOAD, v) == _lib.NKV_ERR_INVALID
     for v in (4, 11):
         assert L.nkv_ctx_set_option(ctx.h, _lib.NKV_OPT_LEAF_LOAD, v) == _lib.NKV_OK
-    for key in (3, 9):  # the retired DEEP_PREFETCH and QUEUE_RING keys (round 4)
-        for v in (0, 3, 13):
+    # the retired DEEP_PREFETCH and QUEUE_RING keys accept their only value
+    # until an ABI version bump, and nothing else
+    for key, only in ((3, 3), (9, 13)):
+        for v in (0, 1, 4, 12, 14):
             assert L.nkv_ctx_set_option(ctx.h, key, v) == _lib.NKV_ERR_INVALID
+        assert L.nkv_ctx_set_option(ctx.h, key, only) == _lib.NKV_OK
     for v in (0, 4, 5):
         assert L.nkv_ctx_set_option(ctx.h, _lib.NKV_OPT_QUEUE_WAVES, v) == _lib.NKV_ERR_INVALID
     assert L.nkv_ctx_set_option(ctx.h, _lib.NKV_OPT_QUEUE_WAVES, 3) == _lib.NKV_OK

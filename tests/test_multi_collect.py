@@ -27,6 +27,8 @@ def test_collected_over_eight_devices():
     assert "tests/test_gpu_multi.py::test_group_split_fuzz_distinct_devices[0-devs01234567]" in ids
     assert "tests/test_gpu_multi.py::test_group_refuses_pointers_on_another_device[devs01234567]" in ids
     assert "tests/test_gpu_multi.py::test_group_mixed_copy_transport[devs001]" in ids
+    assert "tests/test_gpu_multi.py::test_group_peer_access[devs01234567]" in ids
+    assert "tests/test_gpu_multi.py::test_group_peer_access[devs01]" in ids
     assert "tests/test_gpu_multi.py::test_bench_nccl_world_n[world8]" in ids
 
 

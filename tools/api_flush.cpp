@@ -23,6 +23,10 @@
 //                 write (MerkleTree::LastSerializeTiming)
 //
 // Usage: api_flush N VLEN CYCLES DIR [STREAMING=1] [SEED] [NONTEMPORAL=1] [COPY_THREADS=-1] [RETAIN_HEAP=1]
+//                  [RESERVE=1]
+// (RESERVE 1: Session::Reserve sizes the pinned arena before the first flush,
+// as an engine does once from its memtable capacity; 0: the first flush grows
+// it by doubling.)
 // (COPY_THREADS -1: the mirror's default, min(16, cores) or NKV_COPY_THREADS.
 // RETAIN_HEAP 1: the process keeps freed memory mapped between flushes, as a Go
 // process's garbage-collected heap does; glibc's default hands every block over
@@ -76,6 +80,7 @@ int main(int argc, char** argv) {
     const bool nontemporal = argc > 7 ? std::atoi(argv[7]) != 0 : true;
     const int copy_threads = argc > 8 ? std::atoi(argv[8]) : -1;
     const bool retain_heap = argc > 9 ? std::atoi(argv[9]) != 0 : true;
+    const bool reserve = argc > 10 ? std::atoi(argv[10]) != 0 : true;
     if (retain_heap) {
         mallopt(M_MMAP_THRESHOLD, 1 << 30);  // large blocks from the heap, not fresh mappings
         mallopt(M_TRIM_THRESHOLD, -1);       // and the heap is not trimmed on free
@@ -87,6 +92,12 @@ int main(int argc, char** argv) {
     S.SetNonTemporal(nontemporal);
     if (copy_threads >= 0) S.SetCopyThreads(copy_threads);
     check(nkv_ctx_set_timing(S.ctx(), NKV_TIMING_EVENTS), "timing");
+    // RESERVE 1: the engine sizes the arena once at start from the memtable's
+    // capacity (what the Go shim's merkletree.Reserve does from coreconf's
+    // MEMTABLE_THRESHOLD), outside any flush; 0: the first flush grows it
+    const auto r0 = clk::now();
+    if (reserve) S.Reserve(n * ((vlen + 15) & ~uint64_t(15)));
+    const double reserve_ms = ms(r0, clk::now());
     for (int cyc = 0; cyc < cycles; ++cyc) {
         const std::string fname = dir + "/api_flush-1-" + std::to_string(cyc) + "-metadata.db";
         unlink(fname.c_str());
@@ -116,11 +127,12 @@ int main(int argc, char** argv) {
             "\"total_ms\": %.3f, \"newleaf_ms\": %.3f, \"new_call_ms\": %.3f, \"upload_ms\": %.3f, "
             "\"kernels_ms\": %.3f, \"download_ms\": %.3f, \"materialize_ms\": %.3f, \"root_ms\": %.3f, "
             "\"walk_ms\": %.3f, \"write_ms\": %.3f, \"image_bytes\": %zu, \"arena_allocs\": %llu, "
-            "\"root\": \"%s\"}\n",
+            "\"reserve\": %d, \"reserve_ms\": %.3f, \"root\": \"%s\"}\n",
             cyc, (unsigned long long)n, (unsigned long long)vlen, int(streaming), int(nontemporal), S.CopyThreads(), int(retain_heap),
             double(n * vlen) / (total * 1e-3) / double(1ull << 30), total, ms(t0, t1),
             tree->LastNewTiming().call_ms, up, ker, down, tree->LastNewTiming().materialize_ms, ms(t2, t3),
-            st.walk_ms, st.write_ms, size_t(st.bytes), (unsigned long long)S.arena_allocs(), root.c_str());
+            st.walk_ms, st.write_ms, size_t(st.bytes), (unsigned long long)S.arena_allocs(), int(reserve),
+            reserve_ms, root.c_str());
         std::fflush(stdout);
     }
     return 0;
