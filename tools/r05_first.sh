@@ -9,7 +9,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
 OUT=gpurun_out/${OUT:-r05a}
 mkdir -p "$OUT"
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-timeout -k 10 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu -p no:cacheprovider \
+NKV_DEBUG=1 timeout -k 10 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu -p no:cacheprovider \
     tests/test_gpu_small.py tests/test_abi_c.py > "$OUT/small_tests.log" 2>&1
 rc=$?; tail -4 "$OUT/small_tests.log"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -u bench.py --config small_flush > "$OUT/small_flush.json" 2> "$OUT/small_flush.err"
