@@ -239,8 +239,6 @@ int small_tree(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint6
     const uint64_t img_len = layout_of(counts_of(n)).total;
     const uint64_t img_at = align16(20 * tot);
     const uint64_t in_bytes = 16 * n + vbytes, out_bytes = img_at + align16(img_len);
-    const uint32_t lds = small_lds_bytes(n, tot, img_len);
-    if (lds > kSmallMaxLds) return NKV_OK;
     uint64_t lo = 0, hi = 0;  // a call over a pinned block ends its batch (nkv_host_stream)
     if (nkv_ctx::Pinned* blk = pinned_extent(c, base, off, len, n, &lo, &hi)) blk->streamed = 0;
     TRY(grow_coherent(&c->h_sin, &c->h_sin_cap, in_bytes));
@@ -264,7 +262,7 @@ int small_tree(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint6
         TRY(grow(c->d_sout, out_bytes));
         HIPTRY(hipMemcpyAsync(c->d_sin.p, c->h_sin, in_bytes, hipMemcpyHostToDevice, c->stream));
         HIPTRY(launch_small_tree(static_cast<const uint8_t*>(c->d_sin.p), uint32_t(n),
-                                 static_cast<uint8_t*>(c->d_sout.p), uint32_t(img_at), lds, scratch, ticket,
+                                 static_cast<uint8_t*>(c->d_sout.p), uint32_t(img_at), scratch, ticket,
                                  c->stream));
         HIPTRY(hipMemcpyAsync(c->h_sout, c->d_sout.p, out_bytes, hipMemcpyDeviceToHost, c->stream));
     } else {  // the kernel reads the values and writes its results across PCIe
@@ -272,7 +270,7 @@ int small_tree(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint6
         HIPTRY(hipHostGetDevicePointer(&din, c->h_sin, 0));
         HIPTRY(hipHostGetDevicePointer(&dout, c->h_sout, 0));
         HIPTRY(launch_small_tree(static_cast<const uint8_t*>(din), uint32_t(n), static_cast<uint8_t*>(dout),
-                                 uint32_t(img_at), lds, scratch, ticket, c->stream));
+                                 uint32_t(img_at), scratch, ticket, c->stream));
     }
     HIPTRY(hipStreamSynchronize(c->stream));
     if (nodes_out) memcpy(nodes_out, c->h_sout, 20 * tot);

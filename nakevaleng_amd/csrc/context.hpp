@@ -4,6 +4,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
 
 #include <algorithm>
 #include <new>
@@ -81,12 +83,27 @@ inline int st(hipError_t e) {
     return NKV_ERR_DEVICE;
 }
 
+// NKV_DEBUG=1 in the environment: every failing HIP call behind HIPTRY is
+// named on stderr (the status code alone does not say which call failed)
+inline bool debug_on() {
+    static const bool on = [] {
+        const char* e = getenv("NKV_DEBUG");
+        return e && *e && *e != '0';
+    }();
+    return on;
+}
+inline int st_at(hipError_t e, const char* what, const char* file, int line) {
+    if (e != hipSuccess && debug_on())
+        fprintf(stderr, "nkv: %s:%d: %s -> %s\n", file, line, what, hipGetErrorString(e));
+    return st(e);
+}
+
 #define TRY(x)                         \
     do {                               \
         int _rc = (x);                 \
         if (_rc != NKV_OK) return _rc; \
     } while (0)
-#define HIPTRY(x) TRY(::nkv::st(x))
+#define HIPTRY(x) TRY(::nkv::st_at((x), #x, __FILE__, __LINE__))
 // Every C-ABI entry is a function-try-block: a host allocation or thread start
 // that throws inside the library becomes a status code, never an exception
 // crossing the C boundary (cgo / ctypes callers cannot catch it).

@@ -241,10 +241,13 @@ __global__ __launch_bounds__(kCrcLanesWG) void k_crc_lanes(const uint8_t* __rest
     // lane constants of the two halves: the copy offset (byte 0), the half (byte
     // 2), built on the table's real LDS address.  The v_perm address
     // form has no room for a base, so the table must be the kernel's only LDS
-    // object, at address 0: anything else is a build defect, stopped here
-    // rather than left to give wrong checksums.
+    // object, at address 0: the launcher checks the kernel's LDS size once
+    // (lanes_layout_ok) and refuses to launch otherwise (a trap here
+    // would take the whole process down); the diagnostic build also asserts it.
     const uint32_t lds_tab = uint32_t(reinterpret_cast<uintptr_t>(tab));
+#ifdef NKV_DIAG
     if (lds_tab != 0u) __builtin_trap();
+#endif
     const uint32_t la0 = lds_tab + (threadIdx.x & 31u) * 4u, la1 = la0 | 0x10000u;
     const uint64_t stride = uint64_t(gridDim.x) * WG;
     const uint64_t w0 = uint64_t(blockIdx.x) * WG + (threadIdx.x & ~63u);  // this wave's first span
@@ -505,8 +508,26 @@ static void launch_crc(int variant, const uint8_t* base, const uint64_t* off, co
     go(k_crc_lanes<RECORDS>, kCrcLanesWG);
 }
 
+// k_crc_lanes addresses its table by v_perm with no base, so the table must
+// be the kernel's only LDS object (at address 0): its static LDS size is
+// exactly the table's.  Checked once per process and kernel on the host.
+template <bool RECORDS>
+static hipError_t lanes_layout_ok() {
+    static const hipError_t ok = [] {
+        hipFuncAttributes a;
+        hipError_t e = hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&k_crc_lanes<RECORDS>));
+        if (e != hipSuccess) return e;
+        return a.sharedSizeBytes == size_t(kLaneTabWords) * 4 ? hipSuccess : hipErrorInvalidDeviceFunction;
+    }();
+    return ok;
+}
+
 hipError_t launch_crc_spans(const uint8_t* base, const uint64_t* off, const uint64_t* len, uint64_t n,
                             uint32_t* out, int variant, hipStream_t s) {
+    if (variant != 8) {
+        const hipError_t e = lanes_layout_ok<false>();
+        if (e != hipSuccess) return e;
+    }
     launch_crc<false>(variant, base, off, len, 0, n, out, nullptr, s, Gate{});
     return hipGetLastError();
 }
@@ -514,6 +535,10 @@ hipError_t launch_crc_spans(const uint8_t* base, const uint64_t* off, const uint
 hipError_t launch_record_crc(const uint8_t* stream, uint64_t stream_len, const uint64_t* rec_off, uint64_t n,
                              uint32_t* out, unsigned long long* stats, int variant, hipStream_t s, Gate gate,
                              bool init_stats) {
+    if (variant != 8) {
+        const hipError_t e = lanes_layout_ok<true>();
+        if (e != hipSuccess) return e;
+    }
     if (init_stats) {
         hipError_t e = hipMemsetAsync(stats, 0, 3 * sizeof(unsigned long long), s);
         if (e == hipSuccess) e = hipMemsetAsync(stats + 1, 0xFF, sizeof(unsigned long long), s);

@@ -166,12 +166,10 @@ hipError_t launch_fill(uint8_t* buf, uint64_t nbytes, uint64_t seed, hipStream_t
 // pairs then the values at in + 16 n + offset (16-byte aligned); out receives
 // the nodes (level-major) and, at out + img_at (16-byte aligned), the Serialize
 // image.  scratch: 20 n device bytes; ticket: one device u32, zero before the
-// first launch (each launch leaves it zero).  lds_bytes = small_lds_bytes().
+// first launch (each launch leaves it zero).
 constexpr uint32_t kSmallMaxN = 1024;
-constexpr uint32_t kSmallMaxLds = 160 * 1024;  // gfx950 LDS per workgroup
-uint32_t small_lds_bytes(uint64_t n, uint64_t total_nodes, uint64_t img_bytes);
-hipError_t launch_small_tree(const uint8_t* in, uint32_t n, uint8_t* out, uint32_t img_at, uint32_t lds_bytes,
-                             uint8_t* scratch, unsigned int* ticket, hipStream_t s);
+hipError_t launch_small_tree(const uint8_t* in, uint32_t n, uint8_t* out, uint32_t img_at, uint8_t* scratch,
+                             unsigned int* ticket, hipStream_t s);
 // Clock probe of the leaf kernels on the current device (NKV_TIMING_CLOCK):
 // p = kClockWords u64 (8 slots of 32: shader-clock cycles, 100 MHz ticks, waves;
 // zeroed by the caller) or nullptr to switch it off.

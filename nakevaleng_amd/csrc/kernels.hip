@@ -1938,10 +1938,12 @@ __global__ __launch_bounds__(kBlock) void k_fill(uint8_t* __restrict__ buf, uint
 // last workgroup to finish (a ticket) takes every leaf digest, builds all levels
 // (merkletree.go:31-64) and the Serialize image (merkletree.go:67-92,
 // merklenode.go:37-63) in LDS, and stores nodes (level-major, 20 B each) at out
-// and the image at out + img_at with 16-byte stores.  Dynamic LDS:
-// small_lds_bytes(n).
+// and the image at out + img_at with 16-byte stores.  LDS: every node (at most
+// 2 x 1024 - 1) plus one 16 KiB image segment, under the 64 KiB a workgroup
+// gets without opting in.
 
 constexpr uint32_t kSmallBlock = 256;
+constexpr uint32_t kSmallSeg = 16384;  // image bytes built in LDS per pass
 
 // SHA-1 of p[0, len), p 16-byte aligned, one block of register lookahead
 __device__ __forceinline__ void sha1_value_aligned(const uint8_t* p, uint64_t len, uint32_t h[5]) {
@@ -1976,11 +1978,14 @@ __device__ __forceinline__ void small_copy_out(const uint8_t* src, uint8_t* dst,
     for (uint32_t b = whole + threadIdx.x; b < bytes; b += kSmallBlock) dst[b] = src[b];
 }
 
+__device__ __forceinline__ uint32_t small_count(uint32_t n, int L) { return L == 0 ? n : ((n - 1) >> L) + 1; }
+
 __global__ __launch_bounds__(kSmallBlock) void k_small_tree(const uint8_t* __restrict__ in, uint32_t n,
                                                             uint8_t* __restrict__ out, uint32_t img_at,
                                                             uint8_t* __restrict__ scratch,
                                                             unsigned int* __restrict__ ticket) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
+    __shared__ __attribute__((aligned(16))) uint8_t sm[20 * (2 * kSmallMaxN - 1) + 12];  // every node
+    __shared__ __attribute__((aligned(16))) uint8_t seg[kSmallSeg];                    // one image segment
     __shared__ uint32_t is_last;
     const uint32_t tid = threadIdx.x;
     const uint32_t i = blockIdx.x * kSmallBlock + tid;
@@ -2026,55 +2031,55 @@ __global__ __launch_bounds__(kSmallBlock) void k_small_tree(const uint8_t* __res
         ++lv;
     } while (cnt > 1);
     const uint32_t total = base + 1;
-    // the image, top level first: 0x00 + digest per node, one 0x01 after each
-    // odd level below the top (merklenode.go:37-63, MERKLE_NODE_EMPTY :11)
-    uint8_t* img = sm + ((20u * total + 15u) & ~15u);
-    uint32_t p = 0;
-    for (int L = lv - 1; L >= 0; --L) {
-        const uint32_t c = L == 0 ? n : ((n - 1) >> L) + 1;
-        uint32_t s = 0;
-        for (int j = 0; j < L; ++j) s += j == 0 ? n : ((n - 1) >> j) + 1;
-        for (uint32_t k = tid; k < c; k += kSmallBlock) {
-            uint8_t* o = img + p + 21u * k;
-            const uint8_t* d = sm + 20u * (s + k);
-            o[0] = 0u;
-#pragma unroll
-            for (int b = 0; b < 20; ++b) o[1 + b] = d[b];
-        }
-        p += 21u * c;
-        if (L < lv - 1 && (c & 1u)) {
-            if (tid == 0) img[p] = NKV_MERKLE_NODE_EMPTY;
-            ++p;
-        }
-    }
-    __syncthreads();
     small_copy_out(sm, out, 20u * total);
-    small_copy_out(img, out + img_at, p);
+    // the image, top level first: 0x00 + digest per node, one 0x01 after each
+    // odd level below the top (merklenode.go:37-63, MERKLE_NODE_EMPTY :11),
+    // built kSmallSeg bytes at a time in LDS from whole node records clipped to
+    // the segment (as k_bfs_image does)
+    uint32_t img_len = 0;
+    for (int L = lv - 1; L >= 0; --L) {
+        const uint32_t c = small_count(n, L);
+        img_len += 21u * c + ((L < lv - 1 && (c & 1u)) ? 1u : 0u);
+    }
+    for (uint32_t s0 = 0; s0 < img_len; s0 += kSmallSeg) {
+        const uint32_t s1 = min(s0 + kSmallSeg, img_len);
+        uint32_t A = 0;  // image offset of level L's first record
+        for (int L = lv - 1; L >= 0; --L) {
+            const uint32_t c = small_count(n, L);
+            uint32_t ns = 0;  // node index of level L's first node
+            for (int j = 0; j < L; ++j) ns += small_count(n, j);
+            const uint32_t E = A + 21u * c;
+            const bool pad = L < lv - 1 && (c & 1u);
+            if (pad && E >= s0 && E < s1 && tid == 0) seg[E - s0] = NKV_MERKLE_NODE_EMPTY;
+            if (E > s0 && A < s1) {
+                const uint32_t k0 = s0 > A ? (s0 - A) / 21u : 0u;
+                const uint32_t k1 = (min(s1, E) - 1u - A) / 21u;  // last record with a byte in the segment
+                for (uint32_t k = k0 + tid; k <= k1; k += kSmallBlock) {
+                    const uint8_t* d = sm + 20u * (ns + k);
+                    const int32_t pos = int32_t(A + 21u * k) - int32_t(s0);
+#pragma unroll
+                    for (int b = 0; b < 21; ++b) {
+                        const int32_t q = pos + b;
+                        if (q >= 0 && q < int32_t(kSmallSeg)) seg[q] = b == 0 ? 0u : d[b - 1];
+                    }
+                }
+            }
+            A = E + (pad ? 1u : 0u);
+        }
+        __syncthreads();
+        small_copy_out(seg, out + img_at + s0, s1 - s0);
+        __syncthreads();
+    }
 }
 
 // ---------------------------------------------------------------------------
 // host-side launchers
 
-uint32_t small_lds_bytes(uint64_t n, uint64_t total_nodes, uint64_t img_bytes) {
-    (void)n;
-    return uint32_t(((20 * total_nodes + 15) & ~uint64_t(15)) + ((img_bytes + 15) & ~uint64_t(15)));
-}
-
-hipError_t launch_small_tree(const uint8_t* in, uint32_t n, uint8_t* out, uint32_t img_at, uint32_t lds_bytes,
-                             uint8_t* scratch, unsigned int* ticket, hipStream_t s) {
-    if (n == 0 || n > kSmallMaxN || lds_bytes > kSmallMaxLds) return hipErrorInvalidValue;
-    static thread_local int attr_device = -1;  // the attribute is per device
-    int dev = -1;
-    hipError_t e = hipGetDevice(&dev);
-    if (e != hipSuccess) return e;
-    if (attr_device != dev) {
-        e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_small_tree),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, int(kSmallMaxLds));
-        if (e != hipSuccess) return e;
-        attr_device = dev;
-    }
+hipError_t launch_small_tree(const uint8_t* in, uint32_t n, uint8_t* out, uint32_t img_at, uint8_t* scratch,
+                             unsigned int* ticket, hipStream_t s) {
+    if (n == 0 || n > kSmallMaxN || (img_at & 15u)) return hipErrorInvalidValue;
     const unsigned grid = unsigned((n + kSmallBlock - 1) / kSmallBlock);
-    hipLaunchKernelGGL(k_small_tree, dim3(grid), dim3(kSmallBlock), lds_bytes, s, in, n, out, img_at, scratch, ticket);
+    hipLaunchKernelGGL(k_small_tree, dim3(grid), dim3(kSmallBlock), 0, s, in, n, out, img_at, scratch, ticket);
     return hipGetLastError();
 }
 
