@@ -163,6 +163,9 @@ int nkv_ctx_sync(nkv_ctx *ctx);
 #define NKV_OPT_SMALL_MAX_N 15     /* 0..1024 (default 1024) */
 #define NKV_OPT_SMALL_MAX_BYTES 16 /* payload bound of the small path (default 1 MiB; the values
                                       16-byte aligned; for records the whole stream) */
+#define NKV_OPT_ARENA_COHERENT 17   /* nkv_host_alloc blocks: 1 (default) = host-coherent pinned memory
+                                       (copies read it as any pinned block, and the small path's kernel
+                                       reads NewLeaf values in place); 0 = default pinned memory */
 int nkv_ctx_set_option(nkv_ctx *ctx, int key, int64_t value);
 /* Which path the latest host-buffer tree call of the context took */
 #define NKV_PATH_GRID 0  /* copies + leaf kernel + per-level reduce launches */

@@ -34,6 +34,7 @@
 #include <condition_variable>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <exception>
@@ -315,7 +316,12 @@ class Session {
     Session& operator=(const Session&) = delete;
 
     nkv_ctx* ctx() {
-        std::call_once(ctx_once_, [this] { check(nkv_ctx_create(device_, &ctx_), "nkv_ctx_create"); });
+        std::call_once(ctx_once_, [this] {
+            check(nkv_ctx_create(device_, &ctx_), "nkv_ctx_create");
+            // NKV_ARENA_COHERENT=0: the arena in default pinned memory (A/B runs)
+            if (const char* e = std::getenv("NKV_ARENA_COHERENT"))
+                check(nkv_ctx_set_option(ctx_, NKV_OPT_ARENA_COHERENT, std::atoi(e) ? 1 : 0), "NKV_ARENA_COHERENT");
+        });
         return ctx_;
     }
 
@@ -435,6 +441,8 @@ class Session {
     // it to a pool thread and waiting for it costs two thread wake-ups, more
     // than the copy (the reference's default flush is ~2 KB).
     static constexpr uint64_t kInlineJob = uint64_t(256) << 10;
+    // A larger last job (a flush under kJobBytes, e.g. 1 Ki x 1 KiB) goes to the
+    // pool in pieces of about kInlineJob, one per copy thread.
     void Settle() {
         if (!pool_) return;
         if (job_ && job_bytes_ <= kInlineJob) {
@@ -442,6 +450,31 @@ class Session {
             for (const CopyPool::Task& t : job_->tasks) copy(job_->base + t.at, t.src, t.n);
             pool_->Recycle(std::move(job_));
             job_.reset();
+            job_bytes_ = 0;
+        } else if (job_ && pool_->threads() > 1) {
+            const uint64_t parts = std::min<uint64_t>(uint64_t(pool_->threads()), job_bytes_ / kInlineJob + 1);
+            const uint64_t per = job_bytes_ / parts + 1;
+            std::unique_ptr<CopyPool::Job> big = std::move(job_);
+            std::unique_ptr<CopyPool::Job> piece;
+            uint64_t bytes = 0;
+            for (const CopyPool::Task& t : big->tasks) {
+                if (!piece) {
+                    piece = pool_->Fresh();
+                    piece->base = big->base;
+                }
+                piece->tasks.push_back(t);
+                piece->end = t.at + t.n;  // tasks are in arena order
+                bytes += t.n;
+                if (bytes >= per) {
+                    pool_->Submit(std::move(piece));
+                    bytes = 0;
+                }
+            }
+            if (piece) {
+                piece->end = used_;
+                pool_->Submit(std::move(piece));
+            }
+            pool_->Recycle(std::move(big));
             job_bytes_ = 0;
         } else {
             SubmitJob();

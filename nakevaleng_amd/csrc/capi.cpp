@@ -238,41 +238,82 @@ int small_tree(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint6
     const uint64_t tot = total_of(n);
     const uint64_t img_len = layout_of(counts_of(n)).total;
     const uint64_t img_at = align16(20 * tot);
-    const uint64_t in_bytes = 16 * n + vbytes, out_bytes = img_at + align16(img_len);
-    uint64_t lo = 0, hi = 0;  // a call over a pinned block ends its batch (nkv_host_stream)
-    if (nkv_ctx::Pinned* blk = pinned_extent(c, base, off, len, n, &lo, &hi)) blk->streamed = 0;
+    const uint64_t out_bytes = img_at + align16(img_len);
+    uint64_t lo = 0, hi = 0;
+    nkv_ctx::Pinned* blk = pinned_extent(c, base, off, len, n, &lo, &hi);
+    if (blk) blk->streamed = 0;  // a call over a pinned block ends its batch (nkv_host_stream)
+    // values in a host-coherent arena block at 16-byte aligned places (the
+    // mirrors' NewLeaf arena) are read where they lie: no pack, no copy
+    bool in_place = blk && blk->coherent && c->small_path == 1 && (lo & 15) == 0;
+    const uint64_t adj = blk ? uint64_t(base - blk->p) : 0;
+    for (uint64_t i = 0; in_place && i < n; ++i) in_place = ((adj + off[i]) & 15) == 0;
+    const uint64_t vext = in_place ? align16(hi) - lo : vbytes;  // the values' extent
+    const uint64_t in_bytes = 16 * n + (in_place ? 0 : vbytes);
     TRY(grow_coherent(&c->h_sin, &c->h_sin_cap, in_bytes));
-    TRY(grow_coherent(&c->h_sout, &c->h_sout_cap, out_bytes));
+    TRY(grow_coherent(&c->h_sout, &c->h_sout_cap, out_bytes + 64));  // + the completion word
     const size_t small_cap = c->d_small.cap;
     TRY(grow(c->d_small, 64 + 20 * kSmallMaxN));
     if (c->d_small.cap != small_cap) HIPTRY(hipMemsetAsync(c->d_small.p, 0, 64, c->stream));  // the ticket
     uint64_t* desc = reinterpret_cast<uint64_t*>(c->h_sin);
-    uint8_t* vals = c->h_sin + 16 * n;
-    uint64_t p = 0;
-    for (uint64_t i = 0; i < n; ++i) {
-        desc[2 * i] = p;
-        desc[2 * i + 1] = len[i];
-        if (len[i]) memcpy(vals + p, base + off[i], len[i]);
-        p += align16(len[i]);
+    if (in_place) {
+        for (uint64_t i = 0; i < n; ++i) {
+            desc[2 * i] = adj + off[i] - lo;
+            desc[2 * i + 1] = len[i];
+        }
+    } else {
+        uint8_t* vals = c->h_sin + 16 * n;
+        uint64_t p = 0;
+        for (uint64_t i = 0; i < n; ++i) {
+            desc[2 * i] = p;
+            desc[2 * i + 1] = len[i];
+            if (len[i]) memcpy(vals + p, base + off[i], len[i]);
+            p += align16(len[i]);
+        }
     }
     uint8_t* scratch = static_cast<uint8_t*>(c->d_small.p) + 64;
     unsigned int* ticket = static_cast<unsigned int*>(c->d_small.p);
+    volatile unsigned int* hdone = reinterpret_cast<volatile unsigned int*>(c->h_sout + out_bytes);
+    uint32_t seq = ++c->small_seq;
+    if (seq == 0) seq = c->small_seq = 1;  // 0 is the word's cleared state
+    *hdone = 0;
     if (c->small_path == 2) {  // through HBM: one copy in, one launch, one copy out
         TRY(grow(c->d_sin, in_bytes));
         TRY(grow(c->d_sout, out_bytes));
         HIPTRY(hipMemcpyAsync(c->d_sin.p, c->h_sin, in_bytes, hipMemcpyHostToDevice, c->stream));
-        HIPTRY(launch_small_tree(static_cast<const uint8_t*>(c->d_sin.p), uint32_t(n),
-                                 static_cast<uint8_t*>(c->d_sout.p), uint32_t(img_at), scratch, ticket,
-                                 c->stream));
+        const uint64_t* d_desc = static_cast<const uint64_t*>(c->d_sin.p);
+        HIPTRY(launch_small_tree(d_desc, reinterpret_cast<const uint8_t*>(d_desc + 2 * n), uint32_t(vext),
+                                 uint32_t(n), static_cast<uint8_t*>(c->d_sout.p), uint32_t(img_at), scratch, ticket,
+                                 nullptr, 0, c->stream));
         HIPTRY(hipMemcpyAsync(c->h_sout, c->d_sout.p, out_bytes, hipMemcpyDeviceToHost, c->stream));
+        HIPTRY(hipStreamSynchronize(c->stream));
     } else {  // the kernel reads the values and writes its results across PCIe
-        void *din = nullptr, *dout = nullptr;
+        void *din = nullptr, *dout = nullptr, *dblk = nullptr;
         HIPTRY(hipHostGetDevicePointer(&din, c->h_sin, 0));
         HIPTRY(hipHostGetDevicePointer(&dout, c->h_sout, 0));
-        HIPTRY(launch_small_tree(static_cast<const uint8_t*>(din), uint32_t(n), static_cast<uint8_t*>(dout),
-                                 uint32_t(img_at), scratch, ticket, c->stream));
+        if (in_place) HIPTRY(hipHostGetDevicePointer(&dblk, blk->p, 0));
+        const uint64_t* d_desc = static_cast<const uint64_t*>(din);
+        const uint8_t* d_vals = in_place ? static_cast<const uint8_t*>(dblk) + lo
+                                         : reinterpret_cast<const uint8_t*>(d_desc + 2 * n);
+        HIPTRY(launch_small_tree(d_desc, d_vals, uint32_t(vext), uint32_t(n), static_cast<uint8_t*>(dout),
+                                 uint32_t(img_at), scratch, ticket,
+                                 reinterpret_cast<unsigned int*>(static_cast<uint8_t*>(dout) + out_bytes), seq,
+                                 c->stream));
+        // the kernel's last store is seq into the completion word, after every
+        // output byte: spin on it (a few us sooner than the runtime's
+        // completion wait); every 256 polls ask the stream whether it failed
+        for (uint32_t k = 1;; ++k) {
+            if (__atomic_load_n(hdone, __ATOMIC_ACQUIRE) == seq) break;
+            if ((k & 255u) == 0u) {
+                const hipError_t q = hipStreamQuery(c->stream);
+                if (q == hipSuccess) {  // finished: the word is there now
+                    if (__atomic_load_n(hdone, __ATOMIC_ACQUIRE) != seq) return NKV_ERR_DEVICE;
+                    break;
+                }
+                if (q != hipErrorNotReady) return st_at(q, "k_small_tree", __FILE__, __LINE__);
+            }
+            __builtin_ia32_pause();
+        }
     }
-    HIPTRY(hipStreamSynchronize(c->stream));
     if (nodes_out) memcpy(nodes_out, c->h_sout, 20 * tot);
     if (root20) memcpy(root20, c->h_sout + 20 * (tot - 1), 20);
     if (img_out) memcpy(img_out, c->h_sout + img_at, img_len);
@@ -657,6 +698,10 @@ int nkv_ctx_set_option(nkv_ctx* c, int key, int64_t value) try {
             if (value < 0 || value > int64_t(kSmallMaxN)) return NKV_ERR_INVALID;
             c->small_max_n = uint64_t(value);
             return NKV_OK;
+        case NKV_OPT_ARENA_COHERENT:
+            if (value < 0 || value > 1) return NKV_ERR_INVALID;
+            c->arena_coherent = int(value);
+            return NKV_OK;
         case NKV_OPT_SMALL_MAX_BYTES:
             if (value < 0 || value > (int64_t(1) << 30)) return NKV_ERR_INVALID;
             c->small_max_bytes = uint64_t(value);
@@ -799,11 +844,16 @@ int nkv_host_alloc(nkv_ctx* c, uint64_t bytes, void** out) try {
     *out = nullptr;
     TRY(bind(c));
     void* p = nullptr;
-    if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) {
+    // host-coherent by default (NKV_OPT_ARENA_COHERENT): DMA reads it as any
+    // pinned block, and the small-tree kernel may read it in place (uncached on
+    // the GPU side, so a block rewritten flush after flush is never stale there)
+    const unsigned flags = c->arena_coherent ? hipHostMallocCoherent : hipHostMallocDefault;
+    if (hipHostMalloc(&p, bytes ? bytes : 1, flags) != hipSuccess) {
         (void)hipGetLastError();
         return NKV_ERR_NOMEM;
     }
-    nkv_ctx::Pinned* blk = new (std::nothrow) nkv_ctx::Pinned{static_cast<uint8_t*>(p), bytes ? bytes : 1, 0, {}};
+    nkv_ctx::Pinned* blk = new (std::nothrow)
+        nkv_ctx::Pinned{static_cast<uint8_t*>(p), bytes ? bytes : 1, 0, {}, c->arena_coherent != 0};
     if (!blk) {
         (void)hipHostFree(p);
         return NKV_ERR_NOMEM;

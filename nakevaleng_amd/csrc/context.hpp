@@ -185,12 +185,14 @@ struct nkv_ctx {
         uint64_t bytes;
         uint64_t streamed;  // bytes [0, streamed) already queued to d_arena
         nkv::DevBuf d_arena;  // device mirror of the block
+        bool coherent;        // host-coherent (the small-tree kernel may read it in place)
     };
     std::vector<Pinned*> pinned;
     // the one-launch small-tree path of the host-buffer calls (NKV_OPT_SMALL_*):
     // host-coherent pinned in / out buffers the kernel reads and writes across
     // PCIe (or device copies of them, small_path 2), and its device scratch
     // (the ticket word + 20 n leaf digests)
+    int arena_coherent = 1;  // NKV_OPT_ARENA_COHERENT: nkv_host_alloc blocks host-coherent
     int small_path = 1;
     uint64_t small_max_n = 1024;
     uint64_t small_max_bytes = uint64_t(1) << 20;
@@ -199,6 +201,7 @@ struct nkv_ctx {
     size_t h_sin_cap = 0, h_sout_cap = 0;
     nkv::DevBuf d_sin, d_sout, d_small;
     int last_path = 0;  // NKV_PATH_* of the latest host-buffer tree call
+    uint32_t small_seq = 0;  // the small-tree kernel's completion word (per call)
 };
 
 namespace nkv {

@@ -162,14 +162,17 @@ hipError_t launch_bloom_staged(int mode, const uint8_t* base, const uint64_t* of
                                uint64_t stream_len, uint64_t n, uint32_t m, uint32_t k, uint32_t seed0,
                                uint32_t* bits, unsigned int* err, uint32_t* scratch, hipStream_t s);
 hipError_t launch_fill(uint8_t* buf, uint64_t nbytes, uint64_t seed, hipStream_t s);
-// One-launch small tree (kernels.hip k_small_tree): in = n (offset, length) u64
-// pairs then the values at in + 16 n + offset (16-byte aligned); out receives
+// One-launch small tree (kernels.hip k_small_tree): desc = n (offset, length)
+// u64 pairs, value i at vals + offset (16-byte aligned); out receives
 // the nodes (level-major) and, at out + img_at (16-byte aligned), the Serialize
 // image.  scratch: 20 n device bytes; ticket: one device u32, zero before the
 // first launch (each launch leaves it zero).
 constexpr uint32_t kSmallMaxN = 1024;
-hipError_t launch_small_tree(const uint8_t* in, uint32_t n, uint8_t* out, uint32_t img_at, uint8_t* scratch,
-                             unsigned int* ticket, hipStream_t s);
+// vbytes: the values lie in vals[0, vbytes).  done (nullable, host-coherent
+// memory): receives seq once every output byte is written.
+hipError_t launch_small_tree(const uint64_t* desc, const uint8_t* vals, uint32_t vbytes, uint32_t n, uint8_t* out,
+                             uint32_t img_at, uint8_t* scratch, unsigned int* ticket, unsigned int* done, uint32_t seq,
+                             hipStream_t s);
 // Clock probe of the leaf kernels on the current device (NKV_TIMING_CLOCK):
 // p = kClockWords u64 (8 slots of 32: shader-clock cycles, 100 MHz ticks, waves;
 // zeroed by the caller) or nullptr to switch it off.

@@ -1929,10 +1929,11 @@ __global__ __launch_bounds__(kBlock) void k_fill(uint8_t* __restrict__ buf, uint
 // :39: a compaction of lsm_run_max = 4 such runs), where a launch per level
 // and copies per buffer would cost more than the hashing.
 //
-// Input `in` (16-byte aligned): n (offset, length) u64 pairs, then the values
-// at in + 16 n + offset (16-byte aligned offsets).  The host packs it into
-// host-coherent pinned memory that the kernel reads across PCIe (no DMA), or
-// copies it to HBM first (NKV_OPT_SMALL_PATH).  One lane per leaf and one
+// Input: n (offset, length) u64 pairs at desc and the values at vals + offset
+// (16-byte aligned).  The host packs both into host-coherent pinned memory that
+// the kernel reads across PCIe (no DMA), or copies them to HBM first
+// (NKV_OPT_SMALL_PATH); values already in a host-coherent pinned arena block
+// (the deferred-NewLeaf arena, nkv_host_alloc) are read where they lie.  One lane per leaf and one
 // 256-lane workgroup per 256 leaves, so each wave runs alone on its SIMD (a
 // leaf's SHA-1 is a serial chain: DESIGN.md section 4, lone-wave cadence); the
 // last workgroup to finish (a ticket) takes every leaf digest, builds all levels
@@ -1980,18 +1981,54 @@ __device__ __forceinline__ void small_copy_out(const uint8_t* src, uint8_t* dst,
 
 __device__ __forceinline__ uint32_t small_count(uint32_t n, int L) { return L == 0 ? n : ((n - 1) >> L) + 1; }
 
-__global__ __launch_bounds__(kSmallBlock) void k_small_tree(const uint8_t* __restrict__ in, uint32_t n,
-                                                            uint8_t* __restrict__ out, uint32_t img_at,
+// bytes [0, bytes) of src (16-byte aligned, host or device memory) into LDS
+// dst: every thread's loads are issued before any store, so an input of up to
+// 16 KiB crosses PCIe in one round trip
+__device__ __forceinline__ void small_stage_in(const uint8_t* src, uint8_t* dst, uint32_t bytes) {
+    const uint4* s4 = reinterpret_cast<const uint4*>(src);
+    uint4* d4 = reinterpret_cast<uint4*>(dst);
+    const uint32_t nq = (bytes + 15u) >> 4;
+    for (uint32_t c0 = 0; c0 < nq; c0 += 4 * kSmallBlock) {
+        uint4 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t c = c0 + threadIdx.x + k * kSmallBlock;
+            v[k] = c < nq ? s4[c] : make_uint4(0u, 0u, 0u, 0u);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t c = c0 + threadIdx.x + k * kSmallBlock;
+            if (c < nq) d4[c] = v[k];
+        }
+    }
+}
+
+// vbytes: the extent of vals the values lie in.  A one-workgroup launch whose
+// descriptors and values fit kSmallSeg bytes stages both into LDS first (one
+// PCIe round trip for the whole input instead of one per block of each lane).
+// done (nullable, host-coherent): receives seq once every output byte is
+// written, so the host can spin on it instead of waiting for the runtime's
+// completion signal.
+__global__ __launch_bounds__(kSmallBlock) void k_small_tree(const uint64_t* __restrict__ desc,
+                                                            const uint8_t* __restrict__ vals, uint32_t vbytes,
+                                                            uint32_t n, uint8_t* __restrict__ out, uint32_t img_at,
                                                             uint8_t* __restrict__ scratch,
-                                                            unsigned int* __restrict__ ticket) {
+                                                            unsigned int* __restrict__ ticket,
+                                                            unsigned int* __restrict__ done, uint32_t seq) {
     __shared__ __attribute__((aligned(16))) uint8_t sm[20 * (2 * kSmallMaxN - 1) + 12];  // every node
-    __shared__ __attribute__((aligned(16))) uint8_t seg[kSmallSeg];                    // one image segment
+    __shared__ __attribute__((aligned(16))) uint8_t seg[kSmallSeg];  // the staged input, then image segments
     __shared__ uint32_t is_last;
     const uint32_t tid = threadIdx.x;
     const uint32_t i = blockIdx.x * kSmallBlock + tid;
-    const uint64_t* desc = reinterpret_cast<const uint64_t*>(in);
+    if (gridDim.x == 1 && 16u * n + vbytes <= kSmallSeg) {
+        small_stage_in(reinterpret_cast<const uint8_t*>(desc), seg, 16u * n);
+        small_stage_in(vals, seg + 16u * n, vbytes);
+        __syncthreads();
+        desc = reinterpret_cast<const uint64_t*>(seg);
+        vals = seg + 16u * n;
+    }
     uint32_t h[5] = {0u, 0u, 0u, 0u, 0u};
-    if (i < n) sha1_value_aligned(in + 16ull * n + desc[2 * i], desc[2 * i + 1], h);  // NewLeaf, merklenode.go:27-34
+    if (i < n) sha1_value_aligned(vals + desc[2 * i], desc[2 * i + 1], h);  // NewLeaf, merklenode.go:27-34
     if (gridDim.x > 1) {
         if (i < n) store_digest(scratch, i, h);
         __threadfence();
@@ -2041,6 +2078,7 @@ __global__ __launch_bounds__(kSmallBlock) void k_small_tree(const uint8_t* __res
         const uint32_t c = small_count(n, L);
         img_len += 21u * c + ((L < lv - 1 && (c & 1u)) ? 1u : 0u);
     }
+    __syncthreads();  // seg may still hold the staged input
     for (uint32_t s0 = 0; s0 < img_len; s0 += kSmallSeg) {
         const uint32_t s1 = min(s0 + kSmallSeg, img_len);
         uint32_t A = 0;  // image offset of level L's first record
@@ -2070,16 +2108,25 @@ __global__ __launch_bounds__(kSmallBlock) void k_small_tree(const uint8_t* __res
         small_copy_out(seg, out + img_at + s0, s1 - s0);
         __syncthreads();
     }
+    if (done) {
+        __threadfence_system();  // each wave's output stores complete at system scope
+        __syncthreads();
+        if (tid == 0) __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 // ---------------------------------------------------------------------------
 // host-side launchers
 
-hipError_t launch_small_tree(const uint8_t* in, uint32_t n, uint8_t* out, uint32_t img_at, uint8_t* scratch,
-                             unsigned int* ticket, hipStream_t s) {
-    if (n == 0 || n > kSmallMaxN || (img_at & 15u)) return hipErrorInvalidValue;
+hipError_t launch_small_tree(const uint64_t* desc, const uint8_t* vals, uint32_t vbytes, uint32_t n, uint8_t* out,
+                             uint32_t img_at, uint8_t* scratch, unsigned int* ticket, unsigned int* done, uint32_t seq,
+                             hipStream_t s) {
+    if (n == 0 || n > kSmallMaxN || (img_at & 15u) || (reinterpret_cast<uintptr_t>(vals) & 15u) ||
+        (reinterpret_cast<uintptr_t>(desc) & 15u))
+        return hipErrorInvalidValue;
     const unsigned grid = unsigned((n + kSmallBlock - 1) / kSmallBlock);
-    hipLaunchKernelGGL(k_small_tree, dim3(grid), dim3(kSmallBlock), 0, s, in, n, out, img_at, scratch, ticket);
+    hipLaunchKernelGGL(k_small_tree, dim3(grid), dim3(kSmallBlock), 0, s, desc, vals, vbytes, n, out, img_at, scratch,
+                       ticket, done, seq);
     return hipGetLastError();
 }
 

@@ -215,3 +215,42 @@ def test_small_flush_tool_roots(oracle, tmp_path):
             want = oracle.tree_from_digests(oracle.leaf_hashes(data, off, ln))[-1].tobytes().hex()
             assert line["root"] == want, (mode, name)
             assert line["path"] == (0 if mode == 0 else 1), (mode, name)
+
+
+@pytest.mark.parametrize("coherent", [1, 0])
+def test_small_path_reads_the_arena_in_place(small_ctx, oracle, coherent):
+    """Values inside an nkv_host_alloc block (the mirrors' NewLeaf arena) at
+    16-byte aligned places: with a host-coherent block (NKV_OPT_ARENA_COHERENT
+    1, the default) the one-launch kernel reads them where they lie; with a
+    default pinned block, or any unaligned place, they are packed first.  Either
+    way bit-exact, and a block rewritten between calls is read afresh."""
+    _lib, ctx = small_ctx
+    L = _lib.lib()
+    ctx.set_option(_lib.NKV_OPT_ARENA_COHERENT, coherent)
+    cap = 1 << 20
+    p = ctypes.c_void_p()
+    _lib.check(L.nkv_host_alloc(ctx.h, cap, ctypes.byref(p)))
+    try:
+        arena = np.ctypeslib.as_array((ctypes.c_uint8 * cap).from_address(p.value))
+        for rnd, (n, pad) in enumerate([(10, 16), (40, 16), (300, 16), (1024, 16), (77, 1), (10, 16), (10, 16)]):
+            rng = np.random.default_rng(rnd)
+            ln = np.array([EDGE[(i + rnd) % len(EDGE)] for i in range(n)], np.uint64)
+            ln = np.minimum(ln, 600).astype(np.uint64)
+            off = np.zeros(n, np.uint64)
+            pos = 16 * rnd  # the batch does not start at the block's first byte
+            for i in range(n):
+                off[i] = pos
+                pos += int(ln[i])
+                pos = (pos + pad - 1) // pad * pad
+            arena[:pos] = np.frombuffer(rng.bytes(pos), np.uint8)  # rewritten every round
+            nodes_w, img_w = _want(oracle, arena[:pos].copy(), off, ln)
+            root = np.zeros(20, np.uint8)
+            nodes = np.zeros((L.nkv_total_nodes(n), 20), np.uint8)
+            img = np.zeros(L.nkv_bfs_size(n), np.uint8)
+            _lib.check(L.nkv_tree_from_values(ctx.h, ctypes.cast(p, _lib._u8p), _lib.p64(off), _lib.p64(ln), n,
+                                              _lib.p8(root), _lib.p8(nodes), _lib.p8(img)))
+            assert ctx.last_path() == _lib.NKV_PATH_SMALL
+            assert np.array_equal(nodes, nodes_w) and img.tobytes() == img_w, (coherent, rnd)
+    finally:
+        _lib.check(L.nkv_host_free(ctx.h, p))
+        ctx.set_option(_lib.NKV_OPT_ARENA_COHERENT, 1)
