@@ -202,3 +202,45 @@ def test_bloom_insert_then_query(oracle):
     qoff = np.arange(1000, dtype=np.uint64) * 64
     fp = oracle.bloom_query(other, qoff, np.full(1000, 64, np.uint64), m, k, 12345, bits).mean()
     assert fp < 0.05
+
+
+def test_openssl_variant_kats_and_trees(oracle):
+    """The CPU baseline's OpenSSL variant (oracle/merkle_openssl.c): FIPS 180-4
+    known answers, and the same leaves and trees as the portable restatement on
+    ragged values, one thread and several (wide levels split over threads)."""
+    kats = {b"": "da39a3ee5e6b4b0d3255bfef95601890afd80709",
+            b"abc": "a9993e364706816aba3e25717850c26c9cd0d89d",
+            b"abcdbcdecdefdefgefghfghighijhijkijkljklmklmnlmnomnopnopq": "84983e441c3bd26ebaae4aa1f95129e5e54670f1"}
+    for m, want in kats.items():
+        assert oracle.ossl_sha1(m).hex() == want
+    assert oracle.ossl_sha1(b"a" * 1000000).hex() == "34aa973cd4c4daa4f61eeb2bdbad27316534016f"
+    rng = np.random.default_rng(17)
+    for n in (1, 2, 3, 7, 1000, 9001):
+        ln = rng.integers(0, 300, n).astype(np.uint64)
+        off = np.zeros(n, np.uint64)
+        off[1:] = np.cumsum(ln[:-1])
+        base = np.frombuffer(rng.bytes(int(ln.sum()) + 1), np.uint8).copy()
+        want = oracle.tree_from_digests(oracle.leaf_hashes(base, off, ln))
+        for t in (1, 4):
+            got = oracle.ossl_tree_from_digests(oracle.ossl_leaf_hashes(base, off, ln, threads=t), threads=t)
+            assert np.array_equal(got, want), (n, t)
+            assert np.array_equal(oracle.tree_from_digests(oracle.leaf_hashes(base, off, ln, threads=t), threads=t),
+                                  want)
+    data = oracle.splitmix64_bytes(5000 * 64, 3)
+    assert np.array_equal(oracle.ossl_leaf_hashes_strided(data, 64, 64, 5000, threads=3),
+                          oracle.leaf_hashes_strided(data, 64, 64, 5000))
+
+
+def test_flush_reps_matches_the_tree(oracle):
+    """nkvo_flush_reps (small_flush's one-core CPU column) builds the same root
+    with either SHA-1."""
+    rng = np.random.default_rng(5)
+    for n in (1, 10, 40, 1025):
+        ln = rng.integers(1, 200, n).astype(np.uint64)
+        off = np.zeros(n, np.uint64)
+        off[1:] = np.cumsum(ln[:-1])
+        base = np.frombuffer(rng.bytes(int(ln.sum()) + 1), np.uint8).copy()
+        want = oracle.tree_from_digests(oracle.leaf_hashes(base, off, ln))[-1].tobytes().hex()
+        for ossl in (False, True):
+            us, root = oracle.flush_us(base, off, ln, 3, openssl=ossl)
+            assert root == want and us > 0
