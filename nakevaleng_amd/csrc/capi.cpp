@@ -417,7 +417,10 @@ int plan_of(nkv_ctx* c, const uint64_t* len, const uint64_t* host_len, uint64_t 
     unsigned int* d = static_cast<unsigned int*>(c->d_range.p);
     uint32_t* part = nullptr;
     TRY(locate_parts(c, n, &part));
-    HIPTRY(launch_len_range(len, n, d, part, c->stream));
+    const size_t tcap = c->d_ticket.cap;
+    TRY(grow(c->d_ticket, 16));
+    if (c->d_ticket.cap != tcap) HIPTRY(hipMemsetAsync(c->d_ticket.p, 0, 16, c->stream));
+    HIPTRY(launch_len_range(len, n, d, part, static_cast<unsigned int*>(c->d_ticket.p), c->stream));
     gate->range = d;
     *plan = kGated;
     return NKV_OK;
@@ -597,7 +600,7 @@ void nkv_ctx_destroy(nkv_ctx* c) {
     for (DevBuf* b : {&c->d_data, &c->d_off, &c->d_len, &c->d_nodes, &c->d_img, &c->d_tmp,
                       &c->d_err, &c->d_aux, &c->d_keys, &c->d_perm, &c->d_stmp, &c->d_queue, &c->d_stats,
                       &c->d_range, &c->d_part, &c->d_tmp2, &c->d_flags, &c->d_clk, &c->d_sin, &c->d_sout,
-                      &c->d_small})
+                      &c->d_small, &c->d_ticket})
         if (b->p) (void)hipFree(b->p);
     for (nkv_ctx::Pinned* blk : c->pinned) {
         if (blk->d_arena.p) (void)hipFree(blk->d_arena.p);

@@ -160,7 +160,8 @@ struct nkv_ctx {
     hipEvent_t host_ev[2] = {nullptr, nullptr};  // host-buffer call: before the upload, after the download
     bool host_timed = false;
     nkv::DevBuf d_data, d_off, d_len, d_nodes, d_img, d_tmp, d_err, d_aux, d_keys, d_perm, d_stmp, d_queue,
-        d_stats, d_range, d_part, d_tmp2, d_flags, d_clk;
+        d_stats, d_range, d_part, d_tmp2, d_flags, d_clk,
+        d_ticket;  // k_len_range's ticket (zeroed when allocated; each launch leaves it zero)
     int flag_set = 0;  // which of the two pass-flag sets in d_flags the next records call uses
     // the length sort's bucket totals may be non-zero (a sort was cut short):
     // the next sort clears them first (internal.hpp sort_head_words)

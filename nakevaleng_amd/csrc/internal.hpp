@@ -180,6 +180,8 @@ constexpr uint32_t kClockWords = 8 * 32;
 hipError_t set_clock_probe(unsigned long long* p, hipStream_t s);
 // out[0] / out[1] = min / max of len[i] / 64 over the batch (2 u32 on the
 // device); part: scratch of locate_part_words(n) u32
-hipError_t launch_len_range(const uint64_t* len, uint64_t n, unsigned int* out, uint32_t* part, hipStream_t s);
+// ticket: one device u32, zero before the first launch (each launch leaves it zero)
+hipError_t launch_len_range(const uint64_t* len, uint64_t n, unsigned int* out, uint32_t* part, unsigned int* ticket,
+                            hipStream_t s);
 
 }  // namespace nkv

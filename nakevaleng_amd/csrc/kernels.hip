@@ -1861,10 +1861,12 @@ __global__ __launch_bounds__(kBlock, kRecordsWaves) void k_leaf_records(
 // the leaf level choose input order (narrow range: no sort) or the
 // length-sorted work queue, on the device (Gate).
 __global__ __launch_bounds__(kBlock) void k_len_range(const uint64_t* __restrict__ len, uint64_t n,
-                                                       uint32_t* __restrict__ part) {
+                                                       uint32_t* __restrict__ part, unsigned int* __restrict__ out,
+                                                       unsigned int* __restrict__ ticket) {
     // eight values per thread, loads first; one (lo, hi, 0) partial per
-    // workgroup, folded by k_locate_fold (no same-address atomics: a grid
-    // fold over 256 workgroups serialised its atomics for 12.6 us at 453 K values)
+    // workgroup, and the last workgroup to finish (a ticket) folds them into
+    // out (no same-address min/max atomics: a grid fold over 256 workgroups
+    // serialised them for 12.6 us at 453 K values; and no fold launch)
     uint32_t lo = 0xFFFFFFFFu, hi = 0u, none = 0u;
     unsigned long long zero = 0;
     const uint64_t base = uint64_t(blockIdx.x) * (kBlock * 8) + threadIdx.x;
@@ -1883,17 +1885,35 @@ __global__ __launch_bounds__(kBlock) void k_len_range(const uint64_t* __restrict
         hi = max(hi, bb);
     }
     block_fold(lo, hi, none, zero);
+    __shared__ uint32_t is_last;
     if (threadIdx.x == 0) {
         part[3 * blockIdx.x] = lo;
         part[3 * blockIdx.x + 1] = hi;
         part[3 * blockIdx.x + 2] = 0u;
+        __threadfence();
+        is_last = atomicAdd(ticket, 1u) == gridDim.x - 1 ? 1u : 0u;
+    }
+    __syncthreads();
+    if (!is_last) return;
+    __threadfence();
+    lo = 0xFFFFFFFFu;
+    hi = 0u;
+    for (uint32_t b = threadIdx.x; b < gridDim.x; b += kBlock) {
+        lo = min(lo, __atomic_load_n(part + 3 * b, __ATOMIC_RELAXED));
+        hi = max(hi, __atomic_load_n(part + 3 * b + 1, __ATOMIC_RELAXED));
+    }
+    block_fold(lo, hi, none, zero);
+    if (threadIdx.x == 0) {
+        out[0] = lo;
+        out[1] = hi;
+        atomicExch(ticket, 0u);  // the next launch counts from 0
     }
 }
 
-hipError_t launch_len_range(const uint64_t* len, uint64_t n, unsigned int* out, uint32_t* part, hipStream_t s) {
+hipError_t launch_len_range(const uint64_t* len, uint64_t n, unsigned int* out, uint32_t* part, unsigned int* ticket,
+                            hipStream_t s) {
     const unsigned nb = unsigned((n + kBlock * 8 - 1) / (kBlock * 8));
-    hipLaunchKernelGGL(k_len_range, dim3(nb), dim3(kBlock), 0, s, len, n, part);
-    hipLaunchKernelGGL(k_locate_fold, dim3(1), dim3(kBlock), 0, s, part, nb, nullptr, out);
+    hipLaunchKernelGGL(k_len_range, dim3(nb), dim3(kBlock), 0, s, len, n, part, out, ticket);
     return hipGetLastError();
 }
 
