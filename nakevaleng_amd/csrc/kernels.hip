@@ -2040,6 +2040,7 @@ __global__ __launch_bounds__(kSmallBlock) void k_small_tree(const uint64_t* __re
     __shared__ uint32_t is_last;
     const uint32_t tid = threadIdx.x;
     const uint32_t i = blockIdx.x * kSmallBlock + tid;
+    NKV_STAMP(0);
     if (gridDim.x == 1 && 16u * n + vbytes <= kSmallSeg) {
         small_stage_in(reinterpret_cast<const uint8_t*>(desc), seg, 16u * n);
         small_stage_in(vals, seg + 16u * n, vbytes);
@@ -2047,8 +2048,10 @@ __global__ __launch_bounds__(kSmallBlock) void k_small_tree(const uint64_t* __re
         desc = reinterpret_cast<const uint64_t*>(seg);
         vals = seg + 16u * n;
     }
+    NKV_STAMP(1);
     uint32_t h[5] = {0u, 0u, 0u, 0u, 0u};
     if (i < n) sha1_value_aligned(vals + desc[2 * i], desc[2 * i + 1], h);  // NewLeaf, merklenode.go:27-34
+    NKV_STAMP(2);
     if (gridDim.x > 1) {
         if (i < n) store_digest(scratch, i, h);
         __threadfence();
@@ -2087,6 +2090,7 @@ __global__ __launch_bounds__(kSmallBlock) void k_small_tree(const uint64_t* __re
         cnt = pc;
         ++lv;
     } while (cnt > 1);
+    NKV_STAMP(3);
     const uint32_t total = base + 1;
     small_copy_out(sm, out, 20u * total);
     // the image, top level first: 0x00 + digest per node, one 0x01 after each
