@@ -166,6 +166,11 @@ int nkv_ctx_sync(nkv_ctx *ctx);
 #define NKV_OPT_ARENA_COHERENT 17   /* nkv_host_alloc blocks: 1 (default) = host-coherent pinned memory
                                        (copies read it as any pinned block, and the small path's kernel
                                        reads NewLeaf values in place); 0 = default pinned memory */
+#define NKV_OPT_SIDE_GATE 18 /* device-length batches on the gated plan (NKV_OPT_BUCKET 2): 1 (default) =
+                                the input-order leaf kernel runs on a second stream of the context,
+                                beside the length sort and the work queue (whichever of the two the
+                                device-side range opens does the work; the other exits), joined
+                                before the levels; 0 = all of them in turn on the context's stream */
 int nkv_ctx_set_option(nkv_ctx *ctx, int key, int64_t value);
 /* Which path the latest host-buffer tree call of the context took */
 #define NKV_PATH_GRID 0  /* copies + leaf kernel + per-level reduce launches */

@@ -426,6 +426,14 @@ int plan_of(nkv_ctx* c, const uint64_t* len, const uint64_t* host_len, uint64_t 
     return NKV_OK;
 }
 
+// The context's second stream and its fork / join events (NKV_OPT_SIDE_GATE).
+int side_ready(nkv_ctx* c) {
+    if (!c->side) HIPTRY(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+    for (hipEvent_t& e : c->side_ev)
+        if (!e) HIPTRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    return NKV_OK;
+}
+
 // Level 0 in the order plan_of chose.  Gated plans also launch the input-order
 // kernel (it runs when the range is narrow) unless the caller has its own
 // (narrow_kernel = false: k_leaf_verify).
@@ -449,11 +457,29 @@ int leaf_level(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint6
     uint32_t* perm = static_cast<uint32_t*>(c->d_perm.p);
     TRY(grow(c->d_queue, 4 * queue_words(n)));
     const QueueInit qi{static_cast<uint32_t*>(c->d_queue.p), queue_words(n), uint32_t(c->queue_split)};
-    HIPTRY(sort_by_length_desc(len, n, perm, static_cast<uint32_t*>(c->d_keys.p), c->stream, wide, qi, cw));
-    HIPTRY(launch_leaf_queue(base, off, len, perm, n, static_cast<uint32_t*>(c->d_queue.p), c->simds,
-                             uint32_t(c->queue_waves), nodes, c->stream, wide));
-    if (plan == kGated && narrow_kernel)
-        HIPTRY(launch_leaf_offsets(base, off, len, n, aligned, c->leaf_load, nodes, c->stream, Gate{range.range, 1}));
+    // the gated input-order kernel writes level 0 only when the range is narrow,
+    // the sort and the queue only when it is wide: on the side stream it runs
+    // beside them, so the closed ones cost the batch no launch slot
+    const bool narrow = plan == kGated && narrow_kernel;
+    const bool forked = narrow && c->side_gate;
+    if (forked) {
+        TRY(side_ready(c));
+        HIPTRY(hipEventRecord(c->side_ev[0], c->stream));
+        HIPTRY(hipStreamWaitEvent(c->side, c->side_ev[0], 0));
+        HIPTRY(launch_leaf_offsets(base, off, len, n, aligned, c->leaf_load, nodes, c->side, Gate{range.range, 1}));
+        HIPTRY(hipEventRecord(c->side_ev[1], c->side));
+    }
+    int rc = st(sort_by_length_desc(len, n, perm, static_cast<uint32_t*>(c->d_keys.p), c->stream, wide, qi, cw));
+    if (rc == NKV_OK)
+        rc = st(launch_leaf_queue(base, off, len, perm, n, static_cast<uint32_t*>(c->d_queue.p), c->simds,
+                                  uint32_t(c->queue_waves), nodes, c->stream, wide));
+    if (forked) {  // joined whatever happened above: nothing on the stream may pass it
+        const int j = st(hipStreamWaitEvent(c->stream, c->side_ev[1], 0));
+        if (rc == NKV_OK) rc = j;
+    } else if (rc == NKV_OK && narrow) {
+        rc = st(launch_leaf_offsets(base, off, len, n, aligned, c->leaf_load, nodes, c->stream, Gate{range.range, 1}));
+    }
+    TRY(rc);
     c->sort_dirty = false;
     return NKV_OK;
 }
@@ -616,6 +642,10 @@ void nkv_ctx_destroy(nkv_ctx* c) {
     for (hipEvent_t e : c->host_ev)
         if (e) (void)hipEventDestroy(e);
     if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
+    if (c->side) (void)hipStreamSynchronize(c->side);
+    for (hipEvent_t e : c->side_ev)
+        if (e) (void)hipEventDestroy(e);
+    if (c->side) (void)hipStreamDestroy(c->side);
     if (c->switch_ev) (void)hipEventDestroy(c->switch_ev);
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;
@@ -704,6 +734,10 @@ int nkv_ctx_set_option(nkv_ctx* c, int key, int64_t value) try {
         case NKV_OPT_ARENA_COHERENT:
             if (value < 0 || value > 1) return NKV_ERR_INVALID;
             c->arena_coherent = int(value);
+            return NKV_OK;
+        case NKV_OPT_SIDE_GATE:
+            if (value < 0 || value > 1) return NKV_ERR_INVALID;
+            c->side_gate = int(value);
             return NKV_OK;
         case NKV_OPT_SMALL_MAX_BYTES:
             if (value < 0 || value > (int64_t(1) << 30)) return NKV_ERR_INVALID;

@@ -193,6 +193,11 @@ struct nkv_ctx {
     // host-coherent pinned in / out buffers the kernel reads and writes across
     // PCIe (or device copies of them, small_path 2), and its device scratch
     // (the ticket word + 20 n leaf digests)
+    // NKV_OPT_SIDE_GATE: the gated plan's input-order kernel on a second stream
+    // (created on first use), forked after the range and joined before the levels
+    int side_gate = 1;
+    hipStream_t side = nullptr;
+    hipEvent_t side_ev[2] = {nullptr, nullptr};
     int arena_coherent = 1;  // NKV_OPT_ARENA_COHERENT: nkv_host_alloc blocks host-coherent
     int small_path = 1;
     uint64_t small_max_n = 1024;

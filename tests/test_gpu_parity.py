@@ -411,6 +411,45 @@ def test_bucket_modes_narrow_and_wide(nkv, oracle, bucket, spread):
     assert np.array_equal(d_nodes.cpu().numpy().reshape(-1, 20), want)
 
 
+@pytest.mark.parametrize("side_gate", [0, 1])
+def test_side_gate_alternating(nkv, oracle, side_gate):
+    """NKV_OPT_SIDE_GATE: the gated plan's input-order kernel on the context's
+    second stream (1) or in turn on its own stream (0).  Narrow, wide and narrow
+    batches back to back on one context into one node buffer, read only after
+    the last: each call's level 0 and levels are joined before the next call's
+    kernels touch the buffer, so every tree is the oracle's."""
+    torch = _torch()
+    _lib, _ = nkv
+    ctx = _lib.Context(0)
+    _bind(torch, ctx)
+    ctx.set_option(_lib.NKV_OPT_BUCKET, 2)
+    ctx.set_option(_lib.NKV_OPT_SIDE_GATE, side_gate)
+    L = _lib.lib()
+    n = 5000
+    cases = []
+    for k, spread in enumerate((0, 40, 0, 40)):
+        rng = np.random.default_rng(7 * k + spread)
+        lens = (4050 + 64 * rng.integers(-spread, spread + 1, n)).astype(np.uint64)
+        off = np.zeros(n, np.uint64)
+        off[1:] = np.cumsum(lens[:-1] + 17)
+        data = oracle.splitmix64_bytes(int(off[-1] + lens[-1]), SEED + 11 * k)
+        cases.append((data, off, lens))
+    d_nodes = torch.zeros(L.nkv_total_nodes(n) * 20, dtype=torch.uint8, device="cuda")
+    outs = []
+    try:
+        for data, off, lens in cases:
+            d_data, d_off, d_len = _dev(torch, data), _dev(torch, off), _dev(torch, lens)
+            _lib.check(L.nkv_tree_from_values_dev(ctx.h, d_data.data_ptr(), d_off.data_ptr(), d_len.data_ptr(),
+                                                  n, d_nodes.data_ptr()))
+            outs.append(d_nodes.clone())  # torch's stream: ordered behind the call
+        torch.cuda.synchronize()
+    finally:
+        ctx.close()
+    for (data, off, lens), got in zip(cases, outs):
+        want = oracle.tree_from_digests(oracle.leaf_hashes(data, off, lens, threads=8))
+        assert np.array_equal(got.cpu().numpy().reshape(-1, 20), want)
+
+
 @pytest.mark.parametrize("load", [4, 11])
 @pytest.mark.parametrize("shift", [0, 1, 2, 15, 16, 17, 46, 48, 63])
 @pytest.mark.parametrize("n,vlen,rec", [(1, 4050, 4096), (63, 4050, 4096), (3001, 4050, 4096), (777, 327, 400),
