@@ -76,3 +76,19 @@ def test_c_caller_on_gpu(tmp_path, oracle, n):
     assert kv["img_fnv"] == fnv1a64(oracle.bfs_image(nodes, n))
     assert kv["path"] == ("1" if n <= 1024 else "0")
     assert kv["empty"] == "1 cannot build Merkle Tree from 0 nodes"
+
+
+def test_python_constants_match_header():
+    """Every integer #define of include/nkv_merkle.h that the Python binding
+    mirrors has the header's value, and every option key is mirrored."""
+    import re
+    from nakevaleng_amd import _lib
+    text = open(os.path.join(ROOT, "include", "nkv_merkle.h")).read()
+    defs = {m.group(1): int(m.group(2), 0)
+            for m in re.finditer(r"^#define (NKV_[A-Z0-9_]+)\s+\(?(-?(?:0x[0-9a-fA-F]+|\d+))\)?", text, re.M)}
+    assert "NKV_OPT_SIDE_GATE" in defs and "NKV_ABI_VERSION" in defs
+    for name, v in defs.items():
+        if hasattr(_lib, name):
+            assert getattr(_lib, name) == v, name
+    missing = [k for k in defs if k.startswith("NKV_OPT_") and not hasattr(_lib, k)]
+    assert not missing, missing
