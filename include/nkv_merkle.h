@@ -171,6 +171,11 @@ int nkv_ctx_sync(nkv_ctx *ctx);
                                 beside the length sort and the work queue (whichever of the two the
                                 device-side range opens does the work; the other exits), joined
                                 before the levels; 0 = all of them in turn on the context's stream */
+#define NKV_OPT_QUEUE_PAIR 19 /* work-queue kernel, batches bound by their longest chain: 0 (default) = one
+                                 wave per group; p = 1..100: two-wave workgroups, and the groups whose
+                                 first value has >= p % of the longest value's compressions are hashed
+                                 by a pair -- one wave expands the message schedule into LDS, the
+                                 other runs only the rounds (a shorter chain per block) */
 int nkv_ctx_set_option(nkv_ctx *ctx, int key, int64_t value);
 /* Which path the latest host-buffer tree call of the context took */
 #define NKV_PATH_GRID 0  /* copies + leaf kernel + per-level reduce launches */
