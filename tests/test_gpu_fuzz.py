@@ -36,7 +36,6 @@ def _options(rng, _lib):
         _lib.NKV_OPT_HOST_THREADS: int(rng.choice([0, 1, 3, 16])),
         _lib.NKV_OPT_STAGE_CHUNK: int(rng.choice([4096, 65536, 32 << 20])),
         _lib.NKV_OPT_SIDE_GATE: int(rng.integers(0, 2)),
-        _lib.NKV_OPT_QUEUE_PAIR: int(rng.choice([0, 0, 1, 50, 100])),
     }
 
 

@@ -5,6 +5,7 @@ finishes in seconds; the full BASELINE config (1 Mi x 4 KiB) is compared in
 full against the multi-threaded C oracle.
 """
 import hashlib
+import os
 
 import numpy as np
 import pytest
@@ -450,6 +451,9 @@ def test_side_gate_alternating(nkv, oracle, side_gate):
         assert np.array_equal(got.cpu().numpy().reshape(-1, 20), want)
 
 
+@pytest.mark.skipif(os.environ.get("NKV_TEST_QUEUE_PAIR") != "1",
+                    reason="pair mode (NKV_OPT_QUEUE_PAIR, off by default) has not run on a GPU yet: "
+                           "set NKV_TEST_QUEUE_PAIR=1 (tools/r05_fifth.sh does)")
 @pytest.mark.parametrize("pct", [0, 1, 50, 90, 100])
 @pytest.mark.parametrize("shape", ["one_long", "log_uniform", "throughput"])
 def test_queue_pair(nkv, oracle, pct, shape):

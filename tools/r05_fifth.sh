@@ -8,7 +8,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 O=gpurun_out/r05f
 mkdir -p $O
-timeout -k 10 400 python3 -u -m pytest tests/test_gpu_parity.py -k "side_gate or queue_pair or bucket_modes" -x -q \
+NKV_TEST_QUEUE_PAIR=1 timeout -k 10 400 python3 -u -m pytest tests/test_gpu_parity.py -k "side_gate or queue_pair or bucket_modes" -x -q \
     --timeout 120 --timeout-method thread > $O/pair_tests.txt 2>&1 || { tail -30 $O/pair_tests.txt; exit 1; }
 tail -2 $O/pair_tests.txt
 NKV_LONE_SPLIT=1 timeout -k 10 120 ./tools/lone_wave.bin > $O/lone_split.txt 2>&1 || { cat $O/lone_split.txt; exit 1; }
