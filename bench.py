@@ -26,6 +26,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md (chip table)
+PCIE_SPEC_GBS = 63.0  # host link, PCIe Gen5 x16 (same table)
 # The VALU-issue ceiling of the leaf kernel at the shader clock its waves
 # actually ran at in the timed loop (the clock probe, sclk_mhz): every SIMD
 # issuing one VALU instruction per VALU_CYCLES cycles (the half-rate ops
@@ -258,7 +259,22 @@ def cpu_sample(args, rank: int = 0) -> dict:
                 "nbytes": nbytes, "text": f"BASELINE configs[2]'s batch: {len(lens)} values of 64 B - 64 KiB "
                                           f"({nbytes} B, splitmix64 seed {SEED_MIXED + rank:#x})"}
     n = min(args.cpu_sample_leaves, args.leaves)
-    if cfg in ("records", "records_verify"):
+    if cfg == "records_verify":
+        # the Data table build_tables writes (KeySize, ValueSize in every
+        # header, each record's right Crc at +0: record.go:191-199, :51), which
+        # the host reads back as merge does (record.go:163-169, lsmtree.go:210-211)
+        rb, ks = args.value_bytes, args.key_bytes
+        vlen = rb - 30 - ks
+        data = oc.splitmix64_bytes(n * rb, SEED + rank)
+        v = data.reshape(n, rb)
+        v[:, 14:22] = np.frombuffer(np.uint64(ks).tobytes(), np.uint8)
+        v[:, 22:30] = np.frombuffer(np.uint64(vlen).tobytes(), np.uint8)
+        rec_off = np.arange(n, dtype=np.uint64) * rb
+        oc.seal_records(data, rec_off, host_threads())
+        return {"data": data, "rec_off": rec_off, "n": n, "nbytes": n * vlen,
+                "text": f"{n} serialized {rb}-B records ({ks}-B key, {vlen}-B value; splitmix64 seed "
+                        f"{SEED + rank:#x}), each record's Crc over Key ++ Value checked and its Value hashed"}
+    if cfg == "records":
         rb, ks = args.value_bytes, args.key_bytes
         vlen = rb - 30 - ks
         # the Values sit at rec + 30 + KeySize (record.go:191-199); the header
@@ -280,6 +296,13 @@ def cpu_sample(args, rank: int = 0) -> dict:
 # is single-threaded) and on every host thread this process may use.
 CPU_VARIANTS = (("port_1core", "port", False), ("openssl_1core", "openssl", False),
                 ("port_all_cores", "port", True), ("all_cores_openssl", "openssl", True))
+# records_verify's variants add the record check: the port with a
+# slicing-by-8 CRC-32, the OpenSSL variant with a PCLMULQDQ one (what Go's
+# hash/crc32 runs on amd64), fused per record with the leaf SHA-1
+# (oracle/record_crc_oracle.c nkvo_verify_records)
+CPU_IMPL_TEXT = {"port": "the portable C restatement (oracle/merkle_oracle.c)",
+                 "openssl": "the C restatement's tree over OpenSSL's SHA-1 (libcrypto, SHA-NI; "
+                            "oracle/merkle_openssl.c)"}
 
 
 def cpu_baseline(args, rank: int = 0) -> dict:
@@ -297,7 +320,13 @@ def cpu_baseline(args, rank: int = 0) -> dict:
     for name, impl, allc in CPU_VARIANTS:
         t = threads if allc else 1
         t0 = time.perf_counter()
-        if impl == "port":
+        if "rec_off" in s:  # records_verify: Crc check + leaf hash in one pass per record, then the tree
+            leaves, bad = oc.verify_records(data, s["rec_off"], threads=t, openssl=impl == "openssl")
+            if bad:
+                raise SystemExit(f"bench.py: {bad} records failed the CPU Crc check")
+            nodes = (oc.ossl_tree_from_digests(leaves, threads=t) if impl == "openssl"
+                     else oc.tree_from_digests(leaves, threads=t))
+        elif impl == "port":
             leaves = (oc.leaf_hashes_strided(data, s["stride"], s["L"], n, threads=t) if "stride" in s
                       else oc.leaf_hashes(data, s["off"], s["lens"], threads=t))
             nodes = oc.tree_from_digests(leaves, threads=t)
@@ -313,11 +342,18 @@ def cpu_baseline(args, rank: int = 0) -> dict:
     if len(roots) != 1:
         raise SystemExit(f"bench.py: the CPU variants disagree on the root ({sorted(roots)})")
     best = max(out, key=lambda k: out[k]["value"])
+    impl = dict((v[0], v[1]) for v in CPU_VARIANTS)[best]
     return {
         "value": out[best]["value"],
         "unit": "GiB/s",
         "cores": out[best]["cores"],
+        # every variant is a CPU restatement timed on this host (the contract's
+        # "port"; the Go reference cannot run here); `impl` names whose SHA-1
+        # the strongest one, which `value` reports, runs
         "kind": "port",
+        "impl": impl,
+        "impl_text": CPU_IMPL_TEXT[impl] + (f" on {out[best]['cores']} threads" if out[best]["cores"] > 1
+                                            else " on one thread"),
         "best": best,
         "sample": s["text"] + ", leaf hash + full tree",
         "cpu_model": cpu_model(),
@@ -735,10 +771,17 @@ def main():
     print(json.dumps(out), flush=True)
 
 
-# sub-record key -> the child's --config (bench.py --gpus 1 only)
-SUBCONFIGS = (("config2_mixed", "mixed"), ("config1_records", "records"))
+# sub-record key -> the child's --config (bench.py --gpus 1 only): configs[2];
+# configs[1] as serialized records (the flush's input, sstable.go:58-74); the
+# compaction read as merge performs it, every record's Crc checked before its
+# Value is hashed (record.go:163-169, lsmtree.go:210-211); the host-inclusive
+# flush through the Go-API mirror (pinned arena, PCIe both ways)
+SUBCONFIGS = (("config2_mixed", "mixed"), ("config1_records", "records"),
+              ("config1_records_verify", "records_verify"), ("api_flush", "api_flush"))
 SUB_KEYS = ("value", "unit", "n_gpus", "steps", "ms_per_step", "sclk_mhz", "roofline", "kernel_ms",
-            "verified_vs_oracle", "verified_basis", "root", "cpu_baseline", "vs_cpu_best", "vs_cpu_port_1core")
+            "verified_vs_oracle", "verified_basis", "root", "cpu_baseline", "vs_cpu_best", "vs_cpu_port_1core",
+            "crc_checked", "value_basis", "breakdown_ms", "first_flush", "first_over_steady_time", "reserve_ms",
+            "first_flush_no_reserve", "bound_note")
 
 
 def sub_child(args, config, timeout, run=None):
@@ -965,6 +1008,11 @@ def run_ranks(args, T):
         want = expected_roots(args.config, n, t0_.get("rb", vlen), rank, T, args.key_bytes, args.mixed_bytes)
         mine = [t["nodes"][-20:].cpu().numpy().tobytes().hex() for t in tabs]
         code = -1 if want is None else int(mine == want)
+    crc_stats = None
+    if verify_crc:  # the last step's record check: every stored Crc must have matched, no header outside
+        crc_stats = [t["d_stats"].cpu().tolist() for t in tabs]
+        if any(st != [0, -1, 0] for st in crc_stats):
+            code = 0
     codes = rank_codes(dist if use_dist else None, world, rank, code, "cuda")
     verified = verdict(codes)
     if args.verify and rank == 0 and verified is None:
@@ -1051,6 +1099,11 @@ def run_ranks(args, T):
                                     "chain_floor_basis": f"longest value {longest} compressions x "
                                                          f"{LONE_WAVE_CYCLES_PER_BLOCK:g} cycles at {sclk:.0f} MHz",
                                     "chain_frac": round(floor_ms / leaf_ms, 4)})
+        if crc_stats is not None:
+            out["crc_checked"] = {"records_per_table": n, "tables": T,
+                                  "crc_mismatches": sum(st[0] for st in crc_stats),
+                                  "header_errors": sum(st[2] for st in crc_stats),
+                                  "basis": "d_stats of nkv_tree_verify_records_dev after the last timed step"}
         out["verified_vs_oracle"] = verified
         out["verified_ranks"] = [None if c < 0 else bool(c) for c in codes]
         out["verified_basis"] = ("tests/golden/bench_roots.json (C oracle roots of the same seeds, committed)"
@@ -1151,6 +1204,17 @@ def main_api_flush(args):
         "root": root,
         "verified_vs_oracle": verified,
         "cpu_baseline": cpu,
+        # the path starts and ends in host memory: its bound is the host link,
+        # not HBM (the payload crosses PCIe once, host -> HBM)
+        "bound_note": {
+            "bound": "pcie",
+            "link_spec_gbs": PCIE_SPEC_GBS,
+            "achieved_gbs": round(n * vlen / (b["total_ms"] * 1e-3) / 1e9, 2),
+            "frac_of_link": round(n * vlen / (b["total_ms"] * 1e-3) / 1e9 / PCIE_SPEC_GBS, 3),
+            "cpu_comparator": (f"cpu_baseline runs on the {cpu['host_threads']} host threads this job may use "
+                               f"({cpu['cpu_model']}); a whole socket hashing in memory would beat this "
+                               "PCIe-bound path" if cpu else None),
+        },
     }
     out.update(vs_cpu(b["gib_s"], cpu))
     print(json.dumps(out), flush=True)

@@ -222,10 +222,12 @@ uint64_t nkv_bfs_size(uint64_t n); /* Serialize() bytes for 20-byte leaves */
  * overlaps the caller's NewLeaf loop; the next call over the block moves only
  * the rest.  Those bytes must not change until that call returns.  A call over
  * the block ends the batch; an upto below the previous one starts a new batch.
- * nkv_host_free waits for copies from the block.  nkv_host_alloc also
- * allocates the block's device mirror (as many bytes of HBM), so a block
- * reserved once (e.g. at engine start, from the memtable's capacity) costs
- * the flushes that use it no allocation. */
+ * nkv_host_free waits for copies from the block.  For a block of at least
+ * 64 MiB nkv_host_alloc also allocates its device mirror (as many bytes of
+ * HBM), so a block reserved once (e.g. at engine start, from the memtable's
+ * capacity) costs the flushes that use it no allocation; smaller blocks, or a
+ * mirror that does not fit the free HBM at that moment, get it on first use
+ * (values that take the small path never need it). */
 int nkv_host_alloc(nkv_ctx *ctx, uint64_t bytes, void **out);
 int nkv_host_free(nkv_ctx *ctx, void *p);
 int nkv_host_stream(nkv_ctx *ctx, const void *block, uint64_t upto);

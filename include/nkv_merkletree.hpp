@@ -592,8 +592,11 @@ class Session {
     }
     // A block of at least `bytes`: exactly that for Reserve, else (NewLeaf
     // outgrowing the block) twice the old size, from kFirstArena.  The open
-    // batch's values move with it.
-    static constexpr uint64_t kFirstArena = uint64_t(64) << 20;
+    // batch's values move with it.  A process that only flushes the engine's
+    // default 10-value memtables pins 1 MiB (and, since its values take the
+    // small path, no HBM mirror: nkv_host_alloc mirrors blocks of >= 64 MiB
+    // up front, smaller ones on first use).
+    static constexpr uint64_t kFirstArena = uint64_t(1) << 20;
     void Grow(uint64_t bytes, bool doubling) {
         if (bytes <= cap_) return;
         Settle();  // no queued copy may land in the old block

@@ -10,6 +10,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <new>
 #include <vector>
@@ -225,6 +226,8 @@ int grow_coherent(uint8_t** p, size_t* cap, size_t bytes) {
 // (NKV_OPT_SMALL_PATH 1) or that is copied to HBM first (2), the kernel writes
 // nodes + image into a pinned output buffer (or HBM, then one copy back), and
 // the call synchronizes once.  *taken = false: not eligible, nothing done.
+constexpr uint64_t kSmallMaxExtent = 0xFFFFFFF0ull;  // the kernel's 32-bit extent of in-place values
+constexpr int64_t kSmallSpinUs = 2000;  // host spin on the completion word before the runtime's wait
 int small_tree(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint64_t* len, uint64_t n,
                uint8_t* root20, uint8_t* nodes_out, uint8_t* img_out, bool* taken) {
     *taken = false;
@@ -244,7 +247,10 @@ int small_tree(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint6
     if (blk) blk->streamed = 0;  // a call over a pinned block ends its batch (nkv_host_stream)
     // values in a host-coherent arena block at 16-byte aligned places (the
     // mirrors' NewLeaf arena) are read where they lie: no pack, no copy
-    bool in_place = blk && blk->coherent && c->small_path == 1 && (lo & 15) == 0;
+    // (only while their extent in the block, gaps included, stays within the
+    // small bound: the kernel takes the extent as a 32-bit byte count)
+    bool in_place = blk && blk->coherent && c->small_path == 1 && (lo & 15) == 0 &&
+                    align16(hi) - lo <= std::min<uint64_t>(c->small_max_bytes, kSmallMaxExtent);
     const uint64_t adj = blk ? uint64_t(base - blk->p) : 0;
     for (uint64_t i = 0; in_place && i < n; ++i) in_place = ((adj + off[i]) & 15) == 0;
     const uint64_t vext = in_place ? align16(hi) - lo : vbytes;  // the values' extent
@@ -300,7 +306,11 @@ int small_tree(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint6
                                  c->stream));
         // the kernel's last store is seq into the completion word, after every
         // output byte: spin on it (a few us sooner than the runtime's
-        // completion wait); every 256 polls ask the stream whether it failed
+        // completion wait); every 256 polls ask the stream whether it failed.
+        // The spin is bounded (kSmallSpinUs): a kernel queued behind other work
+        // on a caller's stream is waited for by the runtime instead, so no
+        // host core spins for the length of someone else's queue.
+        const auto t_spin = std::chrono::steady_clock::now();
         for (uint32_t k = 1;; ++k) {
             if (__atomic_load_n(hdone, __ATOMIC_ACQUIRE) == seq) break;
             if ((k & 255u) == 0u) {
@@ -310,6 +320,11 @@ int small_tree(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint6
                     break;
                 }
                 if (q != hipErrorNotReady) return st_at(q, "k_small_tree", __FILE__, __LINE__);
+                if (std::chrono::steady_clock::now() - t_spin > std::chrono::microseconds(kSmallSpinUs)) {
+                    HIPTRY(hipStreamSynchronize(c->stream));
+                    if (__atomic_load_n(hdone, __ATOMIC_ACQUIRE) != seq) return NKV_ERR_DEVICE;
+                    break;
+                }
             }
             __builtin_ia32_pause();
         }
@@ -880,6 +895,7 @@ uint64_t nkv_total_nodes(uint64_t n) { return total_of(n); }
 uint64_t nkv_bfs_size(uint64_t n) { return n == 0 ? 0 : layout_of(counts_of(n)).total; }
 
 // ---- pinned arena ----
+constexpr uint64_t kEagerMirrorBytes = uint64_t(64) << 20;
 int nkv_host_alloc(nkv_ctx* c, uint64_t bytes, void** out) try {
     if (!out) return NKV_ERR_INVALID;
     *out = nullptr;
@@ -899,13 +915,12 @@ int nkv_host_alloc(nkv_ctx* c, uint64_t bytes, void** out) try {
         (void)hipHostFree(p);
         return NKV_ERR_NOMEM;
     }
-    // the block's device mirror now, not inside the first flush that streams
-    // into it (an arena reserved at engine start costs a flush nothing)
-    if (grow(blk->d_arena, blk->bytes) != NKV_OK) {
-        (void)hipHostFree(p);
-        delete blk;
-        return NKV_ERR_NOMEM;
-    }
+    // a large block's device mirror now, not inside the first flush that
+    // streams into it (an arena reserved at engine start costs a flush
+    // nothing); small blocks, and any block whose mirror does not fit the HBM
+    // free right now, get theirs on first use (stream_block): a caller whose
+    // values only ever take the small path never needs it
+    if (blk->bytes >= kEagerMirrorBytes && grow(blk->d_arena, blk->bytes) != NKV_OK) (void)hipGetLastError();
     c->pinned.push_back(blk);
     *out = p;
     return NKV_OK;

@@ -510,7 +510,10 @@ __device__ __forceinline__ void wait_vmcnt() {
 // sink(b, w): block b's 16 big-endian words (clobbered), every lane, every
 // b < the wave's longest value (sha1_blocks_ring_vc compresses the lane's own;
 // k_leaf_queue_pair's schedule wave expands them for its partner)
-template <int R, class Sink>
+// kDrain: the window reads of block b + 1 complete before sink(b) runs (a sink
+// that issues LDS instructions and waits of its own must not find the ring's
+// asm ds_reads into nxt still in flight)
+template <int R, bool kDrain = false, class Sink>
 __device__ __forceinline__ void ring_vc_blocks(uint8_t* wbuf, const uint8_t* p, uint32_t my_nfull, Sink&& sink) {
     static_assert(R >= 2 && R <= 4, "ring depth");
     const int lane = threadIdx.x & 63;
@@ -590,6 +593,8 @@ __device__ __forceinline__ void ring_vc_blocks(uint8_t* wbuf, const uint8_t* p, 
         issue(b + R);
         wait_vmcnt<4 * (R - 1)>();
         read_window(b + 1, nxt);
+        if constexpr (kDrain)
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(nxt[0]), "+v"(nxt[1]), "+v"(nxt[2]), "+v"(nxt[3]) : : "memory");
         uint4 c4[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) c4[q] = make_uint4(cur[q].x, cur[q].y, cur[q].z, cur[q].w);
@@ -1398,6 +1403,12 @@ __global__ __launch_bounds__(64, kQueueRing) void k_leaf_queue(const uint8_t* __
 // pair took is still hashed.
 constexpr uint32_t kPairSlots = 3;  // W ring: chunks of 16 words x 64 lanes, 4 KiB each
 constexpr uint32_t kPairRelease = 0xFFFFFFFFu;  // ctl[0]: no long group left, the waves part
+// Every wait on the partner wave is bounded: a wave polls an LDS counter at
+// most kPairSpin times (s_sleep 1 between polls, ~0.1-0.2 s in all), then
+// stops waiting for good and raises ctl[4]; the pair loop then ends for both
+// waves, so a protocol slip gives wrong digests (which the parity tests
+// catch), never a wave that spins until the process is killed.
+constexpr uint32_t kPairSpin = 1u << 21;
 
 __device__ __forceinline__ uint32_t lds_addr(const void* p) { return uint32_t(reinterpret_cast<uintptr_t>(p)); }
 
@@ -1460,10 +1471,17 @@ __device__ __forceinline__ void sha1_rounds16(uint32_t s[5], const u32x4 w[4]) {
 __device__ __forceinline__ void pair_schedule(uint8_t* ring, uint8_t* wring, const uint32_t* ctl,
                                               const uint8_t* p, uint32_t my_nfull) {
     const uint32_t row = lds_addr(wring) + 64u * uint32_t(threadIdx.x & 63);
-    const uint32_t a_written = lds_addr(ctl + 1), a_read = lds_addr(ctl + 2);
+    const uint32_t a_written = lds_addr(ctl + 1), a_read = lds_addr(ctl + 2), a_abort = lds_addr(ctl + 4);
     uint32_t k = 0, read = 0;
+    bool dead = false;  // wave-uniform: gave up on the partner
     auto put = [&](const uint32_t w[16]) {
-        while (k >= read + kPairSlots) {
+        if (dead) return;
+        for (uint32_t spin = 0; k >= read + kPairSlots; ++spin) {
+            if (spin == kPairSpin) {
+                dead = true;
+                lds_poke(a_abort, 1u);
+                return;
+            }
             read = lds_peek(a_read);
             if (k >= read + kPairSlots) __builtin_amdgcn_s_sleep(1);
         }
@@ -1474,7 +1492,7 @@ __device__ __forceinline__ void pair_schedule(uint8_t* ring, uint8_t* wring, con
         ds_write_b128_off<48>(s0, u32x4{w[12], w[13], w[14], w[15]});
         lds_poke(a_written, ++k);
     };
-    ring_vc_blocks<kQueueRing>(ring, p, my_nfull, [&](uint32_t, uint32_t w[16]) {
+    ring_vc_blocks<kQueueRing, true>(ring, p, my_nfull, [&](uint32_t, uint32_t w[16]) {
         put(w);
 #pragma unroll
         for (int j = 1; j < 5; ++j) {
@@ -1488,16 +1506,28 @@ __device__ __forceinline__ void pair_schedule(uint8_t* ring, uint8_t* wring, con
 
 // wave 0 of a pair: the rounds of every block from the W ring, one chunk read
 // ahead; a lane keeps a block's result only while the block is its value's
+// wait until the partner has written chunk `next` (bounded: see kPairSpin)
+__device__ __forceinline__ void pair_wait_written(uint32_t next, uint32_t& written, bool& dead, uint32_t a_written,
+                                                  uint32_t a_abort) {
+    if (dead) return;
+    for (uint32_t spin = 0; written <= next; ++spin) {
+        if (spin == kPairSpin) {
+            dead = true;
+            lds_poke(a_abort, 1u);
+            return;
+        }
+        written = lds_peek(a_written);
+        if (written <= next) __builtin_amdgcn_s_sleep(1);
+    }
+}
+
 template <int J>
 __device__ __forceinline__ void pair_chunk(uint32_t s[5], u32x4 cur[4], u32x4 nxt[4], uint32_t next,
-                                           uint32_t total, uint32_t& written, uint32_t row, uint32_t a_written,
-                                           uint32_t a_read) {
+                                           uint32_t total, uint32_t& written, bool& dead, uint32_t row,
+                                           uint32_t a_written, uint32_t a_read, uint32_t a_abort) {
     const bool more = next < total;
     if (more) {
-        while (written <= next) {
-            written = lds_peek(a_written);
-            if (written <= next) __builtin_amdgcn_s_sleep(1);
-        }
+        pair_wait_written(next, written, dead, a_written, a_abort);
         const uint32_t s0 = row + 4096u * (next % kPairSlots);
         nxt[0] = ds_read_b128_off<0>(s0);
         nxt[1] = ds_read_b128_off<16>(s0);
@@ -1518,14 +1548,12 @@ __device__ __forceinline__ void pair_rounds(uint8_t* wring, const uint32_t* ctl,
     const uint32_t nmax = wave_max_u32(my_nfull);
     if (nmax == 0) return;
     const uint32_t row = lds_addr(wring) + 64u * uint32_t(threadIdx.x & 63);
-    const uint32_t a_written = lds_addr(ctl + 1), a_read = lds_addr(ctl + 2);
+    const uint32_t a_written = lds_addr(ctl + 1), a_read = lds_addr(ctl + 2), a_abort = lds_addr(ctl + 4);
     const uint32_t total = 5u * nmax;
     uint32_t written = 0;
+    bool dead = false;  // wave-uniform: gave up on the partner
     u32x4 cur[4], nxt[4];
-    while (written == 0) {
-        written = lds_peek(a_written);
-        if (written == 0) __builtin_amdgcn_s_sleep(1);
-    }
+    pair_wait_written(0u, written, dead, a_written, a_abort);
     cur[0] = ds_read_b128_off<0>(row);
     cur[1] = ds_read_b128_off<16>(row);
     cur[2] = ds_read_b128_off<32>(row);
@@ -1535,11 +1563,11 @@ __device__ __forceinline__ void pair_rounds(uint8_t* wring, const uint32_t* ctl,
     for (uint32_t b = 0; b < nmax; ++b) {
         uint32_t s[5] = {h[0], h[1], h[2], h[3], h[4]};
         const uint32_t k = 5u * b;
-        pair_chunk<0>(s, cur, nxt, k + 1, total, written, row, a_written, a_read);
-        pair_chunk<1>(s, cur, nxt, k + 2, total, written, row, a_written, a_read);
-        pair_chunk<2>(s, cur, nxt, k + 3, total, written, row, a_written, a_read);
-        pair_chunk<3>(s, cur, nxt, k + 4, total, written, row, a_written, a_read);
-        pair_chunk<4>(s, cur, nxt, k + 5, total, written, row, a_written, a_read);
+        pair_chunk<0>(s, cur, nxt, k + 1, total, written, dead, row, a_written, a_read, a_abort);
+        pair_chunk<1>(s, cur, nxt, k + 2, total, written, dead, row, a_written, a_read, a_abort);
+        pair_chunk<2>(s, cur, nxt, k + 3, total, written, dead, row, a_written, a_read, a_abort);
+        pair_chunk<3>(s, cur, nxt, k + 4, total, written, dead, row, a_written, a_read, a_abort);
+        pair_chunk<4>(s, cur, nxt, k + 5, total, written, dead, row, a_written, a_read, a_abort);
         if (b < my_nfull) {
 #pragma unroll
             for (int q = 0; q < 5; ++q) h[q] += s[q];
@@ -1580,7 +1608,9 @@ __global__ __launch_bounds__(128, kQueueRing) void k_leaf_queue_pair(const uint8
                                                              uint32_t* __restrict__ q, uint32_t pct,
                                                              uint8_t* __restrict__ nodes, Gate gate) {
     __shared__ __attribute__((aligned(16))) uint8_t smem[2][4096 * kQueueRing];
-    __shared__ uint32_t ctl[4];  // [0] the pair's group (kPairRelease: none), [1] chunks written, [2] read
+    // [0] the pair's group (kPairRelease: none), [1] chunks written, [2] read,
+    // [3] the workgroup's mode, [4] a wave gave up on its partner (kPairSpin)
+    __shared__ uint32_t ctl[5];
     if (!gate.open()) return;
     const ClockProbe clk;
     const int wave = threadIdx.x >> 6;
@@ -1613,7 +1643,10 @@ __global__ __launch_bounds__(128, kQueueRing) void k_leaf_queue_pair(const uint8
         P = __builtin_amdgcn_readfirstlane(min(lo, first_short));
     }
     // wave 0's election decides the workgroup's mode
-    if (threadIdx.x == 0) ctl[3] = front && P ? 1u : 0u;
+    if (threadIdx.x == 0) {
+        ctl[3] = front && P ? 1u : 0u;
+        ctl[4] = 0u;
+    }
     __syncthreads();
     const bool pair = ctl[3] != 0u;
     if (pair) {
@@ -1654,6 +1687,7 @@ __global__ __launch_bounds__(128, kQueueRing) void k_leaf_queue_pair(const uint8
                 }
             }
             __syncthreads();  // both waves are done with the rings and the counters
+            if (__builtin_amdgcn_readfirstlane(ctl[4]) != 0u) break;  // no more pairs after a give-up
         }
         if (!front) __builtin_amdgcn_s_setprio(0);
     } else if (front) {

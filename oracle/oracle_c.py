@@ -83,6 +83,15 @@ def lib():
         L.nkvo_crc32.restype = ctypes.c_uint32
         L.nkvo_record_crcs.argtypes = [u8p, u64p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint32), u8p]
         L.nkvo_record_crcs.restype = ctypes.c_uint64
+        L.nkvo_crc32_s8.argtypes = [u8p, ctypes.c_uint64]
+        L.nkvo_crc32_s8.restype = ctypes.c_uint32
+        L.nkvo_crc32_clmul.argtypes = [u8p, ctypes.c_uint64]
+        L.nkvo_crc32_clmul.restype = ctypes.c_uint32
+        L.nkvo_verify_records.argtypes = [u8p, u64p, ctypes.c_uint64, u8p, ctypes.c_int, ctypes.c_void_p,
+                                          ctypes.c_int]
+        L.nkvo_verify_records.restype = ctypes.c_uint64
+        L.nkvo_seal_records.argtypes = [u8p, u64p, ctypes.c_uint64, ctypes.c_int]
+        L.nkvo_seal_records.restype = None
         L.nkvo_murmur3_32.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint32]
         L.nkvo_murmur3_32.restype = ctypes.c_uint32
         L.nkvo_bloom_params.argtypes = [ctypes.c_uint64, ctypes.c_double, ctypes.POINTER(ctypes.c_uint32),
@@ -256,6 +265,39 @@ def record_crcs(stream: np.ndarray, rec_off: np.ndarray):
     bad = lib().nkvo_record_crcs(_p8(stream), _p64(off if n else np.zeros(1, np.uint64)), n,
                                  crc.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), _p8(ok))
     return crc[:n], ok[:n].astype(bool), int(bad)
+
+
+def crc32_fast(data, clmul: bool) -> int:
+    """The baseline's CRC-32 forms (slicing-by-8, or PCLMULQDQ folding), which
+    tests/test_oracle.py pins against crc32() and zlib."""
+    a = np.frombuffer(bytes(data), np.uint8) if not isinstance(data, np.ndarray) else data
+    a = np.ascontiguousarray(a, dtype=np.uint8)
+    buf = a if a.size else np.zeros(1, np.uint8)
+    fn = lib().nkvo_crc32_clmul if clmul else lib().nkvo_crc32_s8
+    return int(fn(_p8(buf), a.size))
+
+
+def verify_records(stream: np.ndarray, rec_off: np.ndarray, threads: int = 1, openssl: bool = False):
+    """The compaction read on the host (bench.py cpu_baseline of records_verify):
+    every record's Crc over Key ++ Value checked and its Value's leaf digest.
+    openssl: OpenSSL's SHA-1 and the PCLMULQDQ CRC, else the portable SHA-1 and
+    slicing-by-8.  Returns (n x 20 digests, number of failed Crcs)."""
+    stream = np.ascontiguousarray(stream, np.uint8)
+    off = np.ascontiguousarray(rec_off, np.uint64)
+    n = off.size
+    out = np.zeros((max(n, 1), 20), np.uint8)
+    fn = ctypes.cast(ossl().nkvo_ossl_sha1, ctypes.c_void_p) if openssl else None
+    bad = lib().nkvo_verify_records(_p8(stream), _p64(off if n else np.zeros(1, np.uint64)), n, _p8(out),
+                                    threads, fn, 1 if openssl else 0)
+    return out[:n], int(bad)
+
+
+def seal_records(stream: np.ndarray, rec_off: np.ndarray, threads: int = 1) -> None:
+    """Write each record's Crc (Key ++ Value, record.go:51) into `stream` in place."""
+    off = np.ascontiguousarray(rec_off, np.uint64)
+    assert stream.flags.c_contiguous and stream.dtype == np.uint8
+    if off.size:
+        lib().nkvo_seal_records(_p8(stream), _p64(off), off.size, threads)
 
 
 def murmur3_32(data, seed: int) -> int:

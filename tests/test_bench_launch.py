@@ -281,10 +281,12 @@ def test_merged_line_shape(monkeypatch, capsys):
                      (1, ("--leaves", str(8 << 20), "--tables", "1"))]
     assert line["capi_config4"]["n_gpus"] == 1
     # configs[2] and the records form of configs[1] as
-    # fresh-child sub-records, each with its own roofline and CPU baseline
-    assert subs == ["mixed", "records"]
+    # fresh-child sub-records, each with its own roofline and CPU baseline;
+    # the compaction read (every Crc checked) and
+    # the host-inclusive flush as well
+    assert subs == ["mixed", "records", "records_verify", "api_flush"]
     assert line["config2_mixed"]["value"] == 3.0 and line["config1_records"]["value"] == 4.0
-    for k in ("config2_mixed", "config1_records"):
+    for k in ("config2_mixed", "config1_records", "config1_records_verify", "api_flush"):
         assert line[k]["verified_vs_oracle"] is True and "roofline" in line[k] and "cpu_baseline" in line[k]
 
 

@@ -149,6 +149,51 @@ def test_record_crcs_on_serialized_stream(oracle):
     assert bad2 == 1 and not ok2[3] and ok2[[i for i in range(len(recs)) if i != 3]].all()
 
 
+def test_fast_crc_forms_match_zlib(oracle):
+    """The CPU baseline's CRC-32 forms (slicing-by-8; PCLMULQDQ folding, as Go's
+    hash/crc32 on amd64) against zlib and the bitwise checker, every length
+    around the folding loop's 16/64-byte steps and every start alignment."""
+    import zlib
+    rng = np.random.default_rng(13)
+    big = rng.integers(0, 256, 70000, dtype=np.uint8)
+    for n in list(range(0, 200)) + [255, 256, 257, 1023, 4066, 4096, 65536, 65599]:
+        for a in (0, 1, 7) if n < 200 else range(16):
+            d = big[a:a + n]
+            want = zlib.crc32(d.tobytes())
+            assert oracle.crc32_fast(d, clmul=False) == want
+            assert oracle.crc32_fast(d, clmul=True) == want
+    assert oracle.crc32_fast(b"123456789", clmul=True) == 0xCBF43926
+
+
+def test_verify_records_cpu_baseline(oracle):
+    """nkvo_seal_records / nkvo_verify_records (bench.py's records_verify CPU
+    baseline): the sealed Crcs are the bitwise checker's, the digests are the
+    leaf oracle's for every variant and thread count, and one flipped key byte
+    is counted once."""
+    rng = np.random.default_rng(14)
+    ks = rng.integers(0, 40, 300).astype(np.uint64)
+    vs = rng.integers(0, 5000, 300).astype(np.uint64)
+    sizes = 30 + ks + vs
+    off = np.zeros(300, np.uint64)
+    off[1:] = np.cumsum(sizes[:-1])
+    stream = rng.integers(0, 256, int(sizes.sum()), dtype=np.uint8)
+    for i in range(300):
+        o = int(off[i])
+        stream[o + 14:o + 22] = np.frombuffer(np.uint64(ks[i]).tobytes(), np.uint8)
+        stream[o + 22:o + 30] = np.frombuffer(np.uint64(vs[i]).tobytes(), np.uint8)
+    oracle.seal_records(stream, off, 3)
+    _, ok, bad = oracle.record_crcs(stream, off)
+    assert bad == 0 and ok.all()
+    want = oracle.leaf_hashes(stream, off + 30 + ks, vs)
+    for ossl in (False, True):
+        for t in (1, 4):
+            d, b = oracle.verify_records(stream, off, threads=t, openssl=ossl)
+            assert b == 0 and np.array_equal(d, want)
+    stream[int(off[7]) + 30 + 0] ^= 1 if ks[7] + vs[7] else 0
+    if ks[7] + vs[7]:
+        assert oracle.verify_records(stream, off, threads=2, openssl=True)[1] == 1
+
+
 # --- SSTable filter (SURVEY.md section 8f row 4): murmur3 Bloom inserts ---
 
 MURMUR3_VECTORS = [  # published MurmurHash3_x86_32 vectors (input, seed, hash)
