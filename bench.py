@@ -1272,7 +1272,7 @@ def main_small_flush(args):
     spec = [f"{n}:{lo}:{hi}:{SMALL_SEED:x}" for _, n, lo, hi in SMALL_SHAPES]
     gpu = {}
     with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
-        for mode in (1, 2, 0):
+        for mode in (1, 3, 2, 0):
             p = subprocess.run([exe, str(mode), str(args.small_reps), td] + spec, capture_output=True, text=True,
                                timeout=600)
             if p.returncode != 0:
@@ -1292,14 +1292,14 @@ def main_small_flush(args):
         best_cpu = min(cpu.values())
         row = {"shape": name, "n": n, "value_bytes": [lo, hi], "payload_bytes": int(lens.sum()), "cpu": cpu,
                "root": root}
-        for mode, key in ((1, "small_pinned"), (2, "small_hbm"), (0, "grid")):
+        for mode, key in ((1, "small_pinned"), (3, "small_resident"), (2, "small_hbm"), (0, "grid")):
             g = gpu[mode][k]
             ok = g["root"] == root
             verified = verified and ok
             row[key] = {"path": "small" if g["path"] == 1 else "grid", "mirror_us": g["mirror_us"],
                         "mirror_us_p10_p90": [g["mirror_us_p10"], g["mirror_us_p90"]], "file_us": g["file_us"],
                         "abi_us": g["abi_us"], "root_ok": ok}
-        best_gpu = min(row[m]["mirror_us"] for m in ("small_pinned", "small_hbm", "grid"))
+        best_gpu = min(row[m]["mirror_us"] for m in ("small_pinned", "small_resident", "small_hbm", "grid"))
         row["gpu_over_cpu_time"] = round(best_gpu / best_cpu, 2)
         shapes.append(row)
     # the smallest payload of the sweep at which the best GPU flush is at least as

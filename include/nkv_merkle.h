@@ -159,7 +159,13 @@ int nkv_ctx_sync(nkv_ctx *ctx);
                                  synchronize.  1 (default) = the kernel reads the packed values
                                  and writes its results across PCIe (host-coherent pinned
                                  buffers, no DMA); 2 = one copy to HBM, the launch, one copy
-                                 back; 0 = off (the grid path for every size) */
+                                 back; 3 = the resident service: one workgroup stays on the GPU
+                                 and serves each call from a host-coherent mailbox as path 1
+                                 does, without a launch or the runtime's completion (it leaves
+                                 20 ms after its last request, or at nkv_ctx_destroy, and the
+                                 next call starts it again; while it runs, a device-wide
+                                 synchronize waits for it to leave); 0 = off (the grid path
+                                 for every size) */
 #define NKV_OPT_SMALL_MAX_N 15     /* 0..1024 (default 1024) */
 #define NKV_OPT_SMALL_MAX_BYTES 16 /* payload bound of the small path (default 1 MiB; the values
                                       16-byte aligned; for records the whole stream) */

@@ -228,6 +228,71 @@ int grow_coherent(uint8_t** p, size_t* cap, size_t bytes) {
 // the call synchronizes once.  *taken = false: not eligible, nothing done.
 constexpr uint64_t kSmallMaxExtent = 0xFFFFFFF0ull;  // the kernel's 32-bit extent of in-place values
 constexpr int64_t kSmallSpinUs = 2000;  // host spin on the completion word before the runtime's wait
+constexpr uint64_t kSvcIdleUs = 20000;  // the resident service leaves after this long without a request
+constexpr int64_t kSvcTimeoutUs = 10000000;  // a request unanswered this long (service alive) is an error
+
+// One request to the resident service: the mailbox fields, then the doorbell
+// (release: x86 keeps the stores in order and the service reads them after its
+// system-scope acquire), then a spin on `done`.  Each 256 polls look at the
+// service stream: a service that has left is started again.
+int small_service_call(nkv_ctx* c, const uint64_t* d_desc, const uint8_t* d_vals, uint32_t vbytes, uint32_t n,
+                       uint8_t* d_out, uint32_t img_at, uint32_t seq) {
+    if (!c->h_mbox) {
+        uint8_t* p = nullptr;
+        size_t cap = 0;
+        TRY(grow_coherent(&p, &cap, sizeof(SmallMailbox)));
+        memset(p, 0, sizeof(SmallMailbox));
+        c->h_mbox = reinterpret_cast<SmallMailbox*>(p);
+    }
+    if (!c->svc) HIPTRY(hipStreamCreateWithFlags(&c->svc, hipStreamNonBlocking));
+    SmallMailbox* mb = c->h_mbox;
+    void* dmb = nullptr;
+    HIPTRY(hipHostGetDevicePointer(&dmb, mb, 0));
+    mb->n = n;
+    mb->vbytes = vbytes;
+    mb->img_at = img_at;
+    mb->desc = reinterpret_cast<uintptr_t>(d_desc);
+    mb->vals = reinterpret_cast<uintptr_t>(d_vals);
+    mb->out = reinterpret_cast<uintptr_t>(d_out);
+    __atomic_store_n(&mb->doorbell, seq, __ATOMIC_RELEASE);
+    if (!c->svc_live) {
+        HIPTRY(launch_small_service(static_cast<SmallMailbox*>(dmb), kSvcIdleUs * 100, c->svc));
+        c->svc_live = true;
+        ++c->svc_launches;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t k = 1;; ++k) {
+        if (__atomic_load_n(&mb->done, __ATOMIC_ACQUIRE) == seq) break;
+        if ((k & 255u) == 0u) {
+            const hipError_t q = hipStreamQuery(c->svc);
+            if (q == hipSuccess) {  // the service has left (idle): start it again, unless it answered
+                if (__atomic_load_n(&mb->done, __ATOMIC_ACQUIRE) == seq) break;
+                HIPTRY(launch_small_service(static_cast<SmallMailbox*>(dmb), kSvcIdleUs * 100, c->svc));
+                ++c->svc_launches;
+            } else if (q != hipErrorNotReady) {
+                return st_at(q, "k_small_service", __FILE__, __LINE__);
+            } else if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(kSvcTimeoutUs)) {
+                return NKV_ERR_DEVICE;
+            }
+        }
+        __builtin_ia32_pause();
+    }
+    return NKV_OK;
+}
+
+// Stop the resident service (nkv_ctx_destroy): the exit doorbell, then wait
+// for the kernel to leave.
+void svc_stop(nkv_ctx* c) {
+    if (c->svc_live && c->h_mbox) {
+        __atomic_store_n(&c->h_mbox->doorbell, kSvcExit, __ATOMIC_RELEASE);
+        (void)hipStreamSynchronize(c->svc);
+    }
+    c->svc_live = false;
+    if (c->svc) (void)hipStreamDestroy(c->svc);
+    c->svc = nullptr;
+    if (c->h_mbox) (void)hipHostFree(c->h_mbox);
+    c->h_mbox = nullptr;
+}
 int small_tree(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint64_t* len, uint64_t n,
                uint8_t* root20, uint8_t* nodes_out, uint8_t* img_out, bool* taken) {
     *taken = false;
@@ -249,7 +314,7 @@ int small_tree(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint6
     // mirrors' NewLeaf arena) are read where they lie: no pack, no copy
     // (only while their extent in the block, gaps included, stays within the
     // small bound: the kernel takes the extent as a 32-bit byte count)
-    bool in_place = blk && blk->coherent && c->small_path == 1 && (lo & 15) == 0 &&
+    bool in_place = blk && blk->coherent && c->small_path != 2 && (lo & 15) == 0 &&
                     align16(hi) - lo <= std::min<uint64_t>(c->small_max_bytes, kSmallMaxExtent);
     const uint64_t adj = blk ? uint64_t(base - blk->p) : 0;
     for (uint64_t i = 0; in_place && i < n; ++i) in_place = ((adj + off[i]) & 15) == 0;
@@ -280,9 +345,18 @@ int small_tree(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint6
     unsigned int* ticket = static_cast<unsigned int*>(c->d_small.p);
     volatile unsigned int* hdone = reinterpret_cast<volatile unsigned int*>(c->h_sout + out_bytes);
     uint32_t seq = ++c->small_seq;
-    if (seq == 0) seq = c->small_seq = 1;  // 0 is the word's cleared state
+    if (seq == 0 || seq == kSvcExit) seq = c->small_seq = 1;  // 0 is the word's cleared state
     *hdone = 0;
-    if (c->small_path == 2) {  // through HBM: one copy in, one launch, one copy out
+    if (c->small_path == 3) {  // the resident service: no launch, no runtime completion
+        void *din = nullptr, *dout = nullptr, *dblk = nullptr;
+        HIPTRY(hipHostGetDevicePointer(&din, c->h_sin, 0));
+        HIPTRY(hipHostGetDevicePointer(&dout, c->h_sout, 0));
+        if (in_place) HIPTRY(hipHostGetDevicePointer(&dblk, blk->p, 0));
+        const uint8_t* d_vals = in_place ? static_cast<const uint8_t*>(dblk) + lo
+                                         : static_cast<const uint8_t*>(din) + 16 * n;
+        TRY(small_service_call(c, static_cast<const uint64_t*>(din), d_vals, uint32_t(vext), uint32_t(n),
+                               static_cast<uint8_t*>(dout), uint32_t(img_at), seq));
+    } else if (c->small_path == 2) {  // through HBM: one copy in, one launch, one copy out
         TRY(grow(c->d_sin, in_bytes));
         TRY(grow(c->d_sout, out_bytes));
         HIPTRY(hipMemcpyAsync(c->d_sin.p, c->h_sin, in_bytes, hipMemcpyHostToDevice, c->stream));
@@ -635,6 +709,7 @@ void nkv_ctx_destroy(nkv_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->own) (void)hipStreamSynchronize(c->own);
+    svc_stop(c);  // the resident small-tree service leaves before anything it reads is freed
     if (c->clock_probe) (void)set_clock_probe(nullptr, c->own);  // kernels must not add into freed memory
     for (nkv_ctx* l : c->lanes) nkv_ctx_destroy(l);
     (void)hipSetDevice(c->device);
@@ -739,7 +814,7 @@ int nkv_ctx_set_option(nkv_ctx* c, int key, int64_t value) try {
             c->timing_calls = 0;
             return NKV_OK;
         case NKV_OPT_SMALL_PATH:
-            if (value < 0 || value > 2) return NKV_ERR_INVALID;
+            if (value < 0 || value > 3) return NKV_ERR_INVALID;
             c->small_path = int(value);
             return NKV_OK;
         case NKV_OPT_SMALL_MAX_N:

@@ -209,6 +209,13 @@ struct nkv_ctx {
     nkv::DevBuf d_sin, d_sout, d_small;
     int last_path = 0;  // NKV_PATH_* of the latest host-buffer tree call
     uint32_t small_seq = 0;  // the small-tree kernel's completion word (per call)
+    // NKV_OPT_SMALL_PATH 3: the resident service's mailbox and stream (created
+    // on first use; the kernel leaves after kSvcIdleUs without a request or at
+    // nkv_ctx_destroy)
+    nkv::SmallMailbox* h_mbox = nullptr;
+    hipStream_t svc = nullptr;
+    bool svc_live = false;   // a service launch was made and may still run
+    uint64_t svc_launches = 0;
 };
 
 namespace nkv {

@@ -173,6 +173,21 @@ constexpr uint32_t kSmallMaxN = 1024;
 hipError_t launch_small_tree(const uint64_t* desc, const uint8_t* vals, uint32_t vbytes, uint32_t n, uint8_t* out,
                              uint32_t img_at, uint8_t* scratch, unsigned int* ticket, unsigned int* done, uint32_t seq,
                              hipStream_t s);
+// The resident small-tree service (kernels.hip k_small_service,
+// NKV_OPT_SMALL_PATH 3): its mailbox lives in host-coherent pinned memory.
+// The host writes a request (the fields after `done`, as launch_small_tree's
+// arguments) and then its seq into `doorbell`; the service answers with seq
+// in `done` behind every output byte.
+struct alignas(64) SmallMailbox {
+    uint32_t doorbell;  // host: seq of the latest request; kSvcExit: leave
+    uint32_t served;    // service: the latest seq it served (a relaunch resumes from it)
+    uint32_t done;      // service: seq whose outputs are all written
+    uint32_t n, vbytes, img_at;
+    uint64_t desc, vals, out;  // device addresses of host-coherent memory
+};
+constexpr uint32_t kSvcExit = 0xFFFFFFFFu;
+constexpr uint32_t kSvcBlock = 1024;  // one workgroup: up to 1024 leaves, one lane each
+hipError_t launch_small_service(SmallMailbox* mb, uint64_t idle_ticks, hipStream_t s);
 // Clock probe of the leaf kernels on the current device (NKV_TIMING_CLOCK):
 // p = kClockWords u64 (8 slots of 32: shader-clock cycles, 100 MHz ticks, waves;
 // zeroed by the caller) or nullptr to switch it off.

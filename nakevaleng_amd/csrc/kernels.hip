@@ -2336,12 +2336,14 @@ __device__ __forceinline__ void sha1_value_aligned(const uint8_t* p, uint64_t le
     sha1_tail<true>(p, len, h);
 }
 
-// bytes [0, bytes) of LDS src to dst (16-byte aligned both), 16 per store
+// bytes [0, bytes) of LDS src to dst (16-byte aligned both), 16 per store;
+// B = the workgroup's threads
+template <uint32_t B>
 __device__ __forceinline__ void small_copy_out(const uint8_t* src, uint8_t* dst, uint32_t bytes) {
     const uint32_t whole = bytes & ~15u;
-    for (uint32_t b = 16 * threadIdx.x; b < whole; b += 16 * kSmallBlock)
+    for (uint32_t b = 16 * threadIdx.x; b < whole; b += 16 * B)
         *reinterpret_cast<uint4*>(dst + b) = *reinterpret_cast<const uint4*>(src + b);
-    for (uint32_t b = whole + threadIdx.x; b < bytes; b += kSmallBlock) dst[b] = src[b];
+    for (uint32_t b = whole + threadIdx.x; b < bytes; b += B) dst[b] = src[b];
 }
 
 __device__ __forceinline__ uint32_t small_count(uint32_t n, int L) { return L == 0 ? n : ((n - 1) >> L) + 1; }
@@ -2349,23 +2351,101 @@ __device__ __forceinline__ uint32_t small_count(uint32_t n, int L) { return L ==
 // bytes [0, bytes) of src (16-byte aligned, host or device memory) into LDS
 // dst: every thread's loads are issued before any store, so an input of up to
 // 16 KiB crosses PCIe in one round trip
+template <uint32_t B>
 __device__ __forceinline__ void small_stage_in(const uint8_t* src, uint8_t* dst, uint32_t bytes) {
     const uint4* s4 = reinterpret_cast<const uint4*>(src);
     uint4* d4 = reinterpret_cast<uint4*>(dst);
     const uint32_t nq = (bytes + 15u) >> 4;
-    for (uint32_t c0 = 0; c0 < nq; c0 += 4 * kSmallBlock) {
+    for (uint32_t c0 = 0; c0 < nq; c0 += 4 * B) {
         uint4 v[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const uint32_t c = c0 + threadIdx.x + k * kSmallBlock;
+            const uint32_t c = c0 + threadIdx.x + k * B;
             v[k] = c < nq ? s4[c] : make_uint4(0u, 0u, 0u, 0u);
         }
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const uint32_t c = c0 + threadIdx.x + k * kSmallBlock;
+            const uint32_t c = c0 + threadIdx.x + k * B;
             if (c < nq) d4[c] = v[k];
         }
     }
+}
+
+// Every level above the leaf digests in sm (at least one; a lone last node is
+// hashed alone, its sibling being the empty pad: merkletree.go:31-64), the
+// nodes stored level-major at out, then the Serialize image at out + img_at,
+// top level first: 0x00 + digest per node, one 0x01 after each odd level below
+// the top (merklenode.go:37-63, MERKLE_NODE_EMPTY :11), built kSmallSeg bytes
+// at a time in seg from whole node records clipped to the segment (as
+// k_bfs_image does).  Starts and ends at a workgroup barrier.
+template <uint32_t B>
+__device__ __forceinline__ void small_levels_and_image(uint8_t* sm, uint8_t* seg, uint32_t n, uint8_t* out,
+                                                       uint32_t img_at) {
+    const uint32_t tid = threadIdx.x;
+    __syncthreads();
+    uint32_t cnt = n, base = 0;
+    int lv = 1;
+    do {
+        const uint32_t pc = (cnt + 1) >> 1;
+        for (uint32_t j = tid; j < pc; j += B) {
+            const bool lone = 2 * j + 1 >= cnt;
+            uint32_t l[5], r[5] = {0u, 0u, 0u, 0u, 0u}, o[5];
+            load_digest(sm, base + 2 * j, l);
+            if (!lone) load_digest(sm, base + 2 * j + 1, r);
+            sha1_parent(l, r, lone, o);
+            store_digest(sm, base + cnt + j, o);
+        }
+        __syncthreads();
+        base += cnt;
+        cnt = pc;
+        ++lv;
+    } while (cnt > 1);
+    NKV_STAMP(3);
+    const uint32_t total = base + 1;
+    small_copy_out<B>(sm, out, 20u * total);
+    uint32_t img_len = 0;
+    for (int L = lv - 1; L >= 0; --L) {
+        const uint32_t c = small_count(n, L);
+        img_len += 21u * c + ((L < lv - 1 && (c & 1u)) ? 1u : 0u);
+    }
+    __syncthreads();  // seg may still hold the staged input
+    for (uint32_t s0 = 0; s0 < img_len; s0 += kSmallSeg) {
+        const uint32_t s1 = min(s0 + kSmallSeg, img_len);
+        uint32_t A = 0;  // image offset of level L's first record
+        for (int L = lv - 1; L >= 0; --L) {
+            const uint32_t c = small_count(n, L);
+            uint32_t ns = 0;  // node index of level L's first node
+            for (int j = 0; j < L; ++j) ns += small_count(n, j);
+            const uint32_t E = A + 21u * c;
+            const bool pad = L < lv - 1 && (c & 1u);
+            if (pad && E >= s0 && E < s1 && tid == 0) seg[E - s0] = NKV_MERKLE_NODE_EMPTY;
+            if (E > s0 && A < s1) {
+                const uint32_t k0 = s0 > A ? (s0 - A) / 21u : 0u;
+                const uint32_t k1 = (min(s1, E) - 1u - A) / 21u;  // last record with a byte in the segment
+                for (uint32_t k = k0 + tid; k <= k1; k += B) {
+                    const uint8_t* d = sm + 20u * (ns + k);
+                    const int32_t pos = int32_t(A + 21u * k) - int32_t(s0);
+#pragma unroll
+                    for (int b = 0; b < 21; ++b) {
+                        const int32_t q = pos + b;
+                        if (q >= 0 && q < int32_t(kSmallSeg)) seg[q] = b == 0 ? 0u : d[b - 1];
+                    }
+                }
+            }
+            A = E + (pad ? 1u : 0u);
+        }
+        __syncthreads();
+        small_copy_out<B>(seg, out + img_at + s0, s1 - s0);
+        __syncthreads();
+    }
+}
+
+// seq into the host-coherent completion word once every output byte of the
+// workgroup is written at system scope
+__device__ __forceinline__ void small_signal_done(unsigned int* done, uint32_t seq) {
+    __threadfence_system();  // each wave's output stores complete at system scope
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // vbytes: the extent of vals the values lie in.  A one-workgroup launch whose
@@ -2387,8 +2467,8 @@ __global__ __launch_bounds__(kSmallBlock) void k_small_tree(const uint64_t* __re
     const uint32_t i = blockIdx.x * kSmallBlock + tid;
     NKV_STAMP(0);
     if (gridDim.x == 1 && 16u * n + vbytes <= kSmallSeg) {
-        small_stage_in(reinterpret_cast<const uint8_t*>(desc), seg, 16u * n);
-        small_stage_in(vals, seg + 16u * n, vbytes);
+        small_stage_in<kSmallBlock>(reinterpret_cast<const uint8_t*>(desc), seg, 16u * n);
+        small_stage_in<kSmallBlock>(vals, seg + 16u * n, vbytes);
         __syncthreads();
         desc = reinterpret_cast<const uint64_t*>(seg);
         vals = seg + 16u * n;
@@ -2415,72 +2495,76 @@ __global__ __launch_bounds__(kSmallBlock) void k_small_tree(const uint64_t* __re
     } else if (i < n) {
         store_digest(sm, i, h);
     }
-    __syncthreads();
-    // every level above the leaves (at least one): a lone last node is hashed
-    // alone, its sibling being the empty pad (merkletree.go:32-34, :44-46)
-    uint32_t cnt = n, base = 0;
-    int lv = 1;
-    do {
-        const uint32_t pc = (cnt + 1) >> 1;
-        for (uint32_t j = tid; j < pc; j += kSmallBlock) {
-            const bool lone = 2 * j + 1 >= cnt;
-            uint32_t l[5], r[5] = {0u, 0u, 0u, 0u, 0u}, o[5];
-            load_digest(sm, base + 2 * j, l);
-            if (!lone) load_digest(sm, base + 2 * j + 1, r);
-            sha1_parent(l, r, lone, o);
-            store_digest(sm, base + cnt + j, o);
-        }
-        __syncthreads();
-        base += cnt;
-        cnt = pc;
-        ++lv;
-    } while (cnt > 1);
-    NKV_STAMP(3);
-    const uint32_t total = base + 1;
-    small_copy_out(sm, out, 20u * total);
-    // the image, top level first: 0x00 + digest per node, one 0x01 after each
-    // odd level below the top (merklenode.go:37-63, MERKLE_NODE_EMPTY :11),
-    // built kSmallSeg bytes at a time in LDS from whole node records clipped to
-    // the segment (as k_bfs_image does)
-    uint32_t img_len = 0;
-    for (int L = lv - 1; L >= 0; --L) {
-        const uint32_t c = small_count(n, L);
-        img_len += 21u * c + ((L < lv - 1 && (c & 1u)) ? 1u : 0u);
-    }
-    __syncthreads();  // seg may still hold the staged input
-    for (uint32_t s0 = 0; s0 < img_len; s0 += kSmallSeg) {
-        const uint32_t s1 = min(s0 + kSmallSeg, img_len);
-        uint32_t A = 0;  // image offset of level L's first record
-        for (int L = lv - 1; L >= 0; --L) {
-            const uint32_t c = small_count(n, L);
-            uint32_t ns = 0;  // node index of level L's first node
-            for (int j = 0; j < L; ++j) ns += small_count(n, j);
-            const uint32_t E = A + 21u * c;
-            const bool pad = L < lv - 1 && (c & 1u);
-            if (pad && E >= s0 && E < s1 && tid == 0) seg[E - s0] = NKV_MERKLE_NODE_EMPTY;
-            if (E > s0 && A < s1) {
-                const uint32_t k0 = s0 > A ? (s0 - A) / 21u : 0u;
-                const uint32_t k1 = (min(s1, E) - 1u - A) / 21u;  // last record with a byte in the segment
-                for (uint32_t k = k0 + tid; k <= k1; k += kSmallBlock) {
-                    const uint8_t* d = sm + 20u * (ns + k);
-                    const int32_t pos = int32_t(A + 21u * k) - int32_t(s0);
-#pragma unroll
-                    for (int b = 0; b < 21; ++b) {
-                        const int32_t q = pos + b;
-                        if (q >= 0 && q < int32_t(kSmallSeg)) seg[q] = b == 0 ? 0u : d[b - 1];
-                    }
+    small_levels_and_image<kSmallBlock>(sm, seg, n, out, img_at);
+    if (done) small_signal_done(done, seq);
+}
+
+// The resident small-tree service (NKV_OPT_SMALL_PATH 3): ONE workgroup of
+// kSvcBlock threads stays on the GPU between calls and serves one request at a
+// time from a host-coherent mailbox, so a default-size flush pays neither a
+// launch nor the runtime's completion path ("The
+// small-flush floor").  Thread 0 polls the doorbell across PCIe (relaxed
+// system-scope loads, s_sleep between polls); a new seq is acquired at system
+// scope, the request (the same descriptors, values and output layout
+// k_small_tree takes) is served exactly as k_small_tree serves a one-workgroup
+// launch -- leaves one lane each, every level and the image in LDS -- and seq
+// goes to mb->done behind every output byte.  Every wave leaves when the
+// doorbell reads kSvcExit (nkv_ctx_destroy) or after idle_ticks of the 100 MHz
+// real-time counter with no request (the host relaunches on its next call), so
+// the grid always drains.
+template <uint32_t B>
+__global__ __launch_bounds__(B) void k_small_service(SmallMailbox* __restrict__ mb, uint64_t idle_ticks) {
+    __shared__ __attribute__((aligned(16))) uint8_t sm[20 * (2 * kSmallMaxN - 1) + 12];
+    __shared__ __attribute__((aligned(16))) uint8_t seg[kSmallSeg];
+    __shared__ uint32_t cmd;
+    const uint32_t tid = threadIdx.x;
+    uint32_t served = __hip_atomic_load(&mb->served, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    while (true) {
+        if (tid == 0) {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            uint32_t bell;
+            while (true) {
+                bell = __hip_atomic_load(&mb->doorbell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (bell != served) break;
+                if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) {
+                    bell = kSvcExit;
+                    break;
                 }
+                __builtin_amdgcn_s_sleep(2);
             }
-            A = E + (pad ? 1u : 0u);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: the request's bytes
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            cmd = bell;
         }
         __syncthreads();
-        small_copy_out(seg, out + img_at + s0, s1 - s0);
-        __syncthreads();
-    }
-    if (done) {
-        __threadfence_system();  // each wave's output stores complete at system scope
-        __syncthreads();
-        if (tid == 0) __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        const uint32_t seq = cmd;
+        if (seq == kSvcExit) break;
+        const uint32_t n = __hip_atomic_load(&mb->n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const uint32_t vbytes = __hip_atomic_load(&mb->vbytes, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const uint32_t img_at = __hip_atomic_load(&mb->img_at, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const uint64_t* desc = reinterpret_cast<const uint64_t*>(
+            __hip_atomic_load(&mb->desc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+        const uint8_t* vals = reinterpret_cast<const uint8_t*>(
+            __hip_atomic_load(&mb->vals, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+        uint8_t* out = reinterpret_cast<uint8_t*>(__hip_atomic_load(&mb->out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+        if (n >= 1 && n <= kSmallMaxN) {  // the host never rings with another n; a bad one only signals
+            if (16u * n + vbytes <= kSmallSeg) {
+                small_stage_in<B>(reinterpret_cast<const uint8_t*>(desc), seg, 16u * n);
+                small_stage_in<B>(vals, seg + 16u * n, vbytes);
+                __syncthreads();
+                desc = reinterpret_cast<const uint64_t*>(seg);
+                vals = seg + 16u * n;
+            }
+            for (uint32_t i = tid; i < n; i += B) {
+                uint32_t h[5];
+                sha1_value_aligned(vals + desc[2 * i], desc[2 * i + 1], h);  // NewLeaf, merklenode.go:27-34
+                store_digest(sm, i, h);
+            }
+            small_levels_and_image<B>(sm, seg, n, out, img_at);
+        }
+        served = seq;
+        if (tid == 0) __hip_atomic_store(&mb->served, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        small_signal_done(&mb->done, seq);
     }
 }
 
@@ -2496,6 +2580,11 @@ hipError_t launch_small_tree(const uint64_t* desc, const uint8_t* vals, uint32_t
     const unsigned grid = unsigned((n + kSmallBlock - 1) / kSmallBlock);
     hipLaunchKernelGGL(k_small_tree, dim3(grid), dim3(kSmallBlock), 0, s, desc, vals, vbytes, n, out, img_at, scratch,
                        ticket, done, seq);
+    return hipGetLastError();
+}
+
+hipError_t launch_small_service(SmallMailbox* mb, uint64_t idle_ticks, hipStream_t s) {
+    hipLaunchKernelGGL(k_small_service<kSvcBlock>, dim3(1), dim3(kSvcBlock), 0, s, mb, idle_ticks);
     return hipGetLastError();
 }
 

@@ -60,7 +60,7 @@ def small_ctx(nkv):
     ctx.set_option(_lib.NKV_OPT_SMALL_MAX_BYTES, 1 << 20)
 
 
-@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("mode", [1, 2, 3])
 def test_small_path_every_n_1_to_1024(small_ctx, oracle, mode):
     """Every tree size n = 1..1024 (each odd level, each power of two and its
     neighbours), values at the padding-boundary lengths, bit-exact; the call
@@ -77,7 +77,7 @@ def test_small_path_every_n_1_to_1024(small_ctx, oracle, mode):
         assert img == img_w, n
 
 
-@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("mode", [1, 2, 3])
 def test_small_path_edge_lengths_and_alignment(small_ctx, oracle, mode):
     """Every edge length at every source alignment 0..15 (the path packs values
     16-byte aligned: the source alignment must not matter)."""
@@ -103,12 +103,12 @@ def test_small_path_matches_grid_path_and_bounds(small_ctx, oracle):
     for n in (1, 2, 3, 10, 40, 257, 1000, 1024):
         base, off, ln = _values(n, 1000 + n)
         out = {}
-        for mode in (0, 1, 2):
+        for mode in (0, 1, 2, 3):
             ctx.set_option(_lib.NKV_OPT_SMALL_PATH, mode)
             root, nodes, img, path = _run(_lib, ctx, base, off, ln)
             assert path == (_lib.NKV_PATH_GRID if mode == 0 else _lib.NKV_PATH_SMALL)
             out[mode] = (root.tobytes(), nodes.tobytes(), img)
-        assert out[0] == out[1] == out[2], n
+        assert out[0] == out[1] == out[2] == out[3], n
     ctx.set_option(_lib.NKV_OPT_SMALL_PATH, 1)
     base, off, ln = _values(1025, 3, maxlen=64)
     nodes_w, img_w = _want(oracle, base, off, ln)
@@ -254,3 +254,30 @@ def test_small_path_reads_the_arena_in_place(small_ctx, oracle, coherent):
     finally:
         _lib.check(L.nkv_host_free(ctx.h, p))
         ctx.set_option(_lib.NKV_OPT_ARENA_COHERENT, 1)
+
+
+def test_resident_service_across_idle_exits_and_contexts(nkv, oracle):
+    """NKV_OPT_SMALL_PATH 3 (the resident service): requests right after each
+    other, after the service has left on its idle timeout (20 ms) and been
+    started again, on a second context at the same time, and a context
+    destroyed while its service waits -- every tree bit-exact."""
+    import time
+    _lib, _ = nkv
+    ctxs = [_lib.Context(0), _lib.Context(0)]
+    try:
+        for c in ctxs:
+            c.set_option(_lib.NKV_OPT_SMALL_PATH, 3)
+        for k in range(60):
+            n = 1 + (k * 37) % 300
+            base, off, ln = _values(n, 5000 + k, maxlen=300)
+            nodes_w, img_w = _want(oracle, base, off, ln)
+            root, nodes, img, path = _run(_lib, ctxs[k % 2], base, off, ln)
+            assert path == _lib.NKV_PATH_SMALL
+            assert np.array_equal(nodes, nodes_w) and img == img_w, k
+            if k % 10 == 9:
+                time.sleep(0.05)  # past the idle timeout: the next call relaunches
+    finally:
+        t0 = time.perf_counter()
+        for c in ctxs:
+            c.close()
+        assert time.perf_counter() - t0 < 5.0

@@ -16,7 +16,8 @@
 //   abi_us      one nkv_tree_from_values call (root, nodes, image) on the values
 //               as they lie in the memtable: the C-ABI's own floor
 // with the context's NKV_OPT_SMALL_PATH set to MODE (0 = the grid path, 1 = the
-// one-launch kernel reading pinned host memory, 2 = the one launch through HBM).
+// one-launch kernel reading pinned host memory, 2 = the one launch through HBM,
+// 3 = the resident service: no launch per flush).
 //
 // Usage: small_flush MODE REPS DIR SHAPE...   SHAPE = N:MINLEN:MAXLEN[:SEED]
 // One JSON line per shape; roots in hex so the caller checks them against the
