@@ -29,6 +29,10 @@
 
 namespace nkv {
 
+#ifndef NKV_EXP_REC
+#define NKV_EXP_REC 0  // experiment builds only (tools/build_exp.sh -DNKV_EXP_REC=k)
+#endif
+
 #ifdef NKV_DIAG
 // Diagnostic build only (tools/diag_timeline.py): per-wave s_memtime /
 // s_memrealtime stamps, never part of an output.
@@ -793,6 +797,46 @@ __device__ __forceinline__ bool sha1_blocks_shift(uint8_t* wbuf, const uint8_t* 
             }
             asm volatile("" ::: "memory");  // the next line's loads stay after this compress
         };
+#if NKV_EXP_REC == 1
+        // experiment: four segment sets, each line issued one block before
+        // the block that first needs it (4 waves per SIMD)
+        uint32_t d[16];
+        line(0u, a, b);
+        if (nmax >= 2) line(2u, c, d);
+        for (uint32_t k = 0; k < nmax; k += 4) {
+            block(a, b);  // k, k + 1
+            if (k + 1 >= nmax) break;
+            block(b, c);  // k + 1, k + 2
+            if (k + 2 >= nmax) break;
+            if (k + 4 <= nmax) line(k + 4, a, b);
+            block(c, d);  // k + 2, k + 3
+            if (k + 3 >= nmax) break;
+            block(d, a);  // k + 3, k + 4
+            if (k + 4 >= nmax) break;
+            if (k + 6 <= nmax) line(k + 6, c, d);
+        }
+        return true;
+#elif NKV_EXP_REC == 2
+        // experiment: three segment sets, each 64-byte segment issued one block
+        // before the block that first needs it (the two halves of a line are
+        // requested one block apart)
+        auto segl = [&](uint32_t sg, uint32_t x[16]) {
+            if (live && sg <= nmax) load_seg(seg + 4 * sg, x);
+        };
+        segl(0u, a);
+        segl(1u, b);
+        for (uint32_t k = 0; k < nmax; k += 3) {
+            segl(k + 2, c);
+            block(a, b);  // k, k + 1
+            if (k + 1 >= nmax) break;
+            segl(k + 3, a);
+            block(b, c);  // k + 1, k + 2
+            if (k + 2 >= nmax) break;
+            segl(k + 4, b);
+            block(c, a);  // k + 2, k + 3
+        }
+        return true;
+#else
         line(0u, a, b);
         for (uint32_t k = 0; k < nmax; k += 4) {
             block(a, b);  // segments k, k + 1
@@ -806,6 +850,7 @@ __device__ __forceinline__ bool sha1_blocks_shift(uint8_t* wbuf, const uint8_t* 
             block(c, a);  // k + 3, k + 4
         }
         return true;
+#endif
     }
     if (wbuf && __all(!live || my_nfull == nmax)) {
         // Equal block counts: the segments go HBM -> LDS by LDS-DMA, one segment
@@ -2120,7 +2165,11 @@ __global__ __launch_bounds__(kBlock) void k_locate_fold(const uint32_t* __restri
 // which k_locate_fold turns into err and a range whose wide Gate opens the
 // sorted pass only when something was deferred.  A header outside the
 // stream flags bad and hashes the empty value (as k_locate).
+#if NKV_EXP_REC == 1
+constexpr int kRecordsWaves = 4;  // experiment: a fourth segment set
+#else
 constexpr int kRecordsWaves = 5;  // narrow waves of line-aligned records take whole lines: ~86 VGPRs
+#endif
 __global__ __launch_bounds__(kBlock, kRecordsWaves) void k_leaf_records(
     const uint8_t* __restrict__ stream, uint64_t stream_len, const uint64_t* __restrict__ rec_off, uint64_t n,
     int policy, uint64_t* __restrict__ voff, uint64_t* __restrict__ vlen, uint8_t* __restrict__ nodes,
