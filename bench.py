@@ -172,9 +172,6 @@ def parse(argv=None):
     ap.add_argument("--mixed-bytes", type=int, default=4 << 30, help="payload of the mixed config")
     ap.add_argument("--no-bucket", action="store_true", help="hash ragged values in input order (--bucket 0)")
     ap.add_argument("--bucket", type=int, default=-1, help="NKV_OPT_BUCKET override (0 input order, 1 sorted, 2 auto)")
-    ap.add_argument("--queue-pair", type=int, default=-1,
-                    help="NKV_OPT_QUEUE_PAIR override (0 = one wave per group; p = two-wave pairs for the groups "
-                         "within p %% of the longest chain)")
     ap.add_argument("--side-gate", type=int, default=-1,
                     help="NKV_OPT_SIDE_GATE override (1 = library default: the gated input-order kernel on a second "
                          "stream; 0 = on the context's stream)")
@@ -648,8 +645,6 @@ def set_options(args, _lib, ctx):
         ctx.set_option(_lib.NKV_OPT_TABLE_LANES, args.table_lanes)
     if args.side_gate >= 0:
         ctx.set_option(_lib.NKV_OPT_SIDE_GATE, args.side_gate)
-    if args.queue_pair >= 0:
-        ctx.set_option(_lib.NKV_OPT_QUEUE_PAIR, args.queue_pair)
 
 
 def workload_text(args, n, vlen, nbytes, world, T, rb=None, ks=None):

@@ -88,7 +88,8 @@ typedef struct nkv_ctx nkv_ctx;
  *   1: nkv_group_tree_dev takes d_roots as an array of g device pointers
  *      (void *const *; before: one device pointer), and the options
  *      NKV_OPT_DEEP_PREFETCH / NKV_OPT_QUEUE_RING accept only their one
- *      remaining value. */
+ *      remaining value (and, since round 6, NKV_OPT_QUEUE_PAIR only 0: the
+ *      opt-in pair kernel it selected never passed a GPU run). */
 #define NKV_ABI_VERSION 1
 int nkv_abi_version(void);
 
@@ -177,11 +178,9 @@ int nkv_ctx_sync(nkv_ctx *ctx);
                                 beside the length sort and the work queue (whichever of the two the
                                 device-side range opens does the work; the other exits), joined
                                 before the levels; 0 = all of them in turn on the context's stream */
-#define NKV_OPT_QUEUE_PAIR 19 /* work-queue kernel, batches bound by their longest chain: 0 (default) = one
-                                 wave per group; p = 1..100: two-wave workgroups, and the groups whose
-                                 first value has >= p % of the longest value's compressions are hashed
-                                 by a pair -- one wave expands the message schedule into LDS, the
-                                 other runs only the rounds (a shorter chain per block) */
+#define NKV_OPT_QUEUE_PAIR 19 /* retired (ABI version 1): 0 is the only value accepted (one wave per
+                                 work-queue group; the two-wave pair kernel of round 5 was removed
+                                 after failing its first GPU parity run) */
 int nkv_ctx_set_option(nkv_ctx *ctx, int key, int64_t value);
 /* Which path the latest host-buffer tree call of the context took */
 #define NKV_PATH_GRID 0  /* copies + leaf kernel + per-level reduce launches */

@@ -36,7 +36,7 @@ NKV_OPT_SMALL_MAX_N = 15
 NKV_OPT_SMALL_MAX_BYTES = 16
 NKV_OPT_ARENA_COHERENT = 17
 NKV_OPT_SIDE_GATE = 18
-NKV_OPT_QUEUE_PAIR = 19
+NKV_OPT_QUEUE_PAIR = 19  # retired: accepts only 0
 NKV_PATH_GRID = 0
 NKV_PATH_SMALL = 1
 NKV_OPT_DEEP_PREFETCH = 3  # retired: accepts only 3

@@ -561,7 +561,7 @@ int leaf_level(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint6
     int rc = st(sort_by_length_desc(len, n, perm, static_cast<uint32_t*>(c->d_keys.p), c->stream, wide, qi, cw));
     if (rc == NKV_OK)
         rc = st(launch_leaf_queue(base, off, len, perm, n, static_cast<uint32_t*>(c->d_queue.p), c->simds,
-                                  uint32_t(c->queue_waves), nodes, c->stream, wide, uint32_t(c->queue_pair)));
+                                  uint32_t(c->queue_waves), nodes, c->stream, wide));
     if (forked) {  // joined whatever happened above: nothing on the stream may pass it
         const int j = st(hipStreamWaitEvent(c->stream, c->side_ev[1], 0));
         if (rc == NKV_OK) rc = j;
@@ -829,10 +829,8 @@ int nkv_ctx_set_option(nkv_ctx* c, int key, int64_t value) try {
             if (value < 0 || value > 1) return NKV_ERR_INVALID;
             c->side_gate = int(value);
             return NKV_OK;
-        case NKV_OPT_QUEUE_PAIR:
-            if (value < 0 || value > 100) return NKV_ERR_INVALID;
-            c->queue_pair = int(value);
-            return NKV_OK;
+        case NKV_OPT_QUEUE_PAIR:  // retired: one wave per group (the pair kernel failed its GPU parity run)
+            return value == 0 ? NKV_OK : NKV_ERR_INVALID;
         case NKV_OPT_SMALL_MAX_BYTES:
             if (value < 0 || value > (int64_t(1) << 30)) return NKV_ERR_INVALID;
             c->small_max_bytes = uint64_t(value);

@@ -141,7 +141,6 @@ struct nkv_ctx {
     uint32_t simds = 1024;  // SIMDs on the device (CUs x 4)
     int queue_split = 32;   // NKV_OPT_QUEUE_SPLIT
     int queue_waves = 3;    // NKV_OPT_QUEUE_WAVES
-    int queue_pair = 0;     // NKV_OPT_QUEUE_PAIR
     int bloom_path = 2;     // NKV_OPT_BLOOM_PATH
     int crc_load = 0;       // NKV_OPT_CRC_LOAD
     int records_fused = 1;  // NKV_OPT_RECORDS_FUSED

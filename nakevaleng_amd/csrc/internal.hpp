@@ -83,7 +83,7 @@ struct QueueInit {
 // ring of value-relative chunks; waves_per_simd: 1..3.
 hipError_t launch_leaf_queue(const uint8_t* base, const uint64_t* off, const uint64_t* len, const uint32_t* perm,
                              uint64_t n, uint32_t* q, uint32_t simds, uint32_t waves_per_simd, uint8_t* nodes,
-                             hipStream_t s, Gate gate = Gate{}, uint32_t pair_pct = 0);
+                             hipStream_t s, Gate gate = Gate{});
 hipError_t launch_reduce(uint8_t* nodes, uint64_t n, int from_level, int top, hipStream_t s, Gate gate = Gate{});
 hipError_t launch_bfs_image(const uint8_t* nodes, const BfsLayout& lay, uint8_t* img,
                             hipStream_t s);

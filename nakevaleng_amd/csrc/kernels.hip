@@ -512,12 +512,8 @@ __device__ __forceinline__ void wait_vmcnt() {
 // b+1 .. b+R, and vmcnt(4 (R-1)) before reading window b+1 lets chunks
 // b+2 .. b+R fly (R-1 blocks of lookahead).
 // sink(b, w): block b's 16 big-endian words (clobbered), every lane, every
-// b < the wave's longest value (sha1_blocks_ring_vc compresses the lane's own;
-// k_leaf_queue_pair's schedule wave expands them for its partner)
-// kDrain: the window reads of block b + 1 complete before sink(b) runs (a sink
-// that issues LDS instructions and waits of its own must not find the ring's
-// asm ds_reads into nxt still in flight)
-template <int R, bool kDrain = false, class Sink>
+// b < the wave's longest value (sha1_blocks_ring_vc compresses the lane's own)
+template <int R, class Sink>
 __device__ __forceinline__ void ring_vc_blocks(uint8_t* wbuf, const uint8_t* p, uint32_t my_nfull, Sink&& sink) {
     static_assert(R >= 2 && R <= 4, "ring depth");
     const int lane = threadIdx.x & 63;
@@ -597,8 +593,6 @@ __device__ __forceinline__ void ring_vc_blocks(uint8_t* wbuf, const uint8_t* p, 
         issue(b + R);
         wait_vmcnt<4 * (R - 1)>();
         read_window(b + 1, nxt);
-        if constexpr (kDrain)
-            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(nxt[0]), "+v"(nxt[1]), "+v"(nxt[2]), "+v"(nxt[3]) : : "memory");
         uint4 c4[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) c4[q] = make_uint4(cur[q].x, cur[q].y, cur[q].z, cur[q].w);
@@ -1429,336 +1423,6 @@ __global__ __launch_bounds__(64, kQueueRing) void k_leaf_queue(const uint8_t* __
         d[7] = d_first;
     }
 #endif
-}
-
-// Pair mode of the work queue (NKV_OPT_QUEUE_PAIR, round 5).  A ragged batch
-// that is not throughput-bound ends on its longest group, whose 64 chains run
-// at one wave's issue rate: 613 VALU per block, ~4.65 cycles each.  208 of
-// those (the 64 schedule words, 3 VALU each, and the 16 byte swaps) do not
-// depend on the chain state.  Here a workgroup is two waves.  When wave 0 is
-// the first wave on its SIMD, the pair takes the batch's longest groups (those
-// whose first value has at least pct % of the longest value's compressions,
-// from their own ticket q[3]) together: wave 1 streams the group's bytes
-// through its LDS ring (ring_vc_blocks) and writes each block's 80 schedule
-// words, 16 at a time, into a 3-slot ring in wave 0's LDS; wave 0 runs only
-// the rounds (5 VALU each) from there.  Two LDS counters (chunks written,
-// chunks read) hand the slots over.  When no such group is left both waves
-// carry on as k_leaf_queue's independent waves; every group is claimed once
-// (claim flags), and the front tickets run on into [0, P) so a long group no
-// pair took is still hashed.
-constexpr uint32_t kPairSlots = 3;  // W ring: chunks of 16 words x 64 lanes, 4 KiB each
-constexpr uint32_t kPairRelease = 0xFFFFFFFFu;  // ctl[0]: no long group left, the waves part
-// Every wait on the partner wave is bounded: a wave polls an LDS counter at
-// most kPairSpin times (s_sleep 1 between polls, ~0.1-0.2 s in all), then
-// stops waiting for good and raises ctl[4]; the pair loop then ends for both
-// waves, so a protocol slip gives wrong digests (which the parity tests
-// catch), never a wave that spins until the process is killed.
-constexpr uint32_t kPairSpin = 1u << 21;
-
-__device__ __forceinline__ uint32_t lds_addr(const void* p) { return uint32_t(reinterpret_cast<uintptr_t>(p)); }
-
-// an LDS word written by the other wave (uniform address; the wait orders it
-// before the reads that depend on it)
-__device__ __forceinline__ uint32_t lds_peek(uint32_t addr) {
-    uint32_t v;
-    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(addr) : "memory");
-    return __builtin_amdgcn_readfirstlane(v);
-}
-// after every earlier LDS access of this wave has completed
-__device__ __forceinline__ void lds_poke(uint32_t addr, uint32_t v) {
-    asm volatile("s_waitcnt lgkmcnt(0)\n\tds_write_b32 %0, %1" : : "v"(addr), "v"(v) : "memory");
-}
-template <int OFF>
-__device__ __forceinline__ void ds_write_b128_off(uint32_t addr, u32x4 v) {
-    asm volatile("ds_write_b128 %0, %1 offset:%2" : : "v"(addr), "v"(v), "i"(OFF) : "memory");
-}
-
-// rounds 16 J .. 16 J + 15 from their 16 schedule words
-template <int J>
-__device__ __forceinline__ void sha1_rounds16(uint32_t s[5], const u32x4 w[4]) {
-    uint32_t a = s[0], b = s[1], c = s[2], d = s[3], e = s[4];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        constexpr int t0 = 16 * J;
-        const int t = t0 + i;
-        const uint32_t wt = w[i >> 2][i & 3];
-        uint32_t f, k;
-        if (t < 20) {
-            f = ch(b, c, d);
-            k = 0x5A827999u;
-        } else if (t < 40) {
-            f = xor3(b, c, d);
-            k = 0x6ED9EBA1u;
-        } else if (t < 60) {
-            f = maj(b, c, d);
-            k = 0x8F1BBCDCu;
-        } else {
-            f = xor3(b, c, d);
-            k = 0xCA62C1D6u;
-        }
-        const uint32_t ewk = add3k(e, wt, k);
-        const uint32_t tmp = add3(rotl(a, 5), f, ewk);
-        e = d;
-        d = c;
-        c = rotl(b, 30);
-        b = a;
-        a = tmp;
-    }
-    s[0] = a;
-    s[1] = b;
-    s[2] = c;
-    s[3] = d;
-    s[4] = e;
-}
-
-// wave 1 of a pair: the group's blocks from its own ring, 80 schedule words
-// per block into the W ring (ctl[1] = chunks written, ctl[2] = chunks read)
-__device__ __forceinline__ void pair_schedule(uint8_t* ring, uint8_t* wring, const uint32_t* ctl,
-                                              const uint8_t* p, uint32_t my_nfull) {
-    const uint32_t row = lds_addr(wring) + 64u * uint32_t(threadIdx.x & 63);
-    const uint32_t a_written = lds_addr(ctl + 1), a_read = lds_addr(ctl + 2), a_abort = lds_addr(ctl + 4);
-    uint32_t k = 0, read = 0;
-    bool dead = false;  // wave-uniform: gave up on the partner
-    auto put = [&](const uint32_t w[16]) {
-        if (dead) return;
-        for (uint32_t spin = 0; k >= read + kPairSlots; ++spin) {
-            if (spin == kPairSpin) {
-                dead = true;
-                lds_poke(a_abort, 1u);
-                return;
-            }
-            read = lds_peek(a_read);
-            if (k >= read + kPairSlots) __builtin_amdgcn_s_sleep(1);
-        }
-        const uint32_t s0 = row + 4096u * (k % kPairSlots);
-        ds_write_b128_off<0>(s0, u32x4{w[0], w[1], w[2], w[3]});
-        ds_write_b128_off<16>(s0, u32x4{w[4], w[5], w[6], w[7]});
-        ds_write_b128_off<32>(s0, u32x4{w[8], w[9], w[10], w[11]});
-        ds_write_b128_off<48>(s0, u32x4{w[12], w[13], w[14], w[15]});
-        lds_poke(a_written, ++k);
-    };
-    ring_vc_blocks<kQueueRing, true>(ring, p, my_nfull, [&](uint32_t, uint32_t w[16]) {
-        put(w);
-#pragma unroll
-        for (int j = 1; j < 5; ++j) {
-#pragma unroll
-            for (int i = 0; i < 16; ++i)
-                w[i] = rotl(xor3(w[(i + 13) & 15], w[(i + 8) & 15], w[(i + 2) & 15]) ^ w[i], 1);
-            put(w);
-        }
-    });
-}
-
-// wave 0 of a pair: the rounds of every block from the W ring, one chunk read
-// ahead; a lane keeps a block's result only while the block is its value's
-// wait until the partner has written chunk `next` (bounded: see kPairSpin)
-__device__ __forceinline__ void pair_wait_written(uint32_t next, uint32_t& written, bool& dead, uint32_t a_written,
-                                                  uint32_t a_abort) {
-    if (dead) return;
-    for (uint32_t spin = 0; written <= next; ++spin) {
-        if (spin == kPairSpin) {
-            dead = true;
-            lds_poke(a_abort, 1u);
-            return;
-        }
-        written = lds_peek(a_written);
-        if (written <= next) __builtin_amdgcn_s_sleep(1);
-    }
-}
-
-template <int J>
-__device__ __forceinline__ void pair_chunk(uint32_t s[5], u32x4 cur[4], u32x4 nxt[4], uint32_t next,
-                                           uint32_t total, uint32_t& written, bool& dead, uint32_t row,
-                                           uint32_t a_written, uint32_t a_read, uint32_t a_abort) {
-    const bool more = next < total;
-    if (more) {
-        pair_wait_written(next, written, dead, a_written, a_abort);
-        const uint32_t s0 = row + 4096u * (next % kPairSlots);
-        nxt[0] = ds_read_b128_off<0>(s0);
-        nxt[1] = ds_read_b128_off<16>(s0);
-        nxt[2] = ds_read_b128_off<32>(s0);
-        nxt[3] = ds_read_b128_off<48>(s0);
-    }
-    sha1_rounds16<J>(s, cur);
-    if (more) {
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(nxt[0]), "+v"(nxt[1]), "+v"(nxt[2]), "+v"(nxt[3]) : : "memory");
-        lds_poke(a_read, next + 1);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) cur[q] = nxt[q];
-    }
-}
-
-__device__ __forceinline__ void pair_rounds(uint8_t* wring, const uint32_t* ctl, uint32_t my_nfull,
-                                            uint32_t h[5]) {
-    const uint32_t nmax = wave_max_u32(my_nfull);
-    if (nmax == 0) return;
-    const uint32_t row = lds_addr(wring) + 64u * uint32_t(threadIdx.x & 63);
-    const uint32_t a_written = lds_addr(ctl + 1), a_read = lds_addr(ctl + 2), a_abort = lds_addr(ctl + 4);
-    const uint32_t total = 5u * nmax;
-    uint32_t written = 0;
-    bool dead = false;  // wave-uniform: gave up on the partner
-    u32x4 cur[4], nxt[4];
-    pair_wait_written(0u, written, dead, a_written, a_abort);
-    cur[0] = ds_read_b128_off<0>(row);
-    cur[1] = ds_read_b128_off<16>(row);
-    cur[2] = ds_read_b128_off<32>(row);
-    cur[3] = ds_read_b128_off<48>(row);
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(cur[0]), "+v"(cur[1]), "+v"(cur[2]), "+v"(cur[3]) : : "memory");
-    lds_poke(a_read, 1u);
-    for (uint32_t b = 0; b < nmax; ++b) {
-        uint32_t s[5] = {h[0], h[1], h[2], h[3], h[4]};
-        const uint32_t k = 5u * b;
-        pair_chunk<0>(s, cur, nxt, k + 1, total, written, dead, row, a_written, a_read, a_abort);
-        pair_chunk<1>(s, cur, nxt, k + 2, total, written, dead, row, a_written, a_read, a_abort);
-        pair_chunk<2>(s, cur, nxt, k + 3, total, written, dead, row, a_written, a_read, a_abort);
-        pair_chunk<3>(s, cur, nxt, k + 4, total, written, dead, row, a_written, a_read, a_abort);
-        pair_chunk<4>(s, cur, nxt, k + 5, total, written, dead, row, a_written, a_read, a_abort);
-        if (b < my_nfull) {
-#pragma unroll
-            for (int q = 0; q < 5; ++q) h[q] += s[q];
-        }
-    }
-}
-
-// front ticket t -> group: [P, ngroups) longest first, then [0, P) (groups the
-// pairs have not claimed yet)
-__device__ __forceinline__ uint32_t front_group(uint32_t t, uint32_t ngroups, uint32_t P) {
-    return t < ngroups - P ? P + t : t - (ngroups - P);
-}
-
-// One group's leaves, by one wave (k_leaf_queue's body)
-__device__ __forceinline__ void queue_group(uint8_t* ring, const uint8_t* base, const uint64_t* off,
-                                            const uint64_t* len, const uint32_t* perm, uint64_t n, uint32_t g,
-                                            uint8_t* nodes) {
-    const uint64_t i = uint64_t(g) * 64 + (threadIdx.x & 63);
-    const uint64_t leaf = i < n ? perm[i] : 0;
-    const uint64_t vo = i < n ? off[leaf] : kDone;
-    const bool live = vo != kDone;
-    const uint8_t* p = live ? base + vo : base;
-    const uint64_t ln = live ? len[leaf] : 0;
-    uint32_t h[5];
-    sha1_init(h);
-    sha1_blocks_ring_vc<kQueueRing>(ring, p, uint32_t(ln >> 6), h);
-    if (live) {
-        sha1_tail<false>(p, ln, h);
-        store_digest(nodes, leaf, h);
-    }
-}
-
-__global__ __launch_bounds__(128, kQueueRing) void k_leaf_queue_pair(const uint8_t* __restrict__ base,
-                                                             const uint64_t* __restrict__ off,
-                                                             const uint64_t* __restrict__ len,
-                                                             const uint32_t* __restrict__ perm, uint64_t n,
-                                                             uint32_t ngroups, uint32_t simds,
-                                                             uint32_t* __restrict__ q, uint32_t pct,
-                                                             uint8_t* __restrict__ nodes, Gate gate) {
-    __shared__ __attribute__((aligned(16))) uint8_t smem[2][4096 * kQueueRing];
-    // [0] the pair's group (kPairRelease: none), [1] chunks written, [2] read,
-    // [3] the workgroup's mode, [4] a wave gave up on its partner (kPairSpin)
-    __shared__ uint32_t ctl[5];
-    if (!gate.open()) return;
-    const ClockProbe clk;
-    const int wave = threadIdx.x >> 6;
-    const int lane = threadIdx.x & 63;
-    uint32_t hw, xcc;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    const uint32_t key = ((((xcc & 7) * 8 + ((hw >> 13) & 7)) * 2 + ((hw >> 12) & 1)) * 16 + ((hw >> 8) & 15)) * 4 +
-                         ((hw >> 4) & 3);
-    uint32_t slot = 0;
-    if (lane == 0) slot = atomicAdd(q + kQueueHeader + key, 1u);
-    slot = __builtin_amdgcn_readfirstlane(slot);
-    const bool front = slot == 0;
-    const uint64_t work = reinterpret_cast<const unsigned long long*>(q)[2];
-    const uint64_t longest = compressions(len[perm[0]]);
-    const bool chain_bound = work < 2ull * simds * longest;
-    const uint32_t first_short = __builtin_amdgcn_readfirstlane(chain_bound ? min(q[2], ngroups) : 0u);
-    uint32_t* claimed = q + kQueueHeader + kSimdKeys;
-    // P: the groups whose first value has >= pct % of the longest compressions
-    // (the sort is by compressions, descending: a binary search on the first values)
-    uint32_t P = 0;
-    if (chain_bound && pct) {
-        const uint64_t thr = (longest * pct + 99) / 100;
-        uint32_t lo = 0, hi = ngroups;
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (compressions(len[perm[uint64_t(mid) * 64]]) >= thr) lo = mid + 1;
-            else hi = mid;
-        }
-        P = __builtin_amdgcn_readfirstlane(min(lo, first_short));
-    }
-    // wave 0's election decides the workgroup's mode
-    if (threadIdx.x == 0) {
-        ctl[3] = front && P ? 1u : 0u;
-        ctl[4] = 0u;
-    }
-    __syncthreads();
-    const bool pair = ctl[3] != 0u;
-    if (pair) {
-        __builtin_amdgcn_s_setprio(3);
-        while (true) {
-            if (threadIdx.x == 0) {
-                uint32_t g = kPairRelease;
-                while (true) {
-                    const uint32_t t = atomicAdd(q + 3, 1u);
-                    if (t >= P) break;
-                    if (atomicExch(claimed + t, 1u) == 0u) {
-                        g = t;
-                        break;
-                    }
-                }
-                ctl[0] = g;
-                ctl[1] = 0u;
-                ctl[2] = 0u;
-            }
-            __syncthreads();
-            const uint32_t g = __builtin_amdgcn_readfirstlane(ctl[0]);
-            if (g == kPairRelease) break;
-            const uint64_t i = uint64_t(g) * 64 + lane;
-            const uint64_t leaf = i < n ? perm[i] : 0;
-            const uint64_t vo = i < n ? off[leaf] : kDone;
-            const bool live = vo != kDone;
-            const uint8_t* p = live ? base + vo : base;
-            const uint64_t ln = live ? len[leaf] : 0;
-            if (wave == 1) {
-                pair_schedule(smem[1], smem[0], ctl, p, uint32_t(ln >> 6));
-            } else {
-                uint32_t h[5];
-                sha1_init(h);
-                pair_rounds(smem[0], ctl, uint32_t(ln >> 6), h);
-                if (live) {
-                    sha1_tail<false>(p, ln, h);
-                    store_digest(nodes, leaf, h);
-                }
-            }
-            __syncthreads();  // both waves are done with the rings and the counters
-            if (__builtin_amdgcn_readfirstlane(ctl[4]) != 0u) break;  // no more pairs after a give-up
-        }
-        if (!front) __builtin_amdgcn_s_setprio(0);
-    } else if (front) {
-        __builtin_amdgcn_s_setprio(3);
-    }
-    // k_leaf_queue's loop, each wave on its own ring
-    while (true) {
-        uint32_t g = 0xFFFFFFFFu;
-        bool stop = false;
-        if (lane == 0) {
-            const uint32_t t = atomicAdd(q + (front ? 0 : 1), 1u);
-            if (t >= ngroups) {
-                stop = true;
-            } else {
-                const uint32_t c = front ? front_group(t, ngroups, P) : ngroups - 1 - t;
-                if (!front && c < first_short) stop = true;
-                else if (atomicExch(claimed + c, 1u) == 0u) g = c;
-            }
-        }
-        stop = __builtin_amdgcn_readfirstlane(stop ? 1u : 0u) != 0u;
-        if (stop) break;
-        g = __builtin_amdgcn_readfirstlane(g);
-        if (g == 0xFFFFFFFFu) continue;  // met the other end: later tickets may still find [0, P)
-        queue_group(smem[wave], base, off, len, perm, n, g, nodes);
-    }
-    clk.end();
 }
 
 // K2: a B-node slab of level j0 (already in nodes) reduced up to
@@ -2685,15 +2349,11 @@ hipError_t launch_leaf_verify(const uint8_t* stream, uint64_t stream_len, const 
 
 hipError_t launch_leaf_queue(const uint8_t* base, const uint64_t* off, const uint64_t* len, const uint32_t* perm,
                              uint64_t n, uint32_t* q, uint32_t simds, uint32_t waves_per_simd, uint8_t* nodes,
-                             hipStream_t s, Gate gate, uint32_t pair_pct) {
+                             hipStream_t s, Gate gate) {
     const uint32_t ngroups = uint32_t((n + 63) / 64);
     const uint32_t waves = simds * std::min<uint32_t>(std::max<uint32_t>(waves_per_simd, 1u), uint32_t(kQueueRing));
-    if (pair_pct)
-        hipLaunchKernelGGL(k_leaf_queue_pair, dim3((waves + 1) / 2), dim3(128), 0, s, base, off, len, perm, n, ngroups,
-                           simds, q, pair_pct, nodes, gate);
-    else
-        hipLaunchKernelGGL(k_leaf_queue, dim3(waves), dim3(64), 0, s, base, off, len, perm, n, ngroups, simds, q,
-                           nodes, gate);
+    hipLaunchKernelGGL(k_leaf_queue, dim3(waves), dim3(64), 0, s, base, off, len, perm, n, ngroups, simds, q, nodes,
+                       gate);
     return hipGetLastError();
 }
 

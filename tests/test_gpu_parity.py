@@ -451,54 +451,6 @@ def test_side_gate_alternating(nkv, oracle, side_gate):
         assert np.array_equal(got.cpu().numpy().reshape(-1, 20), want)
 
 
-@pytest.mark.skipif(os.environ.get("NKV_TEST_QUEUE_PAIR") != "1",
-                    reason="pair mode (NKV_OPT_QUEUE_PAIR, off by default) has not run on a GPU yet: "
-                           "set NKV_TEST_QUEUE_PAIR=1 (tools/r05_fifth.sh does)")
-@pytest.mark.parametrize("pct", [0, 1, 50, 90, 100])
-@pytest.mark.parametrize("shape", ["one_long", "log_uniform", "throughput"])
-def test_queue_pair(nkv, oracle, pct, shape):
-    """NKV_OPT_QUEUE_PAIR: the longest groups of a chain-bound batch hashed by
-    two-wave pairs (schedule wave + rounds wave), the rest by single waves.
-    one_long: a 256 KiB value among short ones (a single pair group);
-    log_uniform: configs[2]'s shape at 1/40 scale (many pair groups, ragged
-    lanes, values of no full block); throughput: a batch whose work keeps
-    every SIMD busy (no pairs whatever pct says).  Unaligned offsets; every
-    setting gives the oracle's tree."""
-    torch = _torch()
-    _lib, _ = nkv
-    ctx = _lib.Context(0)
-    _bind(torch, ctx)
-    ctx.set_option(_lib.NKV_OPT_BUCKET, 1)
-    ctx.set_option(_lib.NKV_OPT_QUEUE_PAIR, pct)
-    L = _lib.lib()
-    rng = np.random.default_rng(1000 + pct + len(shape))
-    if shape == "one_long":
-        lens = rng.integers(0, 3000, 3000).astype(np.uint64)
-        lens[1234] = 256 * 1024 + 17
-    elif shape == "log_uniform":
-        lens = np.exp(rng.uniform(np.log(64), np.log(65536), 12000)).astype(np.uint64)
-        lens[::97] = rng.integers(0, 64, len(lens[::97]))
-    else:
-        lens = rng.integers(3000, 5000, 40000).astype(np.uint64)
-    n = len(lens)
-    off = np.zeros(n, np.uint64)
-    off[1:] = np.cumsum(lens[:-1] + 5)
-    data = oracle.splitmix64_bytes(int(off[-1] + lens[-1]) + 64, SEED + pct)
-    d_data, d_off, d_len = _dev(torch, data), _dev(torch, off), _dev(torch, lens)
-    d_nodes = torch.zeros(L.nkv_total_nodes(n) * 20, dtype=torch.uint8, device="cuda")
-    try:
-        for _ in range(2):  # the second call reuses the queue state
-            d_nodes.zero_()
-            _lib.check(L.nkv_tree_from_values_dev(ctx.h, d_data.data_ptr(), d_off.data_ptr(), d_len.data_ptr(),
-                                                  n, d_nodes.data_ptr()))
-            torch.cuda.synchronize()
-            got = d_nodes.cpu().numpy().reshape(-1, 20)
-            want = oracle.tree_from_digests(oracle.leaf_hashes(data, off, lens, threads=8))
-            assert np.array_equal(got, want)
-    finally:
-        ctx.close()
-
-
 @pytest.mark.parametrize("load", [4, 11])
 @pytest.mark.parametrize("shift", [0, 1, 2, 15, 16, 17, 46, 48, 63])
 @pytest.mark.parametrize("n,vlen,rec", [(1, 4050, 4096), (63, 4050, 4096), (3001, 4050, 4096), (777, 327, 400),

@@ -596,6 +596,11 @@ def test_pruned_variants_are_refused(nkv):
         for v in (0, 1, 4, 12, 14):
             assert L.nkv_ctx_set_option(ctx.h, key, v) == _lib.NKV_ERR_INVALID
         assert L.nkv_ctx_set_option(ctx.h, key, only) == _lib.NKV_OK
+    # round 6: the pair kernel NKV_OPT_QUEUE_PAIR selected is gone (it failed
+    # its first GPU parity run); the key accepts only 0
+    for v in (1, 50, 80, 100, -1):
+        assert L.nkv_ctx_set_option(ctx.h, _lib.NKV_OPT_QUEUE_PAIR, v) == _lib.NKV_ERR_INVALID
+    assert L.nkv_ctx_set_option(ctx.h, _lib.NKV_OPT_QUEUE_PAIR, 0) == _lib.NKV_OK
     for v in (0, 4, 5):
         assert L.nkv_ctx_set_option(ctx.h, _lib.NKV_OPT_QUEUE_WAVES, v) == _lib.NKV_ERR_INVALID
     assert L.nkv_ctx_set_option(ctx.h, _lib.NKV_OPT_QUEUE_WAVES, 3) == _lib.NKV_OK

@@ -1,9 +1,10 @@
 #!/bin/bash
-# Round 6, first GPU call:
-#   1. pair mode's gated parity tests (NKV_TEST_QUEUE_PAIR=1), bounded spins;
-#   1b. the small path's parity tests (modes 1-3: mode 3 = the resident service) and small_flush;
-#   2. the lone-wave split-schedule probe;
-#   3. configs[2] with pairs at 0 / 50 / 80 %, alternating x3, every root verified;
+# Round 6, first GPU call (the run of round 5's
+# pair-mode tests failed its first parity case, so pair mode was removed):
+#   1. the side-stream gate and bucket-mode parity tests;
+#   2. the small path's parity tests (modes 1-3: mode 3 = the resident service) and small_flush;
+#   3. the default line as the driver runs it (every sub-record, api_flush and
+#      config1_records_verify included);
 #   4. rocprofv3 --kernel-trace --stats of the default line and of each
 #      sub-config's command (mixed, records, records_verify);
 #   5. the mixed leaf phase's PMC traffic passes (tools/pmc_config.sh mixed).
@@ -12,9 +13,9 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 O=gpurun_out/r06a
 mkdir -p $O
-NKV_TEST_QUEUE_PAIR=1 timeout -k 10 420 python3 -u -m pytest tests/test_gpu_parity.py -k "side_gate or queue_pair or bucket_modes" \
-    -x -v --timeout 120 --timeout-method thread > $O/pair_tests.txt 2>&1 || { tail -40 $O/pair_tests.txt; exit 1; }
-tail -3 $O/pair_tests.txt
+timeout -k 10 420 python3 -u -m pytest tests/test_gpu_parity.py -k "side_gate or bucket_modes" \
+    -x -v --timeout 120 --timeout-method thread > $O/gate_tests.txt 2>&1 || { tail -40 $O/gate_tests.txt; exit 1; }
+tail -2 $O/gate_tests.txt
 timeout -k 10 400 python3 -u -m pytest tests/test_gpu_small.py -x -v --timeout 120 --timeout-method thread \
     > $O/small_tests.txt 2>&1 || { tail -40 $O/small_tests.txt; exit 1; }
 tail -3 $O/small_tests.txt
@@ -28,15 +29,15 @@ for r in d['shapes']:
     print(r['shape'], r['payload_bytes'], {k: r[k]['mirror_us'] for k in ('small_pinned','small_resident','small_hbm','grid')},
           {k: r[k]['abi_us'] for k in ('small_pinned','small_resident')}, r['cpu'])
 " $O/small_flush.json
-NKV_LONE_SPLIT=1 timeout -k 10 120 ./tools/lone_wave.bin > $O/lone_split.txt 2>&1 || { cat $O/lone_split.txt; exit 1; }
-cat $O/lone_split.txt
-for rep in 1 2 3; do
-  for qp in 0 50 80; do
-    timeout -k 10 180 python3 bench.py --config mixed --steps 40 --warmup 5 --no-capi --no-subconfigs --no-cpu-baseline \
-        --queue-pair $qp > $O/mixed_qp${qp}_${rep}.json 2> $O/mixed_qp${qp}_${rep}.err || { tail -5 $O/mixed_qp${qp}_${rep}.err; exit 1; }
-    echo "queue_pair=$qp rep=$rep $(python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(d['value'], d['ms_per_step'], d['sclk_mhz'], d['kernel_ms'], d['verified_vs_oracle'])" $O/mixed_qp${qp}_${rep}.json)"
-  done
-done
+timeout -k 10 600 python3 bench.py --steps 20 --warmup 5 > $O/default_line.json 2> $O/default_line.err \
+    || { tail -5 $O/default_line.err; exit 1; }
+python3 -c "
+import json,sys
+d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+print('default', d['value'], d['sclk_mhz'], d['roofline']['frac'], d['verified_vs_oracle'], d['cpu_baseline']['value'], d['cpu_baseline']['impl'])
+for k in ('capi_group','capi_one_tree','capi_config4','config2_mixed','config1_records','config1_records_verify','api_flush'):
+    v=d.get(k,{}); print(k, v.get('value'), v.get('verified_vs_oracle'), v.get('error'), (v.get('cpu_baseline') or {}).get('value'), v.get('wall_s'))
+" $O/default_line.json
 for cfg in sstable4k mixed records records_verify; do
   ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
       -d "$GRAFT_REPO_ROOT/$O/prof_$cfg" -o $cfg -- python3 "$GRAFT_REPO_ROOT/bench.py" --config $cfg --steps 20 --warmup 5 \

@@ -6,8 +6,7 @@
 #      block ahead, 4 waves/SIMD; rec2 -DNKV_EXP_REC=2: three sets, each 64-B
 #      segment one block ahead, 5 waves/SIMD), alternating x3, roots verified;
 #   3. SQ counters of k_leaf<0,4> (cfg2) and k_leaf_records: VALU issue, waits;
-#   4. PMC traffic of records and records_verify on this build;
-#   5. the default line as the driver runs it (every sub-record).
+#   4. PMC traffic of records and records_verify on this build.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
 export HSA_ENABLE_IPC_MODE_LEGACY=0 TMPDIR=/tmp
@@ -48,13 +47,4 @@ for cfg in sstable4k records; do
 done
 bash tools/pmc_config.sh records --config records || { echo "pmc records failed"; exit 1; }
 bash tools/pmc_config.sh records_verify --config records_verify || { echo "pmc records_verify failed"; exit 1; }
-timeout -k 10 600 python3 bench.py --steps 20 --warmup 5 > $O/default_line.json 2> $O/default_line.err \
-    || { tail -5 $O/default_line.err; exit 1; }
-python3 -c "
-import json,sys
-d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
-print('default', d['value'], d['sclk_mhz'], d['roofline']['frac'], d['verified_vs_oracle'])
-for k in ('capi_group','capi_one_tree','capi_config4','config2_mixed','config1_records','config1_records_verify','api_flush'):
-    v=d.get(k,{}); print(k, v.get('value'), v.get('verified_vs_oracle'), v.get('error'), (v.get('cpu_baseline') or {}).get('value'), v.get('wall_s'))
-" $O/default_line.json
 echo all done
