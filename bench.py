@@ -157,6 +157,9 @@ def parse(argv=None):
                          "small_flush = microseconds per flush at the reference's default sizes (10 values "
                          "<= 200 B) up to configs[0], GPU paths beside one host core (tools/small_flush.cpp)")
     ap.add_argument("--small-reps", type=int, default=300, help="small_flush: flushes per shape and mode")
+    ap.add_argument("--small-modes", default="1,3,2,0",
+                    help="small_flush: NKV_OPT_SMALL_PATH modes to time (1 one launch over pinned memory, 3 the "
+                         "resident service, 2 one launch through HBM, 0 the grid path)")
     ap.add_argument("--api-cycles", type=int, default=4, help="api_flush: flushes per mode (the first allocates "
                                                               "the pinned arena)")
     ap.add_argument("--tables", type=int, default=0,
@@ -1215,6 +1218,7 @@ def main_api_flush(args):
     print(json.dumps(out), flush=True)
 
 
+SMALL_MODE_KEYS = ((1, "small_pinned"), (3, "small_resident"), (2, "small_hbm"), (0, "grid"))
 # --config small_flush: (name, n, min value length, max value length); lengths
 # uniform in [min, max], seed SMALL_SEED (tools/small_flush.cpp's generator)
 SMALL_SEED = 0x6E616B67
@@ -1267,7 +1271,8 @@ def main_small_flush(args):
     spec = [f"{n}:{lo}:{hi}:{SMALL_SEED:x}" for _, n, lo, hi in SMALL_SHAPES]
     gpu = {}
     with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
-        for mode in (1, 3, 2, 0):
+        modes = [int(m) for m in args.small_modes.split(",") if m.strip()]
+        for mode in modes:
             p = subprocess.run([exe, str(mode), str(args.small_reps), td] + spec, capture_output=True, text=True,
                                timeout=600)
             if p.returncode != 0:
@@ -1287,14 +1292,16 @@ def main_small_flush(args):
         best_cpu = min(cpu.values())
         row = {"shape": name, "n": n, "value_bytes": [lo, hi], "payload_bytes": int(lens.sum()), "cpu": cpu,
                "root": root}
-        for mode, key in ((1, "small_pinned"), (3, "small_resident"), (2, "small_hbm"), (0, "grid")):
+        for mode, key in SMALL_MODE_KEYS:
+            if mode not in gpu:
+                continue
             g = gpu[mode][k]
             ok = g["root"] == root
             verified = verified and ok
             row[key] = {"path": "small" if g["path"] == 1 else "grid", "mirror_us": g["mirror_us"],
                         "mirror_us_p10_p90": [g["mirror_us_p10"], g["mirror_us_p90"]], "file_us": g["file_us"],
                         "abi_us": g["abi_us"], "root_ok": ok}
-        best_gpu = min(row[m]["mirror_us"] for m in ("small_pinned", "small_resident", "small_hbm", "grid"))
+        best_gpu = min(row[key]["mirror_us"] for mode, key in SMALL_MODE_KEYS if key in row)
         row["gpu_over_cpu_time"] = round(best_gpu / best_cpu, 2)
         shapes.append(row)
     # the smallest payload of the sweep at which the best GPU flush is at least as

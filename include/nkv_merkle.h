@@ -186,6 +186,12 @@ int nkv_ctx_set_option(nkv_ctx *ctx, int key, int64_t value);
 #define NKV_PATH_GRID 0  /* copies + leaf kernel + per-level reduce launches */
 #define NKV_PATH_SMALL 1 /* the one-launch small tree (NKV_OPT_SMALL_PATH) */
 int nkv_ctx_last_path(nkv_ctx *ctx, int *path);
+/* The resident small-tree service of the context (NKV_OPT_SMALL_PATH 3), for
+ * diagnostics: out[0] doorbell (latest request), out[1] served (the latest the
+ * service took), out[2] done (the latest it answered), out[3] launches so far,
+ * out[4] 1 while a launch may still run, out[5] 1 if its stream still has work.
+ * All zero before the first request. */
+int nkv_ctx_small_service_state(nkv_ctx *ctx, uint64_t out[6]);
 /* Timing (nkv_ctx_set_timing flags).  NKV_TIMING_EVENTS: the tree calls record
  * HIP events around the leaf kernel and the tree reduce on the context's
  * stream (and, for nkv_tree_from_values, around the upload and the download).

@@ -87,6 +87,7 @@ SIGNATURES = {
     "nkv_ctx_use_own_stream": (_int, [_vp]),
     "nkv_ctx_sync": (_int, [_vp]),
     "nkv_ctx_last_path": (_int, [_vp, ctypes.POINTER(_int)]),
+    "nkv_ctx_small_service_state": (_int, [_vp, ctypes.POINTER(ctypes.c_uint64)]),
     "nkv_ctx_set_option": (_int, [_vp, _int, ctypes.c_int64]),
     "nkv_ctx_set_timing": (_int, [_vp, _int]),
     "nkv_ctx_last_timing": (_int, [_vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
@@ -287,6 +288,12 @@ class Context:
         p = _int()
         check(lib().nkv_ctx_last_path(self.h, ctypes.byref(p)))
         return p.value
+
+    def small_service_state(self) -> dict:
+        """The resident small-tree service's mailbox and launch state (diagnostics)."""
+        a = (ctypes.c_uint64 * 6)()
+        check(lib().nkv_ctx_small_service_state(self.h, a))
+        return dict(zip(("doorbell", "served", "done", "launches", "live", "busy"), list(a)))
 
     def set_timing(self, on, clock: bool = False) -> None:
         """Events around the leaf kernel / reduce (on) and the leaf kernels' clock probe (clock)."""

@@ -228,7 +228,8 @@ int grow_coherent(uint8_t** p, size_t* cap, size_t bytes) {
 // the call synchronizes once.  *taken = false: not eligible, nothing done.
 constexpr uint64_t kSmallMaxExtent = 0xFFFFFFF0ull;  // the kernel's 32-bit extent of in-place values
 constexpr int64_t kSmallSpinUs = 2000;  // host spin on the completion word before the runtime's wait
-constexpr uint64_t kSvcIdleUs = 20000;  // the resident service leaves after this long without a request
+constexpr uint64_t kSvcIdleUs = 20000;   // the resident service leaves after this long without a request
+constexpr uint64_t kSvcLifeUs = 200000;  // ... or, between requests, once it has run this long
 constexpr int64_t kSvcTimeoutUs = 10000000;  // a request unanswered this long (service alive) is an error
 
 // One request to the resident service: the mailbox fields, then the doorbell
@@ -256,7 +257,7 @@ int small_service_call(nkv_ctx* c, const uint64_t* d_desc, const uint8_t* d_vals
     mb->out = reinterpret_cast<uintptr_t>(d_out);
     __atomic_store_n(&mb->doorbell, seq, __ATOMIC_RELEASE);
     if (!c->svc_live) {
-        HIPTRY(launch_small_service(static_cast<SmallMailbox*>(dmb), kSvcIdleUs * 100, c->svc));
+        HIPTRY(launch_small_service(static_cast<SmallMailbox*>(dmb), kSvcIdleUs * 100, kSvcLifeUs * 100, c->svc));
         c->svc_live = true;
         ++c->svc_launches;
     }
@@ -267,7 +268,7 @@ int small_service_call(nkv_ctx* c, const uint64_t* d_desc, const uint8_t* d_vals
             const hipError_t q = hipStreamQuery(c->svc);
             if (q == hipSuccess) {  // the service has left (idle): start it again, unless it answered
                 if (__atomic_load_n(&mb->done, __ATOMIC_ACQUIRE) == seq) break;
-                HIPTRY(launch_small_service(static_cast<SmallMailbox*>(dmb), kSvcIdleUs * 100, c->svc));
+                HIPTRY(launch_small_service(static_cast<SmallMailbox*>(dmb), kSvcIdleUs * 100, kSvcLifeUs * 100, c->svc));
                 ++c->svc_launches;
             } else if (q != hipErrorNotReady) {
                 return st_at(q, "k_small_service", __FILE__, __LINE__);
@@ -285,7 +286,20 @@ int small_service_call(nkv_ctx* c, const uint64_t* d_desc, const uint8_t* d_vals
 void svc_stop(nkv_ctx* c) {
     if (c->svc_live && c->h_mbox) {
         __atomic_store_n(&c->h_mbox->doorbell, kSvcExit, __ATOMIC_RELEASE);
-        (void)hipStreamSynchronize(c->svc);
+        // the service leaves at its next poll (or its idle timeout); never wait
+        // unboundedly in a destructor: a service that has not left after 2 s
+        // keeps its mailbox and stream (leaked) rather than hang the caller
+        const auto t0 = std::chrono::steady_clock::now();
+        while (hipStreamQuery(c->svc) == hipErrorNotReady) {
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+                if (debug_on()) fprintf(stderr, "nkv: the small-tree service did not leave; mailbox leaked\n");
+                c->svc_live = false;
+                c->svc = nullptr;
+                c->h_mbox = nullptr;
+                return;
+            }
+            usleep(50);
+        }
     }
     c->svc_live = false;
     if (c->svc) (void)hipStreamDestroy(c->svc);
@@ -842,6 +856,23 @@ int nkv_ctx_set_option(nkv_ctx* c, int key, int64_t value) try {
         default:
             return NKV_ERR_INVALID;
     }
+} NKV_CATCH
+
+int nkv_ctx_small_service_state(nkv_ctx* c, uint64_t out[6]) try {
+    if (!c || !out) return NKV_ERR_INVALID;
+    for (int k = 0; k < 6; ++k) out[k] = 0;
+    if (c->h_mbox) {
+        out[0] = __atomic_load_n(&c->h_mbox->doorbell, __ATOMIC_ACQUIRE);
+        out[1] = __atomic_load_n(&c->h_mbox->served, __ATOMIC_ACQUIRE);
+        out[2] = __atomic_load_n(&c->h_mbox->done, __ATOMIC_ACQUIRE);
+    }
+    out[3] = c->svc_launches;
+    out[4] = c->svc_live ? 1u : 0u;
+    if (c->svc) {
+        TRY(bind(c));
+        out[5] = hipStreamQuery(c->svc) == hipErrorNotReady ? 1u : 0u;
+    }
+    return NKV_OK;
 } NKV_CATCH
 
 int nkv_ctx_last_path(nkv_ctx* c, int* path) try {

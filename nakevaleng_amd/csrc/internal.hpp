@@ -187,7 +187,7 @@ struct alignas(64) SmallMailbox {
 };
 constexpr uint32_t kSvcExit = 0xFFFFFFFFu;
 constexpr uint32_t kSvcBlock = 1024;  // one workgroup: up to 1024 leaves, one lane each
-hipError_t launch_small_service(SmallMailbox* mb, uint64_t idle_ticks, hipStream_t s);
+hipError_t launch_small_service(SmallMailbox* mb, uint64_t idle_ticks, uint64_t life_ticks, hipStream_t s);
 // Clock probe of the leaf kernels on the current device (NKV_TIMING_CLOCK):
 // p = kClockWords u64 (8 slots of 32: shader-clock cycles, 100 MHz ticks, waves;
 // zeroed by the caller) or nullptr to switch it off.

@@ -2222,16 +2222,19 @@ __global__ __launch_bounds__(kSmallBlock) void k_small_tree(const uint64_t* __re
 // k_small_tree takes) is served exactly as k_small_tree serves a one-workgroup
 // launch -- leaves one lane each, every level and the image in LDS -- and seq
 // goes to mb->done behind every output byte.  Every wave leaves when the
-// doorbell reads kSvcExit (nkv_ctx_destroy) or after idle_ticks of the 100 MHz
-// real-time counter with no request (the host relaunches on its next call), so
-// the grid always drains.
+// doorbell reads kSvcExit (nkv_ctx_destroy), after idle_ticks of the 100 MHz
+// real-time counter with no request, or between requests once it has lived
+// life_ticks (the host relaunches on its next call), so the grid always drains
+// and work queued behind it on a shared hardware queue waits a bounded time.
 template <uint32_t B>
-__global__ __launch_bounds__(B) void k_small_service(SmallMailbox* __restrict__ mb, uint64_t idle_ticks) {
+__global__ __launch_bounds__(B) void k_small_service(SmallMailbox* __restrict__ mb, uint64_t idle_ticks,
+                                                     uint64_t life_ticks) {
     __shared__ __attribute__((aligned(16))) uint8_t sm[20 * (2 * kSmallMaxN - 1) + 12];
     __shared__ __attribute__((aligned(16))) uint8_t seg[kSmallSeg];
     __shared__ uint32_t cmd;
     const uint32_t tid = threadIdx.x;
     uint32_t served = __hip_atomic_load(&mb->served, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const uint64_t born = __builtin_amdgcn_s_memrealtime();
     while (true) {
         if (tid == 0) {
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -2239,7 +2242,8 @@ __global__ __launch_bounds__(B) void k_small_service(SmallMailbox* __restrict__ 
             while (true) {
                 bell = __hip_atomic_load(&mb->doorbell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 if (bell != served) break;
-                if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) {
+                const uint64_t now = __builtin_amdgcn_s_memrealtime();
+                if (now - t0 > idle_ticks || now - born > life_ticks) {
                     bell = kSvcExit;
                     break;
                 }
@@ -2296,8 +2300,8 @@ hipError_t launch_small_tree(const uint64_t* desc, const uint8_t* vals, uint32_t
     return hipGetLastError();
 }
 
-hipError_t launch_small_service(SmallMailbox* mb, uint64_t idle_ticks, hipStream_t s) {
-    hipLaunchKernelGGL(k_small_service<kSvcBlock>, dim3(1), dim3(kSvcBlock), 0, s, mb, idle_ticks);
+hipError_t launch_small_service(SmallMailbox* mb, uint64_t idle_ticks, uint64_t life_ticks, hipStream_t s) {
+    hipLaunchKernelGGL(k_small_service<kSvcBlock>, dim3(1), dim3(kSvcBlock), 0, s, mb, idle_ticks, life_ticks);
     return hipGetLastError();
 }
 

@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""Diagnostic probe of the resident small-tree service (NKV_OPT_SMALL_PATH 3):
+each call's wall time, result against the oracle and the mailbox state
+(nkv_ctx_small_service_state), printed as it goes; a watchdog ends the process
+after --limit seconds so a stuck call cannot hang the GPU job.
+
+    python tools/svc_debug.py [--limit 60]
+"""
+import faulthandler
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    limit = int(sys.argv[sys.argv.index("--limit") + 1]) if "--limit" in sys.argv else 60
+    faulthandler.dump_traceback_later(limit, exit=True)
+    import numpy as np
+    from nakevaleng_amd import _lib
+    from oracle import oracle_c as oc
+    L = _lib.lib()
+    ctx = _lib.Context(0)
+    ctx.set_option(_lib.NKV_OPT_SMALL_PATH, 3)
+    rng = np.random.default_rng(3)
+    print("state0", ctx.small_service_state(), flush=True)
+    for n in (1, 2, 3, 10, 100, 1000, 10, 10):
+        ln = rng.integers(0, 200, n).astype(np.uint64)
+        off = np.zeros(n, np.uint64)
+        off[1:] = np.cumsum(ln[:-1])
+        base = np.frombuffer(rng.bytes(int(ln.sum()) + 1), np.uint8).copy()
+        root = np.zeros(20, np.uint8)
+        nodes = np.zeros((L.nkv_total_nodes(n), 20), np.uint8)
+        t0 = time.perf_counter()
+        rc = L.nkv_tree_from_values(ctx.h, _lib.p8(base), _lib.p64(off), _lib.p64(ln), n, _lib.p8(root),
+                                    _lib.p8(nodes), None)
+        dt = (time.perf_counter() - t0) * 1e6
+        want = oc.tree_from_digests(oc.leaf_hashes(base, off, ln))
+        ok = rc == 0 and np.array_equal(nodes, want)
+        print(f"n={n} rc={rc} ok={ok} us={dt:.1f} path={ctx.last_path()} state={ctx.small_service_state()}",
+              flush=True)
+        if not ok and rc == 0:
+            bad = np.nonzero((nodes != want).any(axis=1))[0]
+            print(f"  wrong nodes: {len(bad)} of {len(want)}, first {bad[:8].tolist()}", flush=True)
+    # steady-state latency of the default flush shape (10 values <= 200 B)
+    n = 10
+    ln = rng.integers(1, 201, n).astype(np.uint64)
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum(ln[:-1])
+    base = np.frombuffer(rng.bytes(int(ln.sum()) + 1), np.uint8).copy()
+    root = np.zeros(20, np.uint8)
+    ts = []
+    for _ in range(300):
+        t0 = time.perf_counter()
+        _lib.check(L.nkv_tree_from_values(ctx.h, _lib.p8(base), _lib.p64(off), _lib.p64(ln), n, _lib.p8(root),
+                                          None, None))
+        ts.append((time.perf_counter() - t0) * 1e6)
+    ts.sort()
+    print(f"n=10 x300: median {ts[150]:.1f} us, p10 {ts[30]:.1f}, p90 {ts[270]:.1f}; "
+          f"state={ctx.small_service_state()}", flush=True)
+    t0 = time.perf_counter()
+    ctx.close()
+    print(f"close {(time.perf_counter() - t0) * 1e3:.1f} ms", flush=True)
+    faulthandler.cancel_dump_traceback_later()
+
+
+if __name__ == "__main__":
+    main()
