@@ -2232,15 +2232,24 @@ __global__ __launch_bounds__(B) void k_small_service(SmallMailbox* __restrict__ 
     __shared__ __attribute__((aligned(16))) uint8_t sm[20 * (2 * kSmallMaxN - 1) + 12];
     __shared__ __attribute__((aligned(16))) uint8_t seg[kSmallSeg];
     __shared__ uint32_t cmd;
+    // Control flow stays wave-uniform: the whole of wave 0 polls (every lane
+    // the same word, the value made scalar), and every decision after the
+    // barrier is on a scalar.  A poll loop run by one LANE with a workgroup
+    // barrier after it lets the compiler park that lane while its wave's other
+    // lanes go round the outer loop's barrier on their own (the first build
+    // served one request and then spun on it).
     const uint32_t tid = threadIdx.x;
-    uint32_t served = __hip_atomic_load(&mb->served, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const bool poller = tid < 64;
+    uint32_t served =
+        __builtin_amdgcn_readfirstlane(__hip_atomic_load(&mb->served, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
     const uint64_t born = __builtin_amdgcn_s_memrealtime();
     while (true) {
-        if (tid == 0) {
+        if (poller) {
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
             uint32_t bell;
             while (true) {
-                bell = __hip_atomic_load(&mb->doorbell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                bell = __builtin_amdgcn_readfirstlane(
+                    __hip_atomic_load(&mb->doorbell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
                 if (bell != served) break;
                 const uint64_t now = __builtin_amdgcn_s_memrealtime();
                 if (now - t0 > idle_ticks || now - born > life_ticks) {
@@ -2251,14 +2260,17 @@ __global__ __launch_bounds__(B) void k_small_service(SmallMailbox* __restrict__ 
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: the request's bytes
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            cmd = bell;
+            if (tid == 0) cmd = bell;
         }
         __syncthreads();
-        const uint32_t seq = cmd;
+        const uint32_t seq = __builtin_amdgcn_readfirstlane(cmd);
         if (seq == kSvcExit) break;
-        const uint32_t n = __hip_atomic_load(&mb->n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        const uint32_t vbytes = __hip_atomic_load(&mb->vbytes, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        const uint32_t img_at = __hip_atomic_load(&mb->img_at, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const uint32_t n =
+            __builtin_amdgcn_readfirstlane(__hip_atomic_load(&mb->n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+        const uint32_t vbytes =
+            __builtin_amdgcn_readfirstlane(__hip_atomic_load(&mb->vbytes, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+        const uint32_t img_at =
+            __builtin_amdgcn_readfirstlane(__hip_atomic_load(&mb->img_at, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
         const uint64_t* desc = reinterpret_cast<const uint64_t*>(
             __hip_atomic_load(&mb->desc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
         const uint8_t* vals = reinterpret_cast<const uint8_t*>(
