@@ -127,7 +127,7 @@ def test_small_path_matches_grid_path_and_bounds(small_ctx, oracle):
     root, nodes, img, path = _run(_lib, ctx, base, off, ln)
     nodes_w, img_w = _want(oracle, base, off, ln)
     assert path == _lib.NKV_PATH_GRID and np.array_equal(nodes, nodes_w) and img == img_w
-    for key, bad in ((_lib.NKV_OPT_SMALL_PATH, 3), (_lib.NKV_OPT_SMALL_PATH, -1), (_lib.NKV_OPT_SMALL_MAX_N, 1025),
+    for key, bad in ((_lib.NKV_OPT_SMALL_PATH, 4), (_lib.NKV_OPT_SMALL_PATH, -1), (_lib.NKV_OPT_SMALL_MAX_N, 1025),
                      (_lib.NKV_OPT_SMALL_MAX_BYTES, (1 << 30) + 1)):
         assert _lib.lib().nkv_ctx_set_option(ctx.h, key, bad) == _lib.NKV_ERR_INVALID
 
