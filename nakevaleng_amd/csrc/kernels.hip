@@ -29,8 +29,15 @@
 
 namespace nkv {
 
+// experiment builds only (tools/build_exp.sh -D...), never the product library
 #ifndef NKV_EXP_REC
-#define NKV_EXP_REC 0  // experiment builds only (tools/build_exp.sh -DNKV_EXP_REC=k)
+#define NKV_EXP_REC 0
+#endif
+#ifndef NKV_EXP_NOTAIL
+#define NKV_EXP_NOTAIL 0
+#endif
+#ifndef NKV_EXP_FIXEDHDR
+#define NKV_EXP_FIXEDHDR 0
 #endif
 
 #ifdef NKV_DIAG
@@ -92,6 +99,14 @@ hipError_t set_clock_probe(unsigned long long* p, hipStream_t s) {
 // not 8-byte aligned; it then holds byte 29, so every load stays inside an
 // aligned word that holds a header byte (no page can be crossed).
 __device__ __forceinline__ void ld_header_sizes(const uint8_t* p, uint64_t& ks, uint64_t& vs) {
+#if NKV_EXP_FIXEDHDR
+    // traffic experiment only (wrong for any other shape): the bench's 16-B
+    // keys and 4,050-B values without reading the header line
+    (void)p;
+    ks = 16;
+    vs = 4050;
+    return;
+#endif
     // pointer arithmetic on p (not an integer-to-pointer cast) keeps the global
     // address space: global_load, not flat_load
     const uint8_t* f = p + 14;
@@ -325,7 +340,13 @@ __device__ __forceinline__ void sha1_tail(const uint8_t* p, uint64_t len, uint32
         be16_from_raw(c, w);
     } else {
         uint32_t d[20];
+#if NKV_EXP_NOTAIL
+        // traffic experiment only (wrong digests): no load of the tail window
+#pragma unroll
+        for (int k = 0; k < 20; ++k) d[k] = 0u;
+#else
         load_window(pt, rem, d);
+#endif
         be16_funnel(d, uint32_t(reinterpret_cast<uintptr_t>(pt) & 15), w);
     }
     hook.tail(w, rem);
@@ -2154,11 +2175,19 @@ __device__ __forceinline__ void small_levels_and_image(uint8_t* sm, uint8_t* seg
 }
 
 // seq into the host-coherent completion word once every output byte of the
-// workgroup is written at system scope
+// workgroup is written at system scope.  One release for the workgroup, not one
+// per wave (the guide's producer form: every storing wave waits for its own
+// stores, a barrier, then ONE lane's release fence -- a single L2 write-back --
+// its wait, and the flag); a fence in every wave cost each wave an L2
+// write-back (16 of them in the 1024-thread service).
 __device__ __forceinline__ void small_signal_done(unsigned int* done, uint32_t seq) {
-    __threadfence_system();  // each wave's output stores complete at system scope
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's output stores have completed
     __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the write-back before the flag (guide: compiler hazard)
+        __hip_atomic_store(done, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 // vbytes: the extent of vals the values lie in.  A one-workgroup launch whose

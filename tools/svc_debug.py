@@ -4,7 +4,7 @@ each call's wall time, result against the oracle and the mailbox state
 (nkv_ctx_small_service_state), printed as it goes; a watchdog ends the process
 after --limit seconds so a stuck call cannot hang the GPU job.
 
-    python tools/svc_debug.py [--limit 60]
+    python tools/svc_debug.py [--limit 60] [--modes 1,3]
 """
 import faulthandler
 import os
@@ -44,22 +44,28 @@ def main():
         if not ok and rc == 0:
             bad = np.nonzero((nodes != want).any(axis=1))[0]
             print(f"  wrong nodes: {len(bad)} of {len(want)}, first {bad[:8].tolist()}", flush=True)
-    # steady-state latency of the default flush shape (10 values <= 200 B)
-    n = 10
-    ln = rng.integers(1, 201, n).astype(np.uint64)
-    off = np.zeros(n, np.uint64)
-    off[1:] = np.cumsum(ln[:-1])
-    base = np.frombuffer(rng.bytes(int(ln.sum()) + 1), np.uint8).copy()
-    root = np.zeros(20, np.uint8)
-    ts = []
-    for _ in range(300):
-        t0 = time.perf_counter()
-        _lib.check(L.nkv_tree_from_values(ctx.h, _lib.p8(base), _lib.p64(off), _lib.p64(ln), n, _lib.p8(root),
-                                          None, None))
-        ts.append((time.perf_counter() - t0) * 1e6)
-    ts.sort()
-    print(f"n=10 x300: median {ts[150]:.1f} us, p10 {ts[30]:.1f}, p90 {ts[270]:.1f}; "
-          f"state={ctx.small_service_state()}", flush=True)
+    # steady-state latency of the default flush (10 values <= 200 B) and
+    # compaction (40) shapes, per small-path mode (--modes, default 3)
+    modes = [int(m) for m in (sys.argv[sys.argv.index("--modes") + 1] if "--modes" in sys.argv else "3").split(",")]
+    for mode in modes:
+        ctx.set_option(_lib.NKV_OPT_SMALL_PATH, mode)
+        for n in (10, 40):
+            ln = rng.integers(1, 201, n).astype(np.uint64)
+            off = np.zeros(n, np.uint64)
+            off[1:] = np.cumsum(ln[:-1])
+            base = np.frombuffer(rng.bytes(int(ln.sum()) + 1), np.uint8).copy()
+            root = np.zeros(20, np.uint8)
+            want = oc.tree_from_digests(oc.leaf_hashes(base, off, ln))[-1].tobytes()
+            ts = []
+            for _ in range(300):
+                t0 = time.perf_counter()
+                _lib.check(L.nkv_tree_from_values(ctx.h, _lib.p8(base), _lib.p64(off), _lib.p64(ln), n,
+                                                  _lib.p8(root), None, None))
+                ts.append((time.perf_counter() - t0) * 1e6)
+            assert root.tobytes() == want, (mode, n)
+            ts.sort()
+            print(f"mode {mode} n={n} x300: median {ts[150]:.1f} us, p10 {ts[30]:.1f}, p90 {ts[270]:.1f}; "
+                  f"state={ctx.small_service_state()}", flush=True)
     t0 = time.perf_counter()
     ctx.close()
     print(f"close {(time.perf_counter() - t0) * 1e3:.1f} ms", flush=True)
