@@ -88,6 +88,7 @@ SIGNATURES = {
     "nkv_ctx_sync": (_int, [_vp]),
     "nkv_ctx_last_path": (_int, [_vp, ctypes.POINTER(_int)]),
     "nkv_ctx_small_service_state": (_int, [_vp, ctypes.POINTER(ctypes.c_uint64)]),
+    "nkv_ctx_small_service_trace": (_int, [_vp, _int, ctypes.POINTER(ctypes.c_uint64)]),
     "nkv_ctx_set_option": (_int, [_vp, _int, ctypes.c_int64]),
     "nkv_ctx_set_timing": (_int, [_vp, _int]),
     "nkv_ctx_last_timing": (_int, [_vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
@@ -294,6 +295,13 @@ class Context:
         a = (ctypes.c_uint64 * 6)()
         check(lib().nkv_ctx_small_service_state(self.h, a))
         return dict(zip(("doorbell", "served", "done", "launches", "live", "busy"), list(a)))
+
+    def small_service_trace(self, enable: bool) -> list:
+        """Turn the service's phase stamps on/off; returns the latest traced request's
+        five (s_memrealtime, s_memtime) pairs."""
+        a = (ctypes.c_uint64 * 10)()
+        check(lib().nkv_ctx_small_service_trace(self.h, 1 if enable else 0, a))
+        return list(a)
 
     def set_timing(self, on, clock: bool = False) -> None:
         """Events around the leaf kernel / reduce (on) and the leaf kernels' clock probe (clock)."""

@@ -255,6 +255,7 @@ int small_service_call(nkv_ctx* c, const uint64_t* d_desc, const uint8_t* d_vals
     mb->desc = reinterpret_cast<uintptr_t>(d_desc);
     mb->vals = reinterpret_cast<uintptr_t>(d_vals);
     mb->out = reinterpret_cast<uintptr_t>(d_out);
+    mb->trace = c->svc_trace ? 1u : 0u;
     __atomic_store_n(&mb->doorbell, seq, __ATOMIC_RELEASE);
     if (!c->svc_live) {
         HIPTRY(launch_small_service(static_cast<SmallMailbox*>(dmb), kSvcIdleUs * 100, kSvcLifeUs * 100, c->svc));
@@ -872,6 +873,16 @@ int nkv_ctx_small_service_state(nkv_ctx* c, uint64_t out[6]) try {
         TRY(bind(c));
         out[5] = hipStreamQuery(c->svc) == hipErrorNotReady ? 1u : 0u;
     }
+    return NKV_OK;
+} NKV_CATCH
+
+int nkv_ctx_small_service_trace(nkv_ctx* c, int enable, uint64_t out[10]) try {
+    if (!c || enable < 0 || enable > 1) return NKV_ERR_INVALID;
+    if (out) {
+        for (int k = 0; k < kSvcStamps; ++k)
+            out[k] = c->h_mbox ? __atomic_load_n(&c->h_mbox->stamps[k], __ATOMIC_ACQUIRE) : 0u;
+    }
+    c->svc_trace = enable != 0;
     return NKV_OK;
 } NKV_CATCH
 

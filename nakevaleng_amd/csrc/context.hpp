@@ -214,6 +214,7 @@ struct nkv_ctx {
     nkv::SmallMailbox* h_mbox = nullptr;
     hipStream_t svc = nullptr;
     bool svc_live = false;   // a service launch was made and may still run
+    bool svc_trace = false;  // nkv_ctx_small_service_trace: stamp each request's phases
     uint64_t svc_launches = 0;
 };
 

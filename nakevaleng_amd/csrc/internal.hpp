@@ -184,7 +184,13 @@ struct alignas(64) SmallMailbox {
     uint32_t done;      // service: seq whose outputs are all written
     uint32_t n, vbytes, img_at;
     uint64_t desc, vals, out;  // device addresses of host-coherent memory
+    uint32_t trace, pad;  // host: nonzero = stamp this request's phases (diagnostics)
+    // service, when traced: (s_memrealtime, s_memtime) after the doorbell was
+    // seen, the input staged, the leaves hashed, the levels + image written,
+    // and the completion word stored
+    uint64_t stamps[10];
 };
+constexpr int kSvcStamps = 10;
 constexpr uint32_t kSvcExit = 0xFFFFFFFFu;
 constexpr uint32_t kSvcBlock = 1024;  // one workgroup: up to 1024 leaves, one lane each
 hipError_t launch_small_service(SmallMailbox* mb, uint64_t idle_ticks, uint64_t life_ticks, hipStream_t s);

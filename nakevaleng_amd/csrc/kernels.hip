@@ -2272,6 +2272,12 @@ __global__ __launch_bounds__(B) void k_small_service(SmallMailbox* __restrict__ 
     uint32_t served =
         __builtin_amdgcn_readfirstlane(__hip_atomic_load(&mb->served, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
     const uint64_t born = __builtin_amdgcn_s_memrealtime();
+    uint64_t seen_rt = 0, seen_mt = 0;  // wave 0: when the latest doorbell was seen (traced requests)
+    // (s_memrealtime, s_memtime) of a traced request's phase k into the mailbox
+    auto stamp = [&](int k, uint64_t rt, uint64_t mt) {
+        __hip_atomic_store(&mb->stamps[2 * k], rt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&mb->stamps[2 * k + 1], mt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    };
     while (true) {
         if (poller) {
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -2279,6 +2285,8 @@ __global__ __launch_bounds__(B) void k_small_service(SmallMailbox* __restrict__ 
             while (true) {
                 bell = __builtin_amdgcn_readfirstlane(
                     __hip_atomic_load(&mb->doorbell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+                seen_rt = __builtin_amdgcn_s_memrealtime();
+                seen_mt = __builtin_amdgcn_s_memtime();
                 if (bell != served) break;
                 const uint64_t now = __builtin_amdgcn_s_memrealtime();
                 if (now - t0 > idle_ticks || now - born > life_ticks) {
@@ -2305,6 +2313,9 @@ __global__ __launch_bounds__(B) void k_small_service(SmallMailbox* __restrict__ 
         const uint8_t* vals = reinterpret_cast<const uint8_t*>(
             __hip_atomic_load(&mb->vals, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
         uint8_t* out = reinterpret_cast<uint8_t*>(__hip_atomic_load(&mb->out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+        const bool traced =
+            __builtin_amdgcn_readfirstlane(__hip_atomic_load(&mb->trace, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) != 0u;
+        if (traced && tid == 0) stamp(0, seen_rt, seen_mt);
         if (n >= 1 && n <= kSmallMaxN) {  // the host never rings with another n; a bad one only signals
             if (16u * n + vbytes <= kSmallSeg) {
                 small_stage_in<B>(reinterpret_cast<const uint8_t*>(desc), seg, 16u * n);
@@ -2313,15 +2324,25 @@ __global__ __launch_bounds__(B) void k_small_service(SmallMailbox* __restrict__ 
                 desc = reinterpret_cast<const uint64_t*>(seg);
                 vals = seg + 16u * n;
             }
+            if (traced && tid == 0) stamp(1, __builtin_amdgcn_s_memrealtime(), __builtin_amdgcn_s_memtime());
             for (uint32_t i = tid; i < n; i += B) {
                 uint32_t h[5];
                 sha1_value_aligned(vals + desc[2 * i], desc[2 * i + 1], h);  // NewLeaf, merklenode.go:27-34
                 store_digest(sm, i, h);
             }
+            if (traced) {
+                __syncthreads();
+                if (tid == 0) stamp(2, __builtin_amdgcn_s_memrealtime(), __builtin_amdgcn_s_memtime());
+            }
             small_levels_and_image<B>(sm, seg, n, out, img_at);
+            if (traced && tid == 0) stamp(3, __builtin_amdgcn_s_memrealtime(), __builtin_amdgcn_s_memtime());
         }
         served = seq;
         if (tid == 0) __hip_atomic_store(&mb->served, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (traced && tid == 0) {  // before the completion word: the host reads the stamps after it
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            stamp(4, __builtin_amdgcn_s_memrealtime(), __builtin_amdgcn_s_memtime());
+        }
         small_signal_done(&mb->done, seq);
     }
 }

@@ -4,7 +4,7 @@ each call's wall time, result against the oracle and the mailbox state
 (nkv_ctx_small_service_state), printed as it goes; a watchdog ends the process
 after --limit seconds so a stuck call cannot hang the GPU job.
 
-    python tools/svc_debug.py [--limit 60] [--modes 1,3]
+    python tools/svc_debug.py [--limit 60] [--modes 1,3] [--trace]
 """
 import faulthandler
 import os
@@ -66,6 +66,35 @@ def main():
             ts.sort()
             print(f"mode {mode} n={n} x300: median {ts[150]:.1f} us, p10 {ts[30]:.1f}, p90 {ts[270]:.1f}; "
                   f"state={ctx.small_service_state()}", flush=True)
+    # where a request's time goes inside the service (--trace): the stamps of
+    # every request, phase medians in us and the shader clock over each phase
+    if "--trace" in sys.argv:
+        import json
+        ctx.set_option(_lib.NKV_OPT_SMALL_PATH, 3)
+        for n, lo, hi in ((10, 1, 200), (40, 1, 200), (256, 1, 200)):
+            ln = rng.integers(lo, hi + 1, n).astype(np.uint64)
+            off = np.zeros(n, np.uint64)
+            off[1:] = np.cumsum(ln[:-1])
+            base = np.frombuffer(rng.bytes(int(ln.sum()) + 1), np.uint8).copy()
+            root = np.zeros(20, np.uint8)
+            ctx.small_service_trace(True)
+            st, walls = [], []
+            for _ in range(200):
+                t0 = time.perf_counter()
+                _lib.check(L.nkv_tree_from_values(ctx.h, _lib.p8(base), _lib.p64(off), _lib.p64(ln), n,
+                                                  _lib.p8(root), None, None))
+                walls.append((time.perf_counter() - t0) * 1e6)
+                st.append(ctx.small_service_trace(True))
+            ctx.small_service_trace(False)
+            a = np.array(st[20:], np.float64)
+            rt, mt = a[:, 0::2], a[:, 1::2]
+            out = {"n": n, "value_bytes": [lo, hi], "wall_us_median": round(float(np.median(walls[20:])), 2)}
+            for name, j0, j1 in (("request_and_stage_in", 0, 1), ("leaves", 1, 2), ("levels_and_image", 2, 3),
+                                 ("signal", 3, 4), ("seen_to_signal", 0, 4)):
+                us = (rt[:, j1] - rt[:, j0]) / 100.0
+                ghz = (mt[:, j1] - mt[:, j0]) / np.maximum(rt[:, j1] - rt[:, j0], 1) * 100e6 / 1e9
+                out[name] = {"us_median": round(float(np.median(us)), 2), "ghz_median": round(float(np.median(ghz)), 3)}
+            print("trace " + json.dumps(out), flush=True)
     t0 = time.perf_counter()
     ctx.close()
     print(f"close {(time.perf_counter() - t0) * 1e3:.1f} ms", flush=True)
