@@ -249,13 +249,13 @@ int small_service_call(nkv_ctx* c, const uint64_t* d_desc, const uint8_t* d_vals
     SmallMailbox* mb = c->h_mbox;
     void* dmb = nullptr;
     HIPTRY(hipHostGetDevicePointer(&dmb, mb, 0));
-    mb->n = n;
-    mb->vbytes = vbytes;
-    mb->img_at = img_at;
-    mb->desc = reinterpret_cast<uintptr_t>(d_desc);
-    mb->vals = reinterpret_cast<uintptr_t>(d_vals);
-    mb->out = reinterpret_cast<uintptr_t>(d_out);
-    mb->trace = c->svc_trace ? 1u : 0u;
+    mb->req.n = n;
+    mb->req.vbytes = vbytes;
+    mb->req.img_at = img_at;
+    mb->req.trace = c->svc_trace ? 1u : 0u;
+    mb->req.desc = reinterpret_cast<uintptr_t>(d_desc);
+    mb->req.vals = reinterpret_cast<uintptr_t>(d_vals);
+    mb->req.out = reinterpret_cast<uintptr_t>(d_out);
     __atomic_store_n(&mb->doorbell, seq, __ATOMIC_RELEASE);
     if (!c->svc_live) {
         HIPTRY(launch_small_service(static_cast<SmallMailbox*>(dmb), kSvcIdleUs * 100, kSvcLifeUs * 100, c->svc));
@@ -362,7 +362,7 @@ int small_tree(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint6
     uint32_t seq = ++c->small_seq;
     if (seq == 0 || seq == kSvcExit) seq = c->small_seq = 1;  // 0 is the word's cleared state
     *hdone = 0;
-    if (c->small_path == 3) {  // the resident service: no launch, no runtime completion
+    if (c->small_path == 3 && n <= kSvcMaxN) {  // the resident service: no launch, no runtime completion
         void *din = nullptr, *dout = nullptr, *dblk = nullptr;
         HIPTRY(hipHostGetDevicePointer(&din, c->h_sin, 0));
         HIPTRY(hipHostGetDevicePointer(&dout, c->h_sout, 0));

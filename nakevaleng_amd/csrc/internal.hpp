@@ -178,13 +178,17 @@ hipError_t launch_small_tree(const uint64_t* desc, const uint8_t* vals, uint32_t
 // The host writes a request (the fields after `done`, as launch_small_tree's
 // arguments) and then its seq into `doorbell`; the service answers with seq
 // in `done` behind every output byte.
+struct alignas(64) SmallRequest {  // one 64-byte line: the service reads it with ONE load
+    uint32_t n, vbytes, img_at, trace;  // trace: nonzero = stamp this request's phases
+    uint64_t desc, vals, out;           // device addresses of host-coherent memory
+    uint64_t pad[2];
+};
 struct alignas(64) SmallMailbox {
     uint32_t doorbell;  // host: seq of the latest request; kSvcExit: leave
     uint32_t served;    // service: the latest seq it served (a relaunch resumes from it)
     uint32_t done;      // service: seq whose outputs are all written
-    uint32_t n, vbytes, img_at;
-    uint64_t desc, vals, out;  // device addresses of host-coherent memory
-    uint32_t trace, pad;  // host: nonzero = stamp this request's phases (diagnostics)
+    uint32_t pad[13];
+    SmallRequest req;   // host: written before the doorbell
     // service, when traced: (s_memrealtime, s_memtime) after the doorbell was
     // seen, the input staged, the leaves hashed, the levels + image written,
     // and the completion word stored
@@ -192,7 +196,8 @@ struct alignas(64) SmallMailbox {
 };
 constexpr int kSvcStamps = 10;
 constexpr uint32_t kSvcExit = 0xFFFFFFFFu;
-constexpr uint32_t kSvcBlock = 1024;  // one workgroup: up to 1024 leaves, one lane each
+constexpr uint32_t kSvcBlock = 256;  // one workgroup, one lane per leaf
+constexpr uint32_t kSvcMaxN = 256;   // larger batches take the one-launch kernel
 hipError_t launch_small_service(SmallMailbox* mb, uint64_t idle_ticks, uint64_t life_ticks, hipStream_t s);
 // Clock probe of the leaf kernels on the current device (NKV_TIMING_CLOCK):
 // p = kClockWords u64 (8 slots of 32: shader-clock cycles, 100 MHz ticks, waves;

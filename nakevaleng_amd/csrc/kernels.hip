@@ -2242,8 +2242,8 @@ __global__ __launch_bounds__(kSmallBlock) void k_small_tree(const uint64_t* __re
 }
 
 // The resident small-tree service (NKV_OPT_SMALL_PATH 3): ONE workgroup of
-// kSvcBlock threads stays on the GPU between calls and serves one request at a
-// time from a host-coherent mailbox, so a default-size flush pays neither a
+// kSvcBlock threads stays on the GPU between calls and serves one request of at
+// most kSvcMaxN leaves at a time from a host-coherent mailbox, so a default-size flush pays neither a
 // launch nor the runtime's completion path ("The
 // small-flush floor").  Thread 0 polls the doorbell across PCIe (relaxed
 // system-scope loads, s_sleep between polls); a new seq is acquired at system
@@ -2258,9 +2258,10 @@ __global__ __launch_bounds__(kSmallBlock) void k_small_tree(const uint64_t* __re
 template <uint32_t B>
 __global__ __launch_bounds__(B) void k_small_service(SmallMailbox* __restrict__ mb, uint64_t idle_ticks,
                                                      uint64_t life_ticks) {
-    __shared__ __attribute__((aligned(16))) uint8_t sm[20 * (2 * kSmallMaxN - 1) + 12];
+    __shared__ __attribute__((aligned(16))) uint8_t sm[20 * (2 * kSvcMaxN - 1) + 12];
     __shared__ __attribute__((aligned(16))) uint8_t seg[kSmallSeg];
     __shared__ uint32_t cmd;
+    __shared__ uint32_t rq[16];  // the request line
     // Control flow stays wave-uniform: the whole of wave 0 polls (every lane
     // the same word, the value made scalar), and every decision after the
     // barrier is on a scalar.  A poll loop run by one LANE with a workgroup
@@ -2297,26 +2298,30 @@ __global__ __launch_bounds__(B) void k_small_service(SmallMailbox* __restrict__ 
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: the request's bytes
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (bell != kSvcExit) {
+                // the request line in one load (16 lanes, one dword each): one
+                // PCIe round trip for every field
+                const uint32_t* rl = reinterpret_cast<const uint32_t*>(&mb->req);
+                if (tid < 16) rq[tid] = __hip_atomic_load(rl + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
             if (tid == 0) cmd = bell;
         }
         __syncthreads();
         const uint32_t seq = __builtin_amdgcn_readfirstlane(cmd);
         if (seq == kSvcExit) break;
-        const uint32_t n =
-            __builtin_amdgcn_readfirstlane(__hip_atomic_load(&mb->n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-        const uint32_t vbytes =
-            __builtin_amdgcn_readfirstlane(__hip_atomic_load(&mb->vbytes, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-        const uint32_t img_at =
-            __builtin_amdgcn_readfirstlane(__hip_atomic_load(&mb->img_at, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-        const uint64_t* desc = reinterpret_cast<const uint64_t*>(
-            __hip_atomic_load(&mb->desc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-        const uint8_t* vals = reinterpret_cast<const uint8_t*>(
-            __hip_atomic_load(&mb->vals, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-        uint8_t* out = reinterpret_cast<uint8_t*>(__hip_atomic_load(&mb->out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-        const bool traced =
-            __builtin_amdgcn_readfirstlane(__hip_atomic_load(&mb->trace, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) != 0u;
+        auto rq64 = [&](int k) {
+            return uint64_t(__builtin_amdgcn_readfirstlane(rq[k])) |
+                   (uint64_t(__builtin_amdgcn_readfirstlane(rq[k + 1])) << 32);
+        };
+        const uint32_t n = __builtin_amdgcn_readfirstlane(rq[0]);
+        const uint32_t vbytes = __builtin_amdgcn_readfirstlane(rq[1]);
+        const uint32_t img_at = __builtin_amdgcn_readfirstlane(rq[2]);
+        const bool traced = __builtin_amdgcn_readfirstlane(rq[3]) != 0u;
+        const uint64_t* desc = reinterpret_cast<const uint64_t*>(rq64(4));
+        const uint8_t* vals = reinterpret_cast<const uint8_t*>(rq64(6));
+        uint8_t* out = reinterpret_cast<uint8_t*>(rq64(8));
         if (traced && tid == 0) stamp(0, seen_rt, seen_mt);
-        if (n >= 1 && n <= kSmallMaxN) {  // the host never rings with another n; a bad one only signals
+        if (n >= 1 && n <= kSvcMaxN) {  // the host never rings with another n; a bad one only signals
             if (16u * n + vbytes <= kSmallSeg) {
                 small_stage_in<B>(reinterpret_cast<const uint8_t*>(desc), seg, 16u * n);
                 small_stage_in<B>(vals, seg + 16u * n, vbytes);
