@@ -26,7 +26,9 @@ def main():
     ctx.set_option(_lib.NKV_OPT_SMALL_PATH, 3)
     rng = np.random.default_rng(3)
     print("state0", ctx.small_service_state(), flush=True)
-    for n in (1, 2, 3, 10, 100, 1000, 10, 10):
+    sizes = ([int(x) for x in sys.argv[sys.argv.index("--sizes") + 1].split(",")] if "--sizes" in sys.argv
+             else [1, 2, 3, 10, 100, 1000, 10, 10])
+    for n in sizes:
         ln = rng.integers(0, 200, n).astype(np.uint64)
         off = np.zeros(n, np.uint64)
         off[1:] = np.cumsum(ln[:-1])
