@@ -264,11 +264,17 @@ int small_service_call(nkv_ctx* c, const uint64_t* d_desc, const uint8_t* d_vals
     }
     const auto t0 = std::chrono::steady_clock::now();
     for (uint32_t k = 1;; ++k) {
-        if (__atomic_load_n(&mb->done, __ATOMIC_ACQUIRE) == seq) break;
+        if (__atomic_load_n(&mb->done, __ATOMIC_ACQUIRE) == seq) {
+            if (__atomic_load_n(&mb->refused, __ATOMIC_ACQUIRE) == seq) return NKV_ERR_DEVICE;
+            break;
+        }
         if ((k & 255u) == 0u) {
             const hipError_t q = hipStreamQuery(c->svc);
             if (q == hipSuccess) {  // the service has left (idle): start it again, unless it answered
-                if (__atomic_load_n(&mb->done, __ATOMIC_ACQUIRE) == seq) break;
+                if (__atomic_load_n(&mb->done, __ATOMIC_ACQUIRE) == seq) {
+                    if (__atomic_load_n(&mb->refused, __ATOMIC_ACQUIRE) == seq) return NKV_ERR_DEVICE;
+                    break;
+                }
                 HIPTRY(launch_small_service(static_cast<SmallMailbox*>(dmb), kSvcIdleUs * 100, kSvcLifeUs * 100, c->svc));
                 ++c->svc_launches;
             } else if (q != hipErrorNotReady) {

@@ -187,7 +187,8 @@ struct alignas(64) SmallMailbox {
     uint32_t doorbell;  // host: seq of the latest request; kSvcExit: leave
     uint32_t served;    // service: the latest seq it served (a relaunch resumes from it)
     uint32_t done;      // service: seq whose outputs are all written
-    uint32_t pad[13];
+    uint32_t refused;   // service: seq of a request it refused (a field out of range): nothing written
+    uint32_t pad[12];
     SmallRequest req;   // host: written before the doorbell
     // service, when traced: (s_memrealtime, s_memtime) after the doorbell was
     // seen, the input staged, the leaves hashed, the levels + image written,
@@ -195,6 +196,12 @@ struct alignas(64) SmallMailbox {
     uint64_t stamps[10];
 };
 constexpr int kSvcStamps = 10;
+// the service reads the request line as 16 dwords: [0] n, [1] vbytes, [2]
+// img_at, [3] trace, [4..5] desc, [6..7] vals, [8..9] out
+static_assert(offsetof(SmallMailbox, req) == 64 && sizeof(SmallRequest) == 64, "request line");
+static_assert(offsetof(SmallRequest, desc) == 16 && offsetof(SmallRequest, vals) == 24 &&
+                  offsetof(SmallRequest, out) == 32,
+              "request dwords");
 constexpr uint32_t kSvcExit = 0xFFFFFFFFu;
 constexpr uint32_t kSvcBlock = 256;  // one workgroup, one lane per leaf
 constexpr uint32_t kSvcMaxN = 256;   // larger batches take the one-launch kernel

@@ -2309,19 +2309,26 @@ __global__ __launch_bounds__(B) void k_small_service(SmallMailbox* __restrict__ 
         __syncthreads();
         const uint32_t seq = __builtin_amdgcn_readfirstlane(cmd);
         if (seq == kSvcExit) break;
-        auto rq64 = [&](int k) {
-            return uint64_t(__builtin_amdgcn_readfirstlane(rq[k])) |
-                   (uint64_t(__builtin_amdgcn_readfirstlane(rq[k + 1])) << 32);
-        };
-        const uint32_t n = __builtin_amdgcn_readfirstlane(rq[0]);
-        const uint32_t vbytes = __builtin_amdgcn_readfirstlane(rq[1]);
-        const uint32_t img_at = __builtin_amdgcn_readfirstlane(rq[2]);
-        const bool traced = __builtin_amdgcn_readfirstlane(rq[3]) != 0u;
+        // readfirstlane returns an int: widen through uint32_t, or a low word
+        // with its top bit set sign-extends into the pointer's high word (the
+        // first build of this read faulted on exactly that)
+        auto rq32 = [&](int k) { return uint32_t(__builtin_amdgcn_readfirstlane(rq[k])); };
+        auto rq64 = [&](int k) { return uint64_t(rq32(k)) | (uint64_t(rq32(k + 1)) << 32); };
+        const uint32_t n = rq32(0);
+        const uint32_t vbytes = rq32(1);
+        const uint32_t img_at = rq32(2);
+        const bool traced = rq32(3) != 0u;
         const uint64_t* desc = reinterpret_cast<const uint64_t*>(rq64(4));
         const uint8_t* vals = reinterpret_cast<const uint8_t*>(rq64(6));
         uint8_t* out = reinterpret_cast<uint8_t*>(rq64(8));
         if (traced && tid == 0) stamp(0, seen_rt, seen_mt);
-        if (n >= 1 && n <= kSvcMaxN) {  // the host never rings with another n; a bad one only signals
+        // the host never rings with other values; a request out of range is
+        // refused (flagged, nothing read or written) rather than followed
+        const bool sane = n >= 1 && n <= kSvcMaxN && desc && vals && out &&
+                          ((reinterpret_cast<uintptr_t>(desc) | reinterpret_cast<uintptr_t>(vals) |
+                            reinterpret_cast<uintptr_t>(out) | img_at) & 15u) == 0u;
+        if (!sane && tid == 0) __hip_atomic_store(&mb->refused, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (sane) {
             if (16u * n + vbytes <= kSmallSeg) {
                 small_stage_in<B>(reinterpret_cast<const uint8_t*>(desc), seg, 16u * n);
                 small_stage_in<B>(vals, seg + 16u * n, vbytes);

@@ -7,6 +7,9 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 O=gpurun_out/r06f
 mkdir -p $O
+timeout -k 5 90 python3 -u tools/svc_debug.py --limit 75 --sizes 1,2,3,10,100,256,257,1000 > $O/svc_probe.txt 2>&1 \
+    || { cat $O/svc_probe.txt; exit 1; }
+grep -E "rc=|close" $O/svc_probe.txt
 timeout -k 10 400 python3 -u -m pytest tests/test_gpu_small.py -x -q --timeout 120 --timeout-method thread \
     > $O/small_tests.txt 2>&1 || { tail -40 $O/small_tests.txt; exit 1; }
 tail -1 $O/small_tests.txt
