@@ -326,8 +326,10 @@ int small_tree(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint6
     }
     const uint64_t tot = total_of(n);
     const uint64_t img_len = layout_of(counts_of(n)).total;
-    const uint64_t img_at = align16(20 * tot);
-    const uint64_t out_bytes = img_at + align16(img_len);
+    // img_at 0 tells the kernel to build no image: a caller that asked for none
+    // (the mirrors' New, whose Serialize walks the live tree) pays none
+    const uint64_t img_at = img_out ? align16(20 * tot) : 0;
+    const uint64_t out_bytes = img_out ? img_at + align16(img_len) : align16(20 * tot);
     uint64_t lo = 0, hi = 0;
     nkv_ctx::Pinned* blk = pinned_extent(c, base, off, len, n, &lo, &hi);
     if (blk) blk->streamed = 0;  // a call over a pinned block ends its batch (nkv_host_stream)

@@ -164,7 +164,7 @@ hipError_t launch_bloom_staged(int mode, const uint8_t* base, const uint64_t* of
 hipError_t launch_fill(uint8_t* buf, uint64_t nbytes, uint64_t seed, hipStream_t s);
 // One-launch small tree (kernels.hip k_small_tree): desc = n (offset, length)
 // u64 pairs, value i at vals + offset (16-byte aligned); out receives
-// the nodes (level-major) and, at out + img_at (16-byte aligned), the Serialize
+// the nodes (level-major) and, at out + img_at (16-byte aligned; 0 = none), the Serialize
 // image.  scratch: 20 n device bytes; ticket: one device u32, zero before the
 // first launch (each launch leaves it zero).
 constexpr uint32_t kSmallMaxN = 1024;

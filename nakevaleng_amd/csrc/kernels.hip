@@ -2111,7 +2111,7 @@ __device__ __forceinline__ void small_stage_in(const uint8_t* src, uint8_t* dst,
 // top level first: 0x00 + digest per node, one 0x01 after each odd level below
 // the top (merklenode.go:37-63, MERKLE_NODE_EMPTY :11), built kSmallSeg bytes
 // at a time in seg from whole node records clipped to the segment (as
-// k_bfs_image does).  Starts and ends at a workgroup barrier.
+// k_bfs_image does); img_at 0: no image.  Starts at a workgroup barrier.
 template <uint32_t B>
 __device__ __forceinline__ void small_levels_and_image(uint8_t* sm, uint8_t* seg, uint32_t n, uint8_t* out,
                                                        uint32_t img_at) {
@@ -2137,6 +2137,7 @@ __device__ __forceinline__ void small_levels_and_image(uint8_t* sm, uint8_t* seg
     NKV_STAMP(3);
     const uint32_t total = base + 1;
     small_copy_out<B>(sm, out, 20u * total);
+    if (img_at == 0u) return;  // the caller asked for no image (the nodes start at out + 0)
     uint32_t img_len = 0;
     for (int L = lv - 1; L >= 0; --L) {
         const uint32_t c = small_count(n, L);

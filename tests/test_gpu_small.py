@@ -281,3 +281,26 @@ def test_resident_service_across_idle_exits_and_contexts(nkv, oracle):
         for c in ctxs:
             c.close()
         assert time.perf_counter() - t0 < 5.0
+
+
+@pytest.mark.parametrize("mode", [1, 2, 3])
+def test_small_path_without_image(small_ctx, oracle, mode):
+    """A call that asks for no image (the mirrors' New: img_out NULL) gets the
+    same nodes and root, for shapes across the service's bound (256) and the
+    one-launch kernel's workgroup boundaries."""
+    _lib, ctx = small_ctx
+    ctx.set_option(_lib.NKV_OPT_SMALL_PATH, mode)
+    L = _lib.lib()
+    for n in (1, 2, 10, 40, 255, 256, 257, 513, 1024):
+        base, off, ln = _values(n, 77 + n, maxlen=300)
+        nodes_w, _ = _want(oracle, base, off, ln)
+        nodes = np.zeros((L.nkv_total_nodes(n), 20), np.uint8)
+        root = np.zeros(20, np.uint8)
+        _lib.check(L.nkv_tree_from_values(ctx.h, _lib.p8(base), _lib.p64(off), _lib.p64(ln), n, _lib.p8(root),
+                                          _lib.p8(nodes), None))
+        assert ctx.last_path() == _lib.NKV_PATH_SMALL
+        assert np.array_equal(nodes, nodes_w) and root.tobytes() == nodes_w[-1].tobytes(), n
+        root2 = np.zeros(20, np.uint8)
+        _lib.check(L.nkv_tree_from_values(ctx.h, _lib.p8(base), _lib.p64(off), _lib.p64(ln), n, _lib.p8(root2),
+                                          None, None))
+        assert root2.tobytes() == nodes_w[-1].tobytes(), n
