@@ -195,10 +195,10 @@ int nkv_ctx_last_path(nkv_ctx *ctx, int *path);
 int nkv_ctx_small_service_state(nkv_ctx *ctx, uint64_t out[6]);
 /* Diagnostics of the same service: enable = 1 makes it stamp the phases of
  * each following request; out (nullable) receives the latest traced request's
- * stamps, five (s_memrealtime at 100 MHz, s_memtime in shader clocks) pairs:
+ * stamps, seven (s_memrealtime at 100 MHz, s_memtime in shader clocks) pairs:
  * doorbell seen, input staged, leaves hashed, levels + image written,
- * completion stored. */
-int nkv_ctx_small_service_trace(nkv_ctx *ctx, int enable, uint64_t out[10]);
+ * completion stored, then levels done and first image segment built. */
+int nkv_ctx_small_service_trace(nkv_ctx *ctx, int enable, uint64_t out[14]);
 /* Timing (nkv_ctx_set_timing flags).  NKV_TIMING_EVENTS: the tree calls record
  * HIP events around the leaf kernel and the tree reduce on the context's
  * stream (and, for nkv_tree_from_values, around the upload and the download).

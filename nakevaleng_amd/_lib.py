@@ -298,8 +298,8 @@ class Context:
 
     def small_service_trace(self, enable: bool) -> list:
         """Turn the service's phase stamps on/off; returns the latest traced request's
-        five (s_memrealtime, s_memtime) pairs."""
-        a = (ctypes.c_uint64 * 10)()
+        seven (s_memrealtime, s_memtime) pairs (nkv_merkle.h)."""
+        a = (ctypes.c_uint64 * 14)()
         check(lib().nkv_ctx_small_service_trace(self.h, 1 if enable else 0, a))
         return list(a)
 

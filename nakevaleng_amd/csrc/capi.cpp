@@ -884,7 +884,7 @@ int nkv_ctx_small_service_state(nkv_ctx* c, uint64_t out[6]) try {
     return NKV_OK;
 } NKV_CATCH
 
-int nkv_ctx_small_service_trace(nkv_ctx* c, int enable, uint64_t out[10]) try {
+int nkv_ctx_small_service_trace(nkv_ctx* c, int enable, uint64_t out[14]) try {
     if (!c || enable < 0 || enable > 1) return NKV_ERR_INVALID;
     if (out) {
         for (int k = 0; k < kSvcStamps; ++k)

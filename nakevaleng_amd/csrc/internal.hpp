@@ -192,10 +192,11 @@ struct alignas(64) SmallMailbox {
     SmallRequest req;   // host: written before the doorbell
     // service, when traced: (s_memrealtime, s_memtime) after the doorbell was
     // seen, the input staged, the leaves hashed, the levels + image written,
-    // and the completion word stored
-    uint64_t stamps[10];
+    // the completion word stored; then after the levels, after the first image
+    // segment was built
+    uint64_t stamps[14];
 };
-constexpr int kSvcStamps = 10;
+constexpr int kSvcStamps = 14;
 // the service reads the request line as 16 dwords: [0] n, [1] vbytes, [2]
 // img_at, [3] trace, [4..5] desc, [6..7] vals, [8..9] out
 static_assert(offsetof(SmallMailbox, req) == 64 && sizeof(SmallRequest) == 64, "request line");

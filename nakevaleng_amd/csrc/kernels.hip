@@ -2114,8 +2114,18 @@ __device__ __forceinline__ void small_stage_in(const uint8_t* src, uint8_t* dst,
 // k_bfs_image does); img_at 0: no image.  Starts at a workgroup barrier.
 template <uint32_t B>
 __device__ __forceinline__ void small_levels_and_image(uint8_t* sm, uint8_t* seg, uint32_t n, uint8_t* out,
-                                                       uint32_t img_at) {
+                                                       uint32_t img_at, uint64_t* trace = nullptr) {
     const uint32_t tid = threadIdx.x;
+    // diagnostics (the service's traced requests): (s_memrealtime, s_memtime)
+    // into trace[2k], trace[2k + 1] by thread 0
+    auto mark = [&](int k) {
+        if (trace && tid == 0) {
+            __hip_atomic_store(trace + 2 * k, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(trace + 2 * k + 1, __builtin_amdgcn_s_memtime(), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    };
     __syncthreads();
     uint32_t cnt = n, base = 0;
     int lv = 1;
@@ -2135,15 +2145,19 @@ __device__ __forceinline__ void small_levels_and_image(uint8_t* sm, uint8_t* seg
         ++lv;
     } while (cnt > 1);
     NKV_STAMP(3);
+    mark(0);
     const uint32_t total = base + 1;
-    small_copy_out<B>(sm, out, 20u * total);
-    if (img_at == 0u) return;  // the caller asked for no image (the nodes start at out + 0)
+    if (img_at == 0u) {  // the caller asked for no image (the nodes start at out + 0)
+        small_copy_out<B>(sm, out, 20u * total);
+        return;
+    }
     uint32_t img_len = 0;
     for (int L = lv - 1; L >= 0; --L) {
         const uint32_t c = small_count(n, L);
         img_len += 21u * c + ((L < lv - 1 && (c & 1u)) ? 1u : 0u);
     }
-    __syncthreads();  // seg may still hold the staged input
+    // (seg's staged input was last read before the first level's barrier)
+    // The nodes leave with the first image segment, after it is built.
     for (uint32_t s0 = 0; s0 < img_len; s0 += kSmallSeg) {
         const uint32_t s1 = min(s0 + kSmallSeg, img_len);
         uint32_t A = 0;  // image offset of level L's first record
@@ -2170,8 +2184,12 @@ __device__ __forceinline__ void small_levels_and_image(uint8_t* sm, uint8_t* seg
             A = E + (pad ? 1u : 0u);
         }
         __syncthreads();
+        if (s0 == 0) {
+            mark(1);
+            small_copy_out<B>(sm, out, 20u * total);
+        }
         small_copy_out<B>(seg, out + img_at + s0, s1 - s0);
-        __syncthreads();
+        if (s1 < img_len) __syncthreads();  // seg is rebuilt for the next segment
     }
 }
 
@@ -2347,7 +2365,7 @@ __global__ __launch_bounds__(B) void k_small_service(SmallMailbox* __restrict__ 
                 __syncthreads();
                 if (tid == 0) stamp(2, __builtin_amdgcn_s_memrealtime(), __builtin_amdgcn_s_memtime());
             }
-            small_levels_and_image<B>(sm, seg, n, out, img_at);
+            small_levels_and_image<B>(sm, seg, n, out, img_at, traced ? mb->stamps + 10 : nullptr);
             if (traced && tid == 0) stamp(3, __builtin_amdgcn_s_memrealtime(), __builtin_amdgcn_s_memtime());
         }
         served = seq;

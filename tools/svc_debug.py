@@ -73,7 +73,9 @@ def main():
     if "--trace" in sys.argv:
         import json
         ctx.set_option(_lib.NKV_OPT_SMALL_PATH, 3)
-        for n, lo, hi in ((10, 1, 200), (40, 1, 200), (256, 1, 200)):
+        for n, lo, hi, with_img in ((10, 1, 200, False), (10, 1, 200, True), (40, 1, 200, True),
+                                    (256, 1, 200, True)):
+            img = np.zeros(L.nkv_bfs_size(n), np.uint8)
             ln = rng.integers(lo, hi + 1, n).astype(np.uint64)
             off = np.zeros(n, np.uint64)
             off[1:] = np.cumsum(ln[:-1])
@@ -84,15 +86,19 @@ def main():
             for _ in range(200):
                 t0 = time.perf_counter()
                 _lib.check(L.nkv_tree_from_values(ctx.h, _lib.p8(base), _lib.p64(off), _lib.p64(ln), n,
-                                                  _lib.p8(root), None, None))
+                                                  _lib.p8(root), None, _lib.p8(img) if with_img else None))
                 walls.append((time.perf_counter() - t0) * 1e6)
                 st.append(ctx.small_service_trace(True))
             ctx.small_service_trace(False)
             a = np.array(st[20:], np.float64)
             rt, mt = a[:, 0::2], a[:, 1::2]
-            out = {"n": n, "value_bytes": [lo, hi], "wall_us_median": round(float(np.median(walls[20:])), 2)}
-            for name, j0, j1 in (("request_and_stage_in", 0, 1), ("leaves", 1, 2), ("levels_and_image", 2, 3),
-                                 ("signal", 3, 4), ("seen_to_signal", 0, 4)):
+            out = {"n": n, "value_bytes": [lo, hi], "image": with_img,
+                   "wall_us_median": round(float(np.median(walls[20:])), 2)}
+            phases = [("request_and_stage_in", 0, 1), ("leaves", 1, 2), ("levels_and_image", 2, 3),
+                      ("signal", 3, 4), ("seen_to_signal", 0, 4), ("levels", 2, 5)]
+            if rt[:, 6].min() > 0:  # an image was built
+                phases += [("image_build", 5, 6), ("copy_out", 6, 3)]
+            for name, j0, j1 in phases:
                 us = (rt[:, j1] - rt[:, j0]) / 100.0
                 ghz = (mt[:, j1] - mt[:, j0]) / np.maximum(rt[:, j1] - rt[:, j0], 1) * 100e6 / 1e9
                 out[name] = {"us_median": round(float(np.median(us)), 2), "ghz_median": round(float(np.median(ghz)), 3)}
