@@ -2158,30 +2158,54 @@ __device__ __forceinline__ void small_levels_and_image(uint8_t* sm, uint8_t* seg
     }
     // (seg's staged input was last read before the first level's barrier)
     // The nodes leave with the first image segment, after it is built.
+    // Every node record of the image is built by its own thread at once (all
+    // levels together): the thread finds its record's level from the top,
+    // loads the 20-byte digest as five LDS words and stores the 21 bytes, so
+    // no LDS load waits inside a byte loop (per-level, byte-by-byte copying
+    // cost 6 us for a 10-leaf tree, more than its four tree levels).
     for (uint32_t s0 = 0; s0 < img_len; s0 += kSmallSeg) {
         const uint32_t s1 = min(s0 + kSmallSeg, img_len);
-        uint32_t A = 0;  // image offset of level L's first record
-        for (int L = lv - 1; L >= 0; --L) {
-            const uint32_t c = small_count(n, L);
-            uint32_t ns = 0;  // node index of level L's first node
-            for (int j = 0; j < L; ++j) ns += small_count(n, j);
-            const uint32_t E = A + 21u * c;
-            const bool pad = L < lv - 1 && (c & 1u);
-            if (pad && E >= s0 && E < s1 && tid == 0) seg[E - s0] = NKV_MERKLE_NODE_EMPTY;
-            if (E > s0 && A < s1) {
-                const uint32_t k0 = s0 > A ? (s0 - A) / 21u : 0u;
-                const uint32_t k1 = (min(s1, E) - 1u - A) / 21u;  // last record with a byte in the segment
-                for (uint32_t k = k0 + tid; k <= k1; k += B) {
-                    const uint8_t* d = sm + 20u * (ns + k);
-                    const int32_t pos = int32_t(A + 21u * k) - int32_t(s0);
+        for (uint32_t r = tid; r < total; r += B) {
+            uint32_t A = 0, before = 0;  // image offset of level L's first record; records above it
+            int L = lv - 1;
+            uint32_t c = small_count(n, L);
+            while (r >= before + c) {
+                A += 21u * c + ((L < lv - 1 && (c & 1u)) ? 1u : 0u);
+                before += c;
+                --L;
+                c = small_count(n, L);
+            }
+            const uint32_t k = r - before;
+            uint32_t ns = 0;  // node index of level L's first node (levels stored bottom-up)
+            for (int jl = 0; jl < L; ++jl) ns += small_count(n, jl);
+            const uint32_t* d = reinterpret_cast<const uint32_t*>(sm + 20u * (ns + k));
+            uint32_t w[5];
 #pragma unroll
-                    for (int b = 0; b < 21; ++b) {
-                        const int32_t q = pos + b;
-                        if (q >= 0 && q < int32_t(kSmallSeg)) seg[q] = b == 0 ? 0u : d[b - 1];
-                    }
+            for (int q = 0; q < 5; ++q) w[q] = d[q];
+            const int32_t pos = int32_t(A + 21u * k) - int32_t(s0);
+            if (pos >= 0 && pos + 21 <= int32_t(s1 - s0)) {
+                seg[pos] = 0u;
+#pragma unroll
+                for (int b = 0; b < 20; ++b) seg[pos + 1 + b] = uint8_t(w[b >> 2] >> (8 * (b & 3)));
+            } else if (pos + 21 > 0 && pos < int32_t(s1 - s0)) {  // a record across a segment edge
+#pragma unroll
+                for (int b = 0; b < 21; ++b) {
+                    const int32_t qb = pos + b;
+                    if (qb >= 0 && qb < int32_t(s1 - s0)) seg[qb] = b == 0 ? 0u : uint8_t(w[(b - 1) >> 2] >> (8 * ((b - 1) & 3)));
                 }
             }
-            A = E + (pad ? 1u : 0u);
+        }
+        // the pads: one 0x01 after each odd level below the top, by thread L
+        if (tid + 1 < uint32_t(lv)) {
+            const int L = int(tid);
+            uint32_t A = 0;
+            for (int Lu = lv - 1; Lu > L; --Lu) {
+                const uint32_t cu = small_count(n, Lu);
+                A += 21u * cu + ((Lu < lv - 1 && (cu & 1u)) ? 1u : 0u);
+            }
+            const uint32_t c = small_count(n, L);
+            const uint32_t E = A + 21u * c;
+            if ((c & 1u) && E >= s0 && E < s1) seg[E - s0] = NKV_MERKLE_NODE_EMPTY;
         }
         __syncthreads();
         if (s0 == 0) {
