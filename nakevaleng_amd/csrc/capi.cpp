@@ -236,8 +236,8 @@ constexpr int64_t kSvcTimeoutUs = 10000000;  // a request unanswered this long (
 // (release: x86 keeps the stores in order and the service reads them after its
 // system-scope acquire), then a spin on `done`.  Each 256 polls look at the
 // service stream: a service that has left is started again.
-int small_service_call(nkv_ctx* c, const uint64_t* d_desc, const uint8_t* d_vals, uint32_t vbytes, uint32_t n,
-                       uint8_t* d_out, uint32_t img_at, uint32_t seq) {
+// The service's mailbox, its own input buffer and its stream (created once).
+int svc_buffers(nkv_ctx* c) {
     if (!c->h_mbox) {
         uint8_t* p = nullptr;
         size_t cap = 0;
@@ -245,10 +245,22 @@ int small_service_call(nkv_ctx* c, const uint64_t* d_desc, const uint8_t* d_vals
         memset(p, 0, sizeof(SmallMailbox));
         c->h_mbox = reinterpret_cast<SmallMailbox*>(p);
     }
+    if (!c->h_svc_in) {
+        size_t cap = 0;
+        TRY(grow_coherent(&c->h_svc_in, &cap, kSmallSeg));
+    }
     if (!c->svc) HIPTRY(hipStreamCreateWithFlags(&c->svc, hipStreamNonBlocking));
+    return NKV_OK;
+}
+
+int small_service_call(nkv_ctx* c, const uint64_t* d_desc, const uint8_t* d_vals, uint32_t vbytes, uint32_t n,
+                       uint8_t* d_out, uint32_t img_at, uint32_t seq, bool inline_in) {
+    TRY(svc_buffers(c));
     SmallMailbox* mb = c->h_mbox;
-    void* dmb = nullptr;
+    void *dmb = nullptr, *din = nullptr;
     HIPTRY(hipHostGetDevicePointer(&dmb, mb, 0));
+    HIPTRY(hipHostGetDevicePointer(&din, c->h_svc_in, 0));
+    const uint8_t* fixed_in = static_cast<const uint8_t*>(din);
     mb->req.n = n;
     mb->req.vbytes = vbytes;
     mb->req.img_at = img_at;
@@ -256,9 +268,10 @@ int small_service_call(nkv_ctx* c, const uint64_t* d_desc, const uint8_t* d_vals
     mb->req.desc = reinterpret_cast<uintptr_t>(d_desc);
     mb->req.vals = reinterpret_cast<uintptr_t>(d_vals);
     mb->req.out = reinterpret_cast<uintptr_t>(d_out);
+    mb->req.inline_in = inline_in ? 1u : 0u;
     __atomic_store_n(&mb->doorbell, seq, __ATOMIC_RELEASE);
     if (!c->svc_live) {
-        HIPTRY(launch_small_service(static_cast<SmallMailbox*>(dmb), kSvcIdleUs * 100, kSvcLifeUs * 100, c->svc));
+        HIPTRY(launch_small_service(static_cast<SmallMailbox*>(dmb), fixed_in, kSvcIdleUs * 100, kSvcLifeUs * 100, c->svc));
         c->svc_live = true;
         ++c->svc_launches;
     }
@@ -275,7 +288,7 @@ int small_service_call(nkv_ctx* c, const uint64_t* d_desc, const uint8_t* d_vals
                     if (__atomic_load_n(&mb->refused, __ATOMIC_ACQUIRE) == seq) return NKV_ERR_DEVICE;
                     break;
                 }
-                HIPTRY(launch_small_service(static_cast<SmallMailbox*>(dmb), kSvcIdleUs * 100, kSvcLifeUs * 100, c->svc));
+                HIPTRY(launch_small_service(static_cast<SmallMailbox*>(dmb), fixed_in, kSvcIdleUs * 100, kSvcLifeUs * 100, c->svc));
                 ++c->svc_launches;
             } else if (q != hipErrorNotReady) {
                 return st_at(q, "k_small_service", __FILE__, __LINE__);
@@ -303,6 +316,7 @@ void svc_stop(nkv_ctx* c) {
                 c->svc_live = false;
                 c->svc = nullptr;
                 c->h_mbox = nullptr;
+                c->h_svc_in = nullptr;
                 return;
             }
             usleep(50);
@@ -313,6 +327,8 @@ void svc_stop(nkv_ctx* c) {
     c->svc = nullptr;
     if (c->h_mbox) (void)hipHostFree(c->h_mbox);
     c->h_mbox = nullptr;
+    if (c->h_svc_in) (void)hipHostFree(c->h_svc_in);
+    c->h_svc_in = nullptr;
 }
 int small_tree(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint64_t* len, uint64_t n,
                uint8_t* root20, uint8_t* nodes_out, uint8_t* img_out, bool* taken) {
@@ -341,21 +357,32 @@ int small_tree(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint6
                     align16(hi) - lo <= std::min<uint64_t>(c->small_max_bytes, kSmallMaxExtent);
     const uint64_t adj = blk ? uint64_t(base - blk->p) : 0;
     for (uint64_t i = 0; in_place && i < n; ++i) in_place = ((adj + off[i]) & 15) == 0;
+    // the resident service: a request whose descriptors and values fit its own
+    // input buffer is packed there (a host copy of at most 16 KiB), so the
+    // service reads it with the request line instead of one round trip later,
+    // values in the arena included
+    const bool svc = c->small_path == 3 && n <= kSvcMaxN;
+    const bool svc_inline = svc && 16 * n + vbytes <= kSmallSeg;
+    if (svc_inline) {
+        in_place = false;
+        TRY(svc_buffers(c));
+    }
     const uint64_t vext = in_place ? align16(hi) - lo : vbytes;  // the values' extent
     const uint64_t in_bytes = 16 * n + (in_place ? 0 : vbytes);
     TRY(grow_coherent(&c->h_sin, &c->h_sin_cap, in_bytes));
+    uint8_t* const h_in = svc_inline ? c->h_svc_in : c->h_sin;
     TRY(grow_coherent(&c->h_sout, &c->h_sout_cap, out_bytes + 64));  // + the completion word
     const size_t small_cap = c->d_small.cap;
     TRY(grow(c->d_small, 64 + 20 * kSmallMaxN));
     if (c->d_small.cap != small_cap) HIPTRY(hipMemsetAsync(c->d_small.p, 0, 64, c->stream));  // the ticket
-    uint64_t* desc = reinterpret_cast<uint64_t*>(c->h_sin);
+    uint64_t* desc = reinterpret_cast<uint64_t*>(h_in);
     if (in_place) {
         for (uint64_t i = 0; i < n; ++i) {
             desc[2 * i] = adj + off[i] - lo;
             desc[2 * i + 1] = len[i];
         }
     } else {
-        uint8_t* vals = c->h_sin + 16 * n;
+        uint8_t* vals = h_in + 16 * n;
         uint64_t p = 0;
         for (uint64_t i = 0; i < n; ++i) {
             desc[2 * i] = p;
@@ -370,15 +397,15 @@ int small_tree(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint6
     uint32_t seq = ++c->small_seq;
     if (seq == 0 || seq == kSvcExit) seq = c->small_seq = 1;  // 0 is the word's cleared state
     *hdone = 0;
-    if (c->small_path == 3 && n <= kSvcMaxN) {  // the resident service: no launch, no runtime completion
+    if (svc) {  // the resident service: no launch, no runtime completion
         void *din = nullptr, *dout = nullptr, *dblk = nullptr;
-        HIPTRY(hipHostGetDevicePointer(&din, c->h_sin, 0));
+        HIPTRY(hipHostGetDevicePointer(&din, h_in, 0));
         HIPTRY(hipHostGetDevicePointer(&dout, c->h_sout, 0));
         if (in_place) HIPTRY(hipHostGetDevicePointer(&dblk, blk->p, 0));
         const uint8_t* d_vals = in_place ? static_cast<const uint8_t*>(dblk) + lo
                                          : static_cast<const uint8_t*>(din) + 16 * n;
         TRY(small_service_call(c, static_cast<const uint64_t*>(din), d_vals, uint32_t(vext), uint32_t(n),
-                               static_cast<uint8_t*>(dout), uint32_t(img_at), seq));
+                               static_cast<uint8_t*>(dout), uint32_t(img_at), seq, svc_inline));
     } else if (c->small_path == 2) {  // through HBM: one copy in, one launch, one copy out
         TRY(grow(c->d_sin, in_bytes));
         TRY(grow(c->d_sout, out_bytes));

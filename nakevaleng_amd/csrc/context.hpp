@@ -212,6 +212,7 @@ struct nkv_ctx {
     // on first use; the kernel leaves after kSvcIdleUs without a request or at
     // nkv_ctx_destroy)
     nkv::SmallMailbox* h_mbox = nullptr;
+    uint8_t* h_svc_in = nullptr;  // the service's own input buffer (kSmallSeg bytes, host-coherent)
     hipStream_t svc = nullptr;
     bool svc_live = false;   // a service launch was made and may still run
     bool svc_trace = false;  // nkv_ctx_small_service_trace: stamp each request's phases

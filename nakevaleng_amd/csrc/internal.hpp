@@ -168,6 +168,7 @@ hipError_t launch_fill(uint8_t* buf, uint64_t nbytes, uint64_t seed, hipStream_t
 // image.  scratch: 20 n device bytes; ticket: one device u32, zero before the
 // first launch (each launch leaves it zero).
 constexpr uint32_t kSmallMaxN = 1024;
+constexpr uint32_t kSmallSeg = 16384;  // LDS stage: the staged input, then image segments
 // vbytes: the values lie in vals[0, vbytes).  done (nullable, host-coherent
 // memory): receives seq once every output byte is written.
 hipError_t launch_small_tree(const uint64_t* desc, const uint8_t* vals, uint32_t vbytes, uint32_t n, uint8_t* out,
@@ -181,7 +182,10 @@ hipError_t launch_small_tree(const uint64_t* desc, const uint8_t* vals, uint32_t
 struct alignas(64) SmallRequest {  // one 64-byte line: the service reads it with ONE load
     uint32_t n, vbytes, img_at, trace;  // trace: nonzero = stamp this request's phases
     uint64_t desc, vals, out;           // device addresses of host-coherent memory
-    uint64_t pad[2];
+    uint32_t inline_in;                 // 1: descriptors + values packed at the service's own
+                                        // input buffer (its first kSvcSpec bytes come with the request)
+    uint32_t pad0;
+    uint64_t pad1;
 };
 struct alignas(64) SmallMailbox {
     uint32_t doorbell;  // host: seq of the latest request; kSvcExit: leave
@@ -198,15 +202,18 @@ struct alignas(64) SmallMailbox {
 };
 constexpr int kSvcStamps = 14;
 // the service reads the request line as 16 dwords: [0] n, [1] vbytes, [2]
-// img_at, [3] trace, [4..5] desc, [6..7] vals, [8..9] out
+// img_at, [3] trace, [4..5] desc, [6..7] vals, [8..9] out, [10] inline_in
 static_assert(offsetof(SmallMailbox, req) == 64 && sizeof(SmallRequest) == 64, "request line");
 static_assert(offsetof(SmallRequest, desc) == 16 && offsetof(SmallRequest, vals) == 24 &&
-                  offsetof(SmallRequest, out) == 32,
+                  offsetof(SmallRequest, out) == 32 && offsetof(SmallRequest, inline_in) == 40,
               "request dwords");
 constexpr uint32_t kSvcExit = 0xFFFFFFFFu;
 constexpr uint32_t kSvcBlock = 256;  // one workgroup, one lane per leaf
 constexpr uint32_t kSvcMaxN = 256;   // larger batches take the one-launch kernel
-hipError_t launch_small_service(SmallMailbox* mb, uint64_t idle_ticks, uint64_t life_ticks, hipStream_t s);
+constexpr uint32_t kSvcSpec = 16 * kSvcBlock;  // input bytes read together with the request line
+// in: the service's own input buffer (host-coherent, kSmallSeg bytes)
+hipError_t launch_small_service(SmallMailbox* mb, const uint8_t* in, uint64_t idle_ticks, uint64_t life_ticks,
+                                hipStream_t s);
 // Clock probe of the leaf kernels on the current device (NKV_TIMING_CLOCK):
 // p = kClockWords u64 (8 slots of 32: shader-clock cycles, 100 MHz ticks, waves;
 // zeroed by the caller) or nullptr to switch it off.

@@ -2043,7 +2043,6 @@ __global__ __launch_bounds__(kBlock) void k_fill(uint8_t* __restrict__ buf, uint
 // gets without opting in.
 
 constexpr uint32_t kSmallBlock = 256;
-constexpr uint32_t kSmallSeg = 16384;  // image bytes built in LDS per pass
 
 // SHA-1 of p[0, len), p 16-byte aligned, one block of register lookahead
 __device__ __forceinline__ void sha1_value_aligned(const uint8_t* p, uint64_t len, uint32_t h[5]) {
@@ -2299,8 +2298,8 @@ __global__ __launch_bounds__(kSmallBlock) void k_small_tree(const uint64_t* __re
 // life_ticks (the host relaunches on its next call), so the grid always drains
 // and work queued behind it on a shared hardware queue waits a bounded time.
 template <uint32_t B>
-__global__ __launch_bounds__(B) void k_small_service(SmallMailbox* __restrict__ mb, uint64_t idle_ticks,
-                                                     uint64_t life_ticks) {
+__global__ __launch_bounds__(B) void k_small_service(SmallMailbox* __restrict__ mb, const uint8_t* __restrict__ fixed_in,
+                                                     uint64_t idle_ticks, uint64_t life_ticks) {
     __shared__ __attribute__((aligned(16))) uint8_t sm[20 * (2 * kSvcMaxN - 1) + 12];
     __shared__ __attribute__((aligned(16))) uint8_t seg[kSmallSeg];
     __shared__ uint32_t cmd;
@@ -2341,17 +2340,20 @@ __global__ __launch_bounds__(B) void k_small_service(SmallMailbox* __restrict__ 
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: the request's bytes
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (bell != kSvcExit) {
-                // the request line in one load (16 lanes, one dword each): one
-                // PCIe round trip for every field
-                const uint32_t* rl = reinterpret_cast<const uint32_t*>(&mb->req);
-                if (tid < 16) rq[tid] = __hip_atomic_load(rl + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            }
             if (tid == 0) cmd = bell;
         }
         __syncthreads();
         const uint32_t seq = __builtin_amdgcn_readfirstlane(cmd);
         if (seq == kSvcExit) break;
+        // One PCIe round trip for the request: the request line (16 lanes of
+        // wave 0, one dword each) and, speculatively, the first kSvcSpec bytes
+        // of the service's input buffer (16 per thread), all in flight at once;
+        // a request packed there (inline_in) needs no second trip below 4 KiB.
+        const uint4 spec = reinterpret_cast<const uint4*>(fixed_in)[tid];
+        if (tid < 16)
+            rq[tid] = __hip_atomic_load(reinterpret_cast<const uint32_t*>(&mb->req) + tid, __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_SYSTEM);
+        __syncthreads();
         // readfirstlane returns an int: widen through uint32_t, or a low word
         // with its top bit set sign-extends into the pointer's high word (the
         // first build of this read faulted on exactly that)
@@ -2364,6 +2366,7 @@ __global__ __launch_bounds__(B) void k_small_service(SmallMailbox* __restrict__ 
         const uint64_t* desc = reinterpret_cast<const uint64_t*>(rq64(4));
         const uint8_t* vals = reinterpret_cast<const uint8_t*>(rq64(6));
         uint8_t* out = reinterpret_cast<uint8_t*>(rq64(8));
+        const bool inline_in = rq32(10) != 0u;
         if (traced && tid == 0) stamp(0, seen_rt, seen_mt);
         // the host never rings with other values; a request out of range is
         // refused (flagged, nothing read or written) rather than followed
@@ -2372,7 +2375,15 @@ __global__ __launch_bounds__(B) void k_small_service(SmallMailbox* __restrict__ 
                             reinterpret_cast<uintptr_t>(out) | img_at) & 15u) == 0u;
         if (!sane && tid == 0) __hip_atomic_store(&mb->refused, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if (sane) {
-            if (16u * n + vbytes <= kSmallSeg) {
+            const uint32_t in_bytes = 16u * n + vbytes;
+            if (inline_in && in_bytes <= kSmallSeg) {  // descriptors + values at fixed_in, packed
+                if (16u * tid < in_bytes) reinterpret_cast<uint4*>(seg)[tid] = spec;
+                if (in_bytes > kSvcSpec)
+                    small_stage_in<B>(fixed_in + kSvcSpec, seg + kSvcSpec, in_bytes - kSvcSpec);
+                __syncthreads();
+                desc = reinterpret_cast<const uint64_t*>(seg);
+                vals = seg + 16u * n;
+            } else if (in_bytes <= kSmallSeg) {
                 small_stage_in<B>(reinterpret_cast<const uint8_t*>(desc), seg, 16u * n);
                 small_stage_in<B>(vals, seg + 16u * n, vbytes);
                 __syncthreads();
@@ -2417,8 +2428,11 @@ hipError_t launch_small_tree(const uint64_t* desc, const uint8_t* vals, uint32_t
     return hipGetLastError();
 }
 
-hipError_t launch_small_service(SmallMailbox* mb, uint64_t idle_ticks, uint64_t life_ticks, hipStream_t s) {
-    hipLaunchKernelGGL(k_small_service<kSvcBlock>, dim3(1), dim3(kSvcBlock), 0, s, mb, idle_ticks, life_ticks);
+hipError_t launch_small_service(SmallMailbox* mb, const uint8_t* in, uint64_t idle_ticks, uint64_t life_ticks,
+                                hipStream_t s) {
+    if (!mb || !in || (reinterpret_cast<uintptr_t>(in) & 15u)) return hipErrorInvalidValue;
+    static_assert(kSvcSpec <= kSmallSeg, "speculative read inside the input buffer");
+    hipLaunchKernelGGL(k_small_service<kSvcBlock>, dim3(1), dim3(kSvcBlock), 0, s, mb, in, idle_ticks, life_ticks);
     return hipGetLastError();
 }
 
