@@ -5,7 +5,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-O=gpurun_out/r06f
+O=gpurun_out/${OUT:-r06f}
 mkdir -p $O
 timeout -k 5 90 python3 -u tools/svc_debug.py --limit 75 --sizes 1,2,3,10,100,256,257,1000 > $O/svc_probe.txt 2>&1 \
     || { cat $O/svc_probe.txt; exit 1; }
