@@ -369,7 +369,7 @@ int small_tree(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint6
     }
     const uint64_t vext = in_place ? align16(hi) - lo : vbytes;  // the values' extent
     const uint64_t in_bytes = 16 * n + (in_place ? 0 : vbytes);
-    TRY(grow_coherent(&c->h_sin, &c->h_sin_cap, in_bytes));
+    if (!svc_inline) TRY(grow_coherent(&c->h_sin, &c->h_sin_cap, in_bytes));
     uint8_t* const h_in = svc_inline ? c->h_svc_in : c->h_sin;
     TRY(grow_coherent(&c->h_sout, &c->h_sout_cap, out_bytes + 64));  // + the completion word
     const size_t small_cap = c->d_small.cap;

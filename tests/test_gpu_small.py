@@ -283,6 +283,53 @@ def test_resident_service_across_idle_exits_and_contexts(nkv, oracle):
         assert time.perf_counter() - t0 < 5.0
 
 
+@pytest.mark.parametrize("in_arena", [False, True])
+def test_resident_service_inline_bound(small_ctx, oracle, in_arena):
+    """The service takes a request whose descriptors and values fit its own
+    16 KiB input buffer (16 n + the 16-byte aligned value bytes <= 16384) with
+    the request line, and any other one from the staging buffer -- or, for
+    values at aligned places in a coherent arena block, where they lie.  Shapes
+    on both sides of that bound and of the service's 256-value bound, plain
+    host values and arena values: every tree bit-exact."""
+    _lib, ctx = small_ctx
+    L = _lib.lib()
+    ctx.set_option(_lib.NKV_OPT_SMALL_PATH, 3)
+    cap = 1 << 20
+    p = ctypes.c_void_p()
+    if in_arena:
+        _lib.check(L.nkv_host_alloc(ctx.h, cap, ctypes.byref(p)))
+    try:
+        # (n, value length): 16 n + n * align16(len) just at, just over, well over 16 KiB
+        shapes = [(256, 48), (256, 47), (255, 48), (256, 49), (10, 1615), (10, 1616), (10, 1617), (10, 1632),
+                  (1, 16368), (1, 16369), (40, 4096), (257, 16), (1, 0), (256, 0)]
+        for k, (n, each) in enumerate(shapes):
+            rng = np.random.default_rng(900 + k)
+            ln = np.full(n, each, np.uint64)
+            off = np.zeros(n, np.uint64)
+            off[1:] = np.cumsum((ln[:-1] + 15) // 16 * 16)  # 16-byte aligned places
+            total = int(off[-1] + ln[-1]) + 1
+            if in_arena:
+                assert total <= cap
+                buf = np.ctypeslib.as_array((ctypes.c_uint8 * cap).from_address(p.value))
+                buf[:total] = np.frombuffer(rng.bytes(total), np.uint8)
+                base_ptr = ctypes.cast(p, _lib._u8p)
+                base = buf[:total].copy()
+            else:
+                base = np.frombuffer(rng.bytes(total), np.uint8).copy()
+                base_ptr = _lib.p8(base)
+            nodes_w, img_w = _want(oracle, base, off, ln)
+            root = np.zeros(20, np.uint8)
+            nodes = np.zeros((L.nkv_total_nodes(n), 20), np.uint8)
+            img = np.zeros(L.nkv_bfs_size(n), np.uint8)
+            _lib.check(L.nkv_tree_from_values(ctx.h, base_ptr, _lib.p64(off), _lib.p64(ln), n, _lib.p8(root),
+                                              _lib.p8(nodes), _lib.p8(img)))
+            assert ctx.last_path() == _lib.NKV_PATH_SMALL
+            assert np.array_equal(nodes, nodes_w) and img.tobytes() == img_w, (in_arena, n, each)
+    finally:
+        if in_arena:
+            _lib.check(L.nkv_host_free(ctx.h, p))
+
+
 @pytest.mark.parametrize("mode", [1, 2, 3])
 def test_small_path_without_image(small_ctx, oracle, mode):
     """A call that asks for no image (the mirrors' New: img_out NULL) gets the
