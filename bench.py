@@ -157,9 +157,10 @@ def parse(argv=None):
                          "small_flush = microseconds per flush at the reference's default sizes (10 values "
                          "<= 200 B) up to configs[0], GPU paths beside one host core (tools/small_flush.cpp)")
     ap.add_argument("--small-reps", type=int, default=300, help="small_flush: flushes per shape and mode")
-    ap.add_argument("--small-modes", default="1,3,2,0",
+    ap.add_argument("--small-modes", default="1,3,3h,2,0",
                     help="small_flush: NKV_OPT_SMALL_PATH modes to time (1 one launch over pinned memory, 3 the "
-                         "resident service, 2 one launch through HBM, 0 the grid path)")
+                         "resident service, 3h the same with its requests in host memory, 2 one launch through HBM, "
+                         "0 the grid path)")
     ap.add_argument("--api-cycles", type=int, default=4, help="api_flush: flushes per mode (the first allocates "
                                                               "the pinned arena)")
     ap.add_argument("--tables", type=int, default=0,
@@ -1218,7 +1219,8 @@ def main_api_flush(args):
     print(json.dumps(out), flush=True)
 
 
-SMALL_MODE_KEYS = ((1, "small_pinned"), (3, "small_resident"), (2, "small_hbm"), (0, "grid"))
+SMALL_MODE_KEYS = (("1", "small_pinned"), ("3", "small_resident"), ("3h", "small_resident_host_mailbox"),
+                   ("2", "small_hbm"), ("0", "grid"))
 # --config small_flush: (name, n, min value length, max value length); lengths
 # uniform in [min, max], seed SMALL_SEED (tools/small_flush.cpp's generator)
 SMALL_SEED = 0x6E616B67
@@ -1259,8 +1261,9 @@ def main_small_flush(args):
     through the C++ Go-API mirror (tools/small_flush.cpp: NewLeaf x n, New,
     Root.String(), the image; with the file write as well; and the bare C-ABI
     call), for each NKV_OPT_SMALL_PATH mode: 1 = the one-launch kernel over
-    pinned host memory (default), 2 = the one launch through HBM, 0 = the grid
-    path.  Beside each shape: the same flush in memory on one host core with the
+    pinned host memory (default), 3 = the resident service (3h: with its
+    requests in host memory, NKV_OPT_SERVICE_MAILBOX 1), 2 = the one launch
+    through HBM, 0 = the grid path.  Beside each shape: the same flush in memory on one host core with the
     portable SHA-1 and with OpenSSL's (oracle/, nkvo_flush_reps), whose root every
     GPU run must reproduce."""
     import subprocess
@@ -1271,9 +1274,9 @@ def main_small_flush(args):
     spec = [f"{n}:{lo}:{hi}:{SMALL_SEED:x}" for _, n, lo, hi in SMALL_SHAPES]
     gpu = {}
     with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
-        modes = [int(m) for m in args.small_modes.split(",") if m.strip()]
+        modes = [m.strip() for m in args.small_modes.split(",") if m.strip()]
         for mode in modes:
-            p = subprocess.run([exe, str(mode), str(args.small_reps), td] + spec, capture_output=True, text=True,
+            p = subprocess.run([exe, mode, str(args.small_reps), td] + spec, capture_output=True, text=True,
                                timeout=600)
             if p.returncode != 0:
                 raise SystemExit(f"small_flush mode {mode} failed: {p.stderr[-2000:]}")

@@ -182,6 +182,14 @@ int nkv_ctx_sync(nkv_ctx *ctx);
 #define NKV_OPT_QUEUE_PAIR 19 /* retired (ABI version 1): 0 is the only value accepted (one wave per
                                  work-queue group; the two-wave pair kernel of round 5 was removed
                                  after failing its first GPU parity run) */
+#define NKV_OPT_SERVICE_MAILBOX 20 /* where the resident service (NKV_OPT_SMALL_PATH 3) takes its
+                                      requests: 0 (default) = the doorbell, the request line and
+                                      the packed input in fine-grained device memory the host
+                                      stores to directly, when the GPU has a large BAR (the service
+                                      polls and reads local memory; else as 1); 1 = in
+                                      host-coherent memory (the service polls across PCIe).
+                                      Answers always land in host memory.  A change stops a
+                                      running service; the next call starts it in the new form */
 int nkv_ctx_set_option(nkv_ctx *ctx, int key, int64_t value);
 /* Which path the latest host-buffer tree call of the context took */
 #define NKV_PATH_GRID 0  /* copies + leaf kernel + per-level reduce launches */
@@ -190,9 +198,10 @@ int nkv_ctx_last_path(nkv_ctx *ctx, int *path);
 /* The resident small-tree service of the context (NKV_OPT_SMALL_PATH 3), for
  * diagnostics: out[0] doorbell (latest request), out[1] served (the latest the
  * service took), out[2] done (the latest it answered), out[3] launches so far,
- * out[4] 1 while a launch may still run, out[5] 1 if its stream still has work.
+ * out[4] 1 while a launch may still run, out[5] 1 if its stream still has work,
+ * out[6] 1 if its requests go through device memory (NKV_OPT_SERVICE_MAILBOX).
  * All zero before the first request. */
-int nkv_ctx_small_service_state(nkv_ctx *ctx, uint64_t out[6]);
+int nkv_ctx_small_service_state(nkv_ctx *ctx, uint64_t out[7]);
 /* Diagnostics of the same service: enable = 1 makes it stamp the phases of
  * each following request; out (nullable) receives the latest traced request's
  * stamps, seven (s_memrealtime at 100 MHz, s_memtime in shader clocks) pairs:

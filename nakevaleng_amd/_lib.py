@@ -37,6 +37,7 @@ NKV_OPT_SMALL_MAX_BYTES = 16
 NKV_OPT_ARENA_COHERENT = 17
 NKV_OPT_SIDE_GATE = 18
 NKV_OPT_QUEUE_PAIR = 19  # retired: accepts only 0
+NKV_OPT_SERVICE_MAILBOX = 20
 NKV_PATH_GRID = 0
 NKV_PATH_SMALL = 1
 NKV_OPT_DEEP_PREFETCH = 3  # retired: accepts only 3
@@ -292,9 +293,9 @@ class Context:
 
     def small_service_state(self) -> dict:
         """The resident small-tree service's mailbox and launch state (diagnostics)."""
-        a = (ctypes.c_uint64 * 6)()
+        a = (ctypes.c_uint64 * 7)()
         check(lib().nkv_ctx_small_service_state(self.h, a))
-        return dict(zip(("doorbell", "served", "done", "launches", "live", "busy"), list(a)))
+        return dict(zip(("doorbell", "served", "done", "launches", "live", "busy", "mailbox_dev"), list(a)))
 
     def small_service_trace(self, enable: bool) -> list:
         """Turn the service's phase stamps on/off; returns the latest traced request's

@@ -25,7 +25,7 @@ FLAGS = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-pt
          "-Wall", "-Wno-unused-result"]
 # RCCL for the multi-GPU group (nkv_group_*: ncclCommInitAll, ncclAllGather)
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
-LIBS = [f"-L{ROCM}/lib", "-lrccl"]
+LIBS = [f"-L{ROCM}/lib", "-lrccl", "-lhsa-runtime64"]
 _ID = re.compile(rb"nkv-src-sha256:([0-9a-f]{64})")
 
 

@@ -6,6 +6,8 @@
 // NKV_ERR_DEVICE.
 #include <fcntl.h>
 #include <hip/hip_runtime.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
 #include <string.h>
 #include <unistd.h>
 
@@ -232,11 +234,31 @@ constexpr uint64_t kSvcIdleUs = 20000;   // the resident service leaves after th
 constexpr uint64_t kSvcLifeUs = 200000;  // ... or, between requests, once it has run this long
 constexpr int64_t kSvcTimeoutUs = 10000000;  // a request unanswered this long (service alive) is an error
 
-// One request to the resident service: the mailbox fields, then the doorbell
-// (release: x86 keeps the stores in order and the service reads them after its
-// system-scope acquire), then a spin on `done`.  Each 256 polls look at the
-// service stream: a service that has left is started again.
-// The service's mailbox, its own input buffer and its stream (created once).
+// Device memory the host may store to directly: fine-grained memory of a
+// large-BAR GPU is mapped into the host's address space at the address the GPU
+// uses (tools/bar_probe.hip on MI355X: hostBaseAddress == the pointer, host
+// stores and loads work, no grant needed).
+bool host_mapped(const void* p) {
+    hsa_amd_pointer_info_t info;
+    memset(&info, 0, sizeof info);
+    info.size = sizeof info;
+    if (hsa_amd_pointer_info(p, &info, nullptr, nullptr, nullptr) != HSA_STATUS_SUCCESS) return false;
+    return info.hostBaseAddress == p;
+}
+
+// Host stores to device memory through the BAR may be write-combined: drained
+// before the doorbell (the request's bytes land first: PCIe keeps posted writes
+// in order) and after it (so it leaves now, not when the buffer fills).
+inline void store_fence() { asm volatile("sfence" ::: "memory"); }
+
+// The service's mailbox, its input buffer and its stream (created on first
+// use, and again after svc_stop).  The answer side (served, done, refused,
+// stamps) is host-coherent memory, where the host spins.  The request side
+// (doorbell, request line) and the service's input buffer go, with
+// NKV_OPT_SERVICE_MAILBOX 0 on a large-BAR GPU, to fine-grained device memory
+// the host stores to: the service then polls and reads local memory instead of
+// crossing PCIe for each poll and for the input (tools/bar_probe.hip: a 4 KiB
+// request's round trip 7.7 -> 5.8 us); otherwise they share the host mailbox.
 int svc_buffers(nkv_ctx* c) {
     if (!c->h_mbox) {
         uint8_t* p = nullptr;
@@ -244,6 +266,21 @@ int svc_buffers(nkv_ctx* c) {
         TRY(grow_coherent(&p, &cap, sizeof(SmallMailbox)));
         memset(p, 0, sizeof(SmallMailbox));
         c->h_mbox = reinterpret_cast<SmallMailbox*>(p);
+        c->svc_box_dev = false;
+        int large = 0;
+        void* d = nullptr;
+        if (c->svc_mailbox == 0 && hipDeviceGetAttribute(&large, hipDeviceAttributeIsLargeBar, c->device) == hipSuccess &&
+            large && hipExtMallocWithFlags(&d, sizeof(SmallMailbox) + kSmallSeg, hipDeviceMallocFinegrained) == hipSuccess) {
+            if (host_mapped(d)) {
+                memset(d, 0, sizeof(SmallMailbox));  // doorbell 0 == served 0
+                store_fence();
+                c->d_svc_box = static_cast<uint8_t*>(d);
+                c->svc_box_dev = true;
+            } else {
+                (void)hipFree(d);
+            }
+        }
+        (void)hipGetLastError();
     }
     if (!c->h_svc_in) {
         size_t cap = 0;
@@ -253,25 +290,54 @@ int svc_buffers(nkv_ctx* c) {
     return NKV_OK;
 }
 
+// The request side as the host stores to it (the device's address too).
+SmallMailbox* svc_request_side(nkv_ctx* c) {
+    return c->svc_box_dev ? reinterpret_cast<SmallMailbox*>(c->d_svc_box) : c->h_mbox;
+}
+
+// One request to the resident service: an inline request's packed input
+// (descriptors + values at h_svc_in, in_bytes) moved to the device buffer when
+// that is where the service reads it, the request line, then the doorbell
+// (release: x86 keeps the stores in order; the fences drain a write-combined
+// mapping; the service reads them after its system-scope acquire), then a
+// spin on `done`.  Each 256 polls look at the service stream: a service that
+// has left is started again.
 int small_service_call(nkv_ctx* c, const uint64_t* d_desc, const uint8_t* d_vals, uint32_t vbytes, uint32_t n,
                        uint8_t* d_out, uint32_t img_at, uint32_t seq, bool inline_in) {
     TRY(svc_buffers(c));
     SmallMailbox* mb = c->h_mbox;
+    SmallMailbox* rb = svc_request_side(c);
     void *dmb = nullptr, *din = nullptr;
     HIPTRY(hipHostGetDevicePointer(&dmb, mb, 0));
-    HIPTRY(hipHostGetDevicePointer(&din, c->h_svc_in, 0));
+    const SmallMailbox* drb = c->svc_box_dev ? rb : static_cast<const SmallMailbox*>(dmb);
+    if (c->svc_box_dev) {
+        din = c->d_svc_box + sizeof(SmallMailbox);
+        if (inline_in) {
+            memcpy(din, c->h_svc_in, 16 * size_t(n) + vbytes);
+            d_desc = static_cast<const uint64_t*>(din);
+            d_vals = static_cast<const uint8_t*>(din) + 16 * size_t(n);
+        }
+    } else {
+        HIPTRY(hipHostGetDevicePointer(&din, c->h_svc_in, 0));
+    }
     const uint8_t* fixed_in = static_cast<const uint8_t*>(din);
-    mb->req.n = n;
-    mb->req.vbytes = vbytes;
-    mb->req.img_at = img_at;
-    mb->req.trace = c->svc_trace ? 1u : 0u;
-    mb->req.desc = reinterpret_cast<uintptr_t>(d_desc);
-    mb->req.vals = reinterpret_cast<uintptr_t>(d_vals);
-    mb->req.out = reinterpret_cast<uintptr_t>(d_out);
-    mb->req.inline_in = inline_in ? 1u : 0u;
-    __atomic_store_n(&mb->doorbell, seq, __ATOMIC_RELEASE);
+    SmallRequest r;
+    memset(&r, 0, sizeof r);
+    r.n = n;
+    r.vbytes = vbytes;
+    r.img_at = img_at;
+    r.trace = c->svc_trace ? 1u : 0u;
+    r.desc = reinterpret_cast<uintptr_t>(d_desc);
+    r.vals = reinterpret_cast<uintptr_t>(d_vals);
+    r.out = reinterpret_cast<uintptr_t>(d_out);
+    r.inline_in = inline_in ? 1u : 0u;
+    memcpy(&rb->req, &r, sizeof r);
+    if (c->svc_box_dev) store_fence();
+    __atomic_store_n(&rb->doorbell, seq, __ATOMIC_RELEASE);
+    if (c->svc_box_dev) store_fence();
     if (!c->svc_live) {
-        HIPTRY(launch_small_service(static_cast<SmallMailbox*>(dmb), fixed_in, kSvcIdleUs * 100, kSvcLifeUs * 100, c->svc));
+        HIPTRY(launch_small_service(static_cast<SmallMailbox*>(dmb), drb, fixed_in, kSvcIdleUs * 100, kSvcLifeUs * 100,
+                                    c->svc));
         c->svc_live = true;
         ++c->svc_launches;
     }
@@ -288,7 +354,8 @@ int small_service_call(nkv_ctx* c, const uint64_t* d_desc, const uint8_t* d_vals
                     if (__atomic_load_n(&mb->refused, __ATOMIC_ACQUIRE) == seq) return NKV_ERR_DEVICE;
                     break;
                 }
-                HIPTRY(launch_small_service(static_cast<SmallMailbox*>(dmb), fixed_in, kSvcIdleUs * 100, kSvcLifeUs * 100, c->svc));
+                HIPTRY(launch_small_service(static_cast<SmallMailbox*>(dmb), drb, fixed_in, kSvcIdleUs * 100,
+                                            kSvcLifeUs * 100, c->svc));
                 ++c->svc_launches;
             } else if (q != hipErrorNotReady) {
                 return st_at(q, "k_small_service", __FILE__, __LINE__);
@@ -301,11 +368,14 @@ int small_service_call(nkv_ctx* c, const uint64_t* d_desc, const uint8_t* d_vals
     return NKV_OK;
 }
 
-// Stop the resident service (nkv_ctx_destroy): the exit doorbell, then wait
-// for the kernel to leave.
+// Stop the resident service (nkv_ctx_destroy, a change of
+// NKV_OPT_SERVICE_MAILBOX): the exit doorbell, then wait for the kernel to
+// leave; its buffers are made again on the next request.
 void svc_stop(nkv_ctx* c) {
     if (c->svc_live && c->h_mbox) {
-        __atomic_store_n(&c->h_mbox->doorbell, kSvcExit, __ATOMIC_RELEASE);
+        SmallMailbox* rb = svc_request_side(c);
+        __atomic_store_n(&rb->doorbell, kSvcExit, __ATOMIC_RELEASE);
+        if (c->svc_box_dev) store_fence();
         // the service leaves at its next poll (or its idle timeout); never wait
         // unboundedly in a destructor: a service that has not left after 2 s
         // keeps its mailbox and stream (leaked) rather than hang the caller
@@ -317,6 +387,8 @@ void svc_stop(nkv_ctx* c) {
                 c->svc = nullptr;
                 c->h_mbox = nullptr;
                 c->h_svc_in = nullptr;
+                c->d_svc_box = nullptr;
+                c->svc_box_dev = false;
                 return;
             }
             usleep(50);
@@ -329,6 +401,9 @@ void svc_stop(nkv_ctx* c) {
     c->h_mbox = nullptr;
     if (c->h_svc_in) (void)hipHostFree(c->h_svc_in);
     c->h_svc_in = nullptr;
+    if (c->d_svc_box) (void)hipFree(c->d_svc_box);
+    c->d_svc_box = nullptr;
+    c->svc_box_dev = false;
 }
 int small_tree(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint64_t* len, uint64_t n,
                uint8_t* root20, uint8_t* nodes_out, uint8_t* img_out, bool* taken) {
@@ -879,6 +954,14 @@ int nkv_ctx_set_option(nkv_ctx* c, int key, int64_t value) try {
             if (value < 0 || value > 1) return NKV_ERR_INVALID;
             c->side_gate = int(value);
             return NKV_OK;
+        case NKV_OPT_SERVICE_MAILBOX:
+            if (value < 0 || value > 1) return NKV_ERR_INVALID;
+            if (int(value) != c->svc_mailbox) {
+                TRY(bind(c));
+                svc_stop(c);  // the next request makes the buffers in the new place
+                c->svc_mailbox = int(value);
+            }
+            return NKV_OK;
         case NKV_OPT_QUEUE_PAIR:  // retired: one wave per group (the pair kernel failed its GPU parity run)
             return value == 0 ? NKV_OK : NKV_ERR_INVALID;
         case NKV_OPT_SMALL_MAX_BYTES:
@@ -894,11 +977,12 @@ int nkv_ctx_set_option(nkv_ctx* c, int key, int64_t value) try {
     }
 } NKV_CATCH
 
-int nkv_ctx_small_service_state(nkv_ctx* c, uint64_t out[6]) try {
+int nkv_ctx_small_service_state(nkv_ctx* c, uint64_t out[7]) try {
     if (!c || !out) return NKV_ERR_INVALID;
-    for (int k = 0; k < 6; ++k) out[k] = 0;
+    for (int k = 0; k < 7; ++k) out[k] = 0;
     if (c->h_mbox) {
-        out[0] = __atomic_load_n(&c->h_mbox->doorbell, __ATOMIC_ACQUIRE);
+        out[0] = __atomic_load_n(&svc_request_side(c)->doorbell, __ATOMIC_ACQUIRE);
+        out[6] = c->svc_box_dev ? 1u : 0u;
         out[1] = __atomic_load_n(&c->h_mbox->served, __ATOMIC_ACQUIRE);
         out[2] = __atomic_load_n(&c->h_mbox->done, __ATOMIC_ACQUIRE);
     }

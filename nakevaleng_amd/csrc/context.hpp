@@ -212,7 +212,13 @@ struct nkv_ctx {
     // on first use; the kernel leaves after kSvcIdleUs without a request or at
     // nkv_ctx_destroy)
     nkv::SmallMailbox* h_mbox = nullptr;
-    uint8_t* h_svc_in = nullptr;  // the service's own input buffer (kSmallSeg bytes, host-coherent)
+    uint8_t* h_svc_in = nullptr;  // host packing buffer of an inline request (kSmallSeg bytes, host-coherent)
+    // NKV_OPT_SERVICE_MAILBOX 0 on a large-BAR GPU: the request side (doorbell,
+    // request line) and the service's input buffer in fine-grained device memory
+    // the host stores to directly (one block: the mailbox, then kSmallSeg bytes)
+    uint8_t* d_svc_box = nullptr;
+    int svc_mailbox = 0;      // NKV_OPT_SERVICE_MAILBOX
+    bool svc_box_dev = false; // the live buffers are d_svc_box's (else h_mbox / h_svc_in)
     hipStream_t svc = nullptr;
     bool svc_live = false;   // a service launch was made and may still run
     bool svc_trace = false;  // nkv_ctx_small_service_trace: stamp each request's phases

@@ -175,10 +175,12 @@ hipError_t launch_small_tree(const uint64_t* desc, const uint8_t* vals, uint32_t
                              uint32_t img_at, uint8_t* scratch, unsigned int* ticket, unsigned int* done, uint32_t seq,
                              hipStream_t s);
 // The resident small-tree service (kernels.hip k_small_service,
-// NKV_OPT_SMALL_PATH 3): its mailbox lives in host-coherent pinned memory.
-// The host writes a request (the fields after `done`, as launch_small_tree's
-// arguments) and then its seq into `doorbell`; the service answers with seq
-// in `done` behind every output byte.
+// NKV_OPT_SMALL_PATH 3).  The host writes a request (the fields after `done`,
+// as launch_small_tree's arguments) and then its seq into `doorbell`; the
+// service answers with seq in `done` behind every output byte.  Two copies of
+// the struct may be in play: the request side (doorbell, req) in device memory
+// the host stores to through a large BAR, the answer side (served, done,
+// refused, stamps) in host-coherent memory; or one host-coherent copy for both.
 struct alignas(64) SmallRequest {  // one 64-byte line: the service reads it with ONE load
     uint32_t n, vbytes, img_at, trace;  // trace: nonzero = stamp this request's phases
     uint64_t desc, vals, out;           // device addresses of host-coherent memory
@@ -211,9 +213,11 @@ constexpr uint32_t kSvcExit = 0xFFFFFFFFu;
 constexpr uint32_t kSvcBlock = 256;  // one workgroup, one lane per leaf
 constexpr uint32_t kSvcMaxN = 256;   // larger batches take the one-launch kernel
 constexpr uint32_t kSvcSpec = 16 * kSvcBlock;  // input bytes read together with the request line
-// in: the service's own input buffer (host-coherent, kSmallSeg bytes)
-hipError_t launch_small_service(SmallMailbox* mb, const uint8_t* in, uint64_t idle_ticks, uint64_t life_ticks,
-                                hipStream_t s);
+// mb: the answer side (served, done, refused, stamps; host-coherent); rb: the
+// request side (doorbell, req): device memory the host maps (a large BAR) or
+// mb itself; in: the service's own input buffer (kSmallSeg bytes, beside rb)
+hipError_t launch_small_service(SmallMailbox* mb, const SmallMailbox* rb, const uint8_t* in, uint64_t idle_ticks,
+                                uint64_t life_ticks, hipStream_t s);
 // Clock probe of the leaf kernels on the current device (NKV_TIMING_CLOCK):
 // p = kClockWords u64 (8 slots of 32: shader-clock cycles, 100 MHz ticks, waves;
 // zeroed by the caller) or nullptr to switch it off.

@@ -2285,9 +2285,14 @@ __global__ __launch_bounds__(kSmallBlock) void k_small_tree(const uint64_t* __re
 
 // The resident small-tree service (NKV_OPT_SMALL_PATH 3): ONE workgroup of
 // kSvcBlock threads stays on the GPU between calls and serves one request of at
-// most kSvcMaxN leaves at a time from a host-coherent mailbox, so a default-size flush pays neither a
+// most kSvcMaxN leaves at a time from a mailbox, so a default-size flush pays neither a
 // launch nor the runtime's completion path ("The
-// small-flush floor").  Thread 0 polls the doorbell across PCIe (relaxed
+// small-flush floor").  The request side (rb: doorbell, request line; fixed_in:
+// the service's own input buffer) lies in device memory the host stores to
+// directly on a large-BAR GPU, else in host-coherent memory with the rest of
+// the mailbox (rb == mb; NKV_OPT_SERVICE_MAILBOX); the answer side (mb: served,
+// done, refused, stamps) is always host-coherent, where the host spins on it.
+// Wave 0 polls the doorbell (relaxed
 // system-scope loads, s_sleep between polls); a new seq is acquired at system
 // scope, the request (the same descriptors, values and output layout
 // k_small_tree takes) is served exactly as k_small_tree serves a one-workgroup
@@ -2298,8 +2303,9 @@ __global__ __launch_bounds__(kSmallBlock) void k_small_tree(const uint64_t* __re
 // life_ticks (the host relaunches on its next call), so the grid always drains
 // and work queued behind it on a shared hardware queue waits a bounded time.
 template <uint32_t B>
-__global__ __launch_bounds__(B) void k_small_service(SmallMailbox* __restrict__ mb, const uint8_t* __restrict__ fixed_in,
-                                                     uint64_t idle_ticks, uint64_t life_ticks) {
+__global__ __launch_bounds__(B) void k_small_service(SmallMailbox* __restrict__ mb, const SmallMailbox* rb,
+                                                     const uint8_t* __restrict__ fixed_in, uint64_t idle_ticks,
+                                                     uint64_t life_ticks) {
     __shared__ __attribute__((aligned(16))) uint8_t sm[20 * (2 * kSvcMaxN - 1) + 12];
     __shared__ __attribute__((aligned(16))) uint8_t seg[kSmallSeg];
     __shared__ uint32_t cmd;
@@ -2327,7 +2333,7 @@ __global__ __launch_bounds__(B) void k_small_service(SmallMailbox* __restrict__ 
             uint32_t bell;
             while (true) {
                 bell = __builtin_amdgcn_readfirstlane(
-                    __hip_atomic_load(&mb->doorbell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+                    __hip_atomic_load(&rb->doorbell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
                 seen_rt = __builtin_amdgcn_s_memrealtime();
                 seen_mt = __builtin_amdgcn_s_memtime();
                 if (bell != served) break;
@@ -2351,7 +2357,7 @@ __global__ __launch_bounds__(B) void k_small_service(SmallMailbox* __restrict__ 
         // a request packed there (inline_in) needs no second trip below 4 KiB.
         const uint4 spec = reinterpret_cast<const uint4*>(fixed_in)[tid];
         if (tid < 16)
-            rq[tid] = __hip_atomic_load(reinterpret_cast<const uint32_t*>(&mb->req) + tid, __ATOMIC_RELAXED,
+            rq[tid] = __hip_atomic_load(reinterpret_cast<const uint32_t*>(&rb->req) + tid, __ATOMIC_RELAXED,
                                         __HIP_MEMORY_SCOPE_SYSTEM);
         __syncthreads();
         // readfirstlane returns an int: widen through uint32_t, or a low word
@@ -2428,11 +2434,12 @@ hipError_t launch_small_tree(const uint64_t* desc, const uint8_t* vals, uint32_t
     return hipGetLastError();
 }
 
-hipError_t launch_small_service(SmallMailbox* mb, const uint8_t* in, uint64_t idle_ticks, uint64_t life_ticks,
-                                hipStream_t s) {
-    if (!mb || !in || (reinterpret_cast<uintptr_t>(in) & 15u)) return hipErrorInvalidValue;
+hipError_t launch_small_service(SmallMailbox* mb, const SmallMailbox* rb, const uint8_t* in, uint64_t idle_ticks,
+                                uint64_t life_ticks, hipStream_t s) {
+    if (!mb || !rb || !in || (reinterpret_cast<uintptr_t>(in) & 15u)) return hipErrorInvalidValue;
     static_assert(kSvcSpec <= kSmallSeg, "speculative read inside the input buffer");
-    hipLaunchKernelGGL(k_small_service<kSvcBlock>, dim3(1), dim3(kSvcBlock), 0, s, mb, in, idle_ticks, life_ticks);
+    hipLaunchKernelGGL(k_small_service<kSvcBlock>, dim3(1), dim3(kSvcBlock), 0, s, mb, rb, in, idle_ticks,
+                       life_ticks);
     return hipGetLastError();
 }
 

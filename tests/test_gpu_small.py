@@ -256,17 +256,21 @@ def test_small_path_reads_the_arena_in_place(small_ctx, oracle, coherent):
         ctx.set_option(_lib.NKV_OPT_ARENA_COHERENT, 1)
 
 
-def test_resident_service_across_idle_exits_and_contexts(nkv, oracle):
+@pytest.mark.parametrize("mailbox", [0, 1])
+def test_resident_service_across_idle_exits_and_contexts(nkv, oracle, mailbox):
     """NKV_OPT_SMALL_PATH 3 (the resident service): requests right after each
     other, after the service has left on its idle timeout (20 ms) and been
     started again, on a second context at the same time, and a context
-    destroyed while its service waits -- every tree bit-exact."""
+    destroyed while its service waits -- every tree bit-exact, with the
+    requests in device memory the host stores to (NKV_OPT_SERVICE_MAILBOX 0, a
+    large-BAR GPU) and in host memory (1)."""
     import time
     _lib, _ = nkv
     ctxs = [_lib.Context(0), _lib.Context(0)]
     try:
         for c in ctxs:
             c.set_option(_lib.NKV_OPT_SMALL_PATH, 3)
+            c.set_option(_lib.NKV_OPT_SERVICE_MAILBOX, mailbox)
         for k in range(60):
             n = 1 + (k * 37) % 300
             base, off, ln = _values(n, 5000 + k, maxlen=300)
@@ -276,6 +280,11 @@ def test_resident_service_across_idle_exits_and_contexts(nkv, oracle):
             assert np.array_equal(nodes, nodes_w) and img == img_w, k
             if k % 10 == 9:
                 time.sleep(0.05)  # past the idle timeout: the next call relaunches
+        for c in ctxs:
+            st = c.small_service_state()
+            assert st["launches"] >= 2 and st["done"] == st["doorbell"]
+            if mailbox == 1:
+                assert st["mailbox_dev"] == 0
     finally:
         t0 = time.perf_counter()
         for c in ctxs:
@@ -283,8 +292,9 @@ def test_resident_service_across_idle_exits_and_contexts(nkv, oracle):
         assert time.perf_counter() - t0 < 5.0
 
 
+@pytest.mark.parametrize("mailbox", [0, 1])
 @pytest.mark.parametrize("in_arena", [False, True])
-def test_resident_service_inline_bound(small_ctx, oracle, in_arena):
+def test_resident_service_inline_bound(small_ctx, oracle, in_arena, mailbox):
     """The service takes a request whose descriptors and values fit its own
     16 KiB input buffer (16 n + the 16-byte aligned value bytes <= 16384) with
     the request line, and any other one from the staging buffer -- or, for
@@ -294,6 +304,7 @@ def test_resident_service_inline_bound(small_ctx, oracle, in_arena):
     _lib, ctx = small_ctx
     L = _lib.lib()
     ctx.set_option(_lib.NKV_OPT_SMALL_PATH, 3)
+    ctx.set_option(_lib.NKV_OPT_SERVICE_MAILBOX, mailbox)
     cap = 1 << 20
     p = ctypes.c_void_p()
     if in_arena:
@@ -328,6 +339,34 @@ def test_resident_service_inline_bound(small_ctx, oracle, in_arena):
     finally:
         if in_arena:
             _lib.check(L.nkv_host_free(ctx.h, p))
+        ctx.set_option(_lib.NKV_OPT_SERVICE_MAILBOX, 0)
+
+
+def test_resident_service_mailbox_switch(small_ctx, oracle):
+    """NKV_OPT_SERVICE_MAILBOX changed while the service runs: the running
+    service is stopped, the next call starts it in the other form, and every
+    tree stays bit-exact; out-of-range values are refused."""
+    _lib, ctx = small_ctx
+    L = _lib.lib()
+    ctx.set_option(_lib.NKV_OPT_SMALL_PATH, 3)
+    for bad in (-1, 2):
+        assert L.nkv_ctx_set_option(ctx.h, _lib.NKV_OPT_SERVICE_MAILBOX, bad) == _lib.NKV_ERR_INVALID
+    forms = []
+    for k, mailbox in enumerate([0, 1, 1, 0, 1, 0, 0]):
+        ctx.set_option(_lib.NKV_OPT_SERVICE_MAILBOX, mailbox)
+        for j in range(3):
+            base, off, ln = _values(5 + 11 * k + j, 6000 + 10 * k + j, maxlen=300)
+            nodes_w, img_w = _want(oracle, base, off, ln)
+            root, nodes, img, path = _run(_lib, ctx, base, off, ln)
+            assert path == _lib.NKV_PATH_SMALL
+            assert np.array_equal(nodes, nodes_w) and img == img_w, (k, j)
+        st = ctx.small_service_state()
+        assert st["live"] == 1 and st["done"] == st["doorbell"]
+        forms.append((mailbox, st["mailbox_dev"]))
+    assert all(dev == 0 for mb, dev in forms if mb == 1)
+    # a large-BAR GPU takes the device form whenever it is asked for
+    assert len({dev for mb, dev in forms if mb == 0}) == 1
+    ctx.set_option(_lib.NKV_OPT_SERVICE_MAILBOX, 0)
 
 
 @pytest.mark.parametrize("mode", [1, 2, 3])

@@ -17,7 +17,8 @@
 //               as they lie in the memtable: the C-ABI's own floor
 // with the context's NKV_OPT_SMALL_PATH set to MODE (0 = the grid path, 1 = the
 // one-launch kernel reading pinned host memory, 2 = the one launch through HBM,
-// 3 = the resident service: no launch per flush).
+// 3 = the resident service: no launch per flush; 3h = the same with its
+// requests in host memory, NKV_OPT_SERVICE_MAILBOX 1).
 //
 // Usage: small_flush MODE REPS DIR SHAPE...   SHAPE = N:MINLEN:MAXLEN[:SEED]
 // One JSON line per shape; roots in hex so the caller checks them against the
@@ -62,10 +63,13 @@ int main(int argc, char** argv) {
         return 2;
     }
     const int mode = std::atoi(argv[1]);
+    // "3h": the service with its requests in host memory (NKV_OPT_SERVICE_MAILBOX 1)
+    const bool host_mailbox = std::string(argv[1]).find('h') != std::string::npos;
     const int reps = std::max(3, std::atoi(argv[2]));
     const std::string dir = argv[3];
     Session& S = Session::Default();
     check(nkv_ctx_set_option(S.ctx(), NKV_OPT_SMALL_PATH, mode), "NKV_OPT_SMALL_PATH");
+    check(nkv_ctx_set_option(S.ctx(), NKV_OPT_SERVICE_MAILBOX, host_mailbox ? 1 : 0), "NKV_OPT_SERVICE_MAILBOX");
     for (int a = 4; a < argc; ++a) {
         unsigned long long n = 0, lo = 0, hi = 0, seed = 0x6E616B67ull;
         if (std::sscanf(argv[a], "%llu:%llu:%llu:%llx", &n, &lo, &hi, &seed) < 3 || n == 0 || hi < lo) {

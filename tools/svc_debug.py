@@ -4,7 +4,7 @@ each call's wall time, result against the oracle and the mailbox state
 (nkv_ctx_small_service_state), printed as it goes; a watchdog ends the process
 after --limit seconds so a stuck call cannot hang the GPU job.
 
-    python tools/svc_debug.py [--limit 60] [--modes 1,3] [--trace]
+    python tools/svc_debug.py [--limit 60] [--modes 1,3] [--trace] [--mailbox 0|1]
 """
 import faulthandler
 import os
@@ -24,6 +24,10 @@ def main():
     L = _lib.lib()
     ctx = _lib.Context(0)
     ctx.set_option(_lib.NKV_OPT_SMALL_PATH, 3)
+    # --mailbox 1: the service's requests in host memory (NKV_OPT_SERVICE_MAILBOX)
+    mailbox = int(sys.argv[sys.argv.index("--mailbox") + 1]) if "--mailbox" in sys.argv else 0
+    ctx.set_option(_lib.NKV_OPT_SERVICE_MAILBOX, mailbox)
+    print("mailbox option", mailbox, flush=True)
     rng = np.random.default_rng(3)
     print("state0", ctx.small_service_state(), flush=True)
     sizes = ([int(x) for x in sys.argv[sys.argv.index("--sizes") + 1].split(",")] if "--sizes" in sys.argv
