@@ -199,9 +199,10 @@ int nkv_ctx_last_path(nkv_ctx *ctx, int *path);
  * diagnostics: out[0] doorbell (latest request), out[1] served (the latest the
  * service took), out[2] done (the latest it answered), out[3] launches so far,
  * out[4] 1 while a launch may still run, out[5] 1 if its stream still has work,
- * out[6] 1 if its requests go through device memory (NKV_OPT_SERVICE_MAILBOX).
- * All zero before the first request. */
-int nkv_ctx_small_service_state(nkv_ctx *ctx, uint64_t out[7]);
+ * out[6] 1 if its requests go through device memory (NKV_OPT_SERVICE_MAILBOX),
+ * out[7] where its latest launch landed: XCC_ID << 32 | HW_ID (the hardware's
+ * wave/SIMD/CU/SE word).  All zero before the first request. */
+int nkv_ctx_small_service_state(nkv_ctx *ctx, uint64_t out[8]);
 /* Diagnostics of the same service: enable = 1 makes it stamp the phases of
  * each following request; out (nullable) receives the latest traced request's
  * stamps, seven (s_memrealtime at 100 MHz, s_memtime in shader clocks) pairs:

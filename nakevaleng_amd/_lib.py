@@ -293,9 +293,13 @@ class Context:
 
     def small_service_state(self) -> dict:
         """The resident small-tree service's mailbox and launch state (diagnostics)."""
-        a = (ctypes.c_uint64 * 7)()
+        a = (ctypes.c_uint64 * 8)()
         check(lib().nkv_ctx_small_service_state(self.h, a))
-        return dict(zip(("doorbell", "served", "done", "launches", "live", "busy", "mailbox_dev"), list(a)))
+        d = dict(zip(("doorbell", "served", "done", "launches", "live", "busy", "mailbox_dev"), list(a)))
+        hw, d["xcc"] = a[7] & 0xFFFFFFFF, a[7] >> 32
+        # HW_REG_HW_ID fields (gfx9): wave [3:0], SIMD [5:4], CU [11:8], SH [12], SE [15:13]
+        d["simd"], d["cu"], d["sh"], d["se"] = (hw >> 4) & 3, (hw >> 8) & 15, (hw >> 12) & 1, (hw >> 13) & 7
+        return d
 
     def small_service_trace(self, enable: bool) -> list:
         """Turn the service's phase stamps on/off; returns the latest traced request's

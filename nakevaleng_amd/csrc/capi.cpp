@@ -977,12 +977,14 @@ int nkv_ctx_set_option(nkv_ctx* c, int key, int64_t value) try {
     }
 } NKV_CATCH
 
-int nkv_ctx_small_service_state(nkv_ctx* c, uint64_t out[7]) try {
+int nkv_ctx_small_service_state(nkv_ctx* c, uint64_t out[8]) try {
     if (!c || !out) return NKV_ERR_INVALID;
-    for (int k = 0; k < 7; ++k) out[k] = 0;
+    for (int k = 0; k < 8; ++k) out[k] = 0;
     if (c->h_mbox) {
         out[0] = __atomic_load_n(&svc_request_side(c)->doorbell, __ATOMIC_ACQUIRE);
         out[6] = c->svc_box_dev ? 1u : 0u;
+        out[7] = (uint64_t(__atomic_load_n(&c->h_mbox->xcc_id, __ATOMIC_ACQUIRE)) << 32) |
+                 __atomic_load_n(&c->h_mbox->hw_id, __ATOMIC_ACQUIRE);
         out[1] = __atomic_load_n(&c->h_mbox->served, __ATOMIC_ACQUIRE);
         out[2] = __atomic_load_n(&c->h_mbox->done, __ATOMIC_ACQUIRE);
     }

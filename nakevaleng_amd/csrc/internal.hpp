@@ -194,7 +194,9 @@ struct alignas(64) SmallMailbox {
     uint32_t served;    // service: the latest seq it served (a relaunch resumes from it)
     uint32_t done;      // service: seq whose outputs are all written
     uint32_t refused;   // service: seq of a request it refused (a field out of range): nothing written
-    uint32_t pad[12];
+    uint32_t hw_id;     // service: HW_REG_HW_ID of its wave 0 at launch (diagnostics: CU, SIMD, SE)
+    uint32_t xcc_id;    // service: HW_REG_XCC_ID at launch (which XCD)
+    uint32_t pad[10];
     SmallRequest req;   // host: written before the doorbell
     // service, when traced: (s_memrealtime, s_memtime) after the doorbell was
     // seen, the input staged, the leaves hashed, the levels + image written,

@@ -2302,6 +2302,11 @@ __global__ __launch_bounds__(kSmallBlock) void k_small_tree(const uint64_t* __re
 // real-time counter with no request, or between requests once it has lived
 // life_ticks (the host relaunches on its next call), so the grid always drains
 // and work queued behind it on a shared hardware queue waits a bounded time.
+// s_getreg_b32 operands: HW_REG_HW_ID (id 4: wave, SIMD, CU, SH, SE ...) and
+// HW_REG_XCC_ID (id 20, bits [3:0]), whole registers
+constexpr int kHwRegHwId = 4 | (0 << 6) | (31 << 11);
+constexpr int kHwRegXccId = 20 | (0 << 6) | (15 << 11);
+
 template <uint32_t B>
 __global__ __launch_bounds__(B) void k_small_service(SmallMailbox* __restrict__ mb, const SmallMailbox* rb,
                                                      const uint8_t* __restrict__ fixed_in, uint64_t idle_ticks,
@@ -2321,6 +2326,12 @@ __global__ __launch_bounds__(B) void k_small_service(SmallMailbox* __restrict__ 
     uint32_t served =
         __builtin_amdgcn_readfirstlane(__hip_atomic_load(&mb->served, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
     const uint64_t born = __builtin_amdgcn_s_memrealtime();
+    if (tid == 0) {  // where this launch landed (nkv_ctx_small_service_state)
+        __hip_atomic_store(&mb->hw_id, uint32_t(__builtin_amdgcn_s_getreg(kHwRegHwId)), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&mb->xcc_id, uint32_t(__builtin_amdgcn_s_getreg(kHwRegXccId)), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     uint64_t seen_rt = 0, seen_mt = 0;  // wave 0: when the latest doorbell was seen (traced requests)
     // (s_memrealtime, s_memtime) of a traced request's phase k into the mailbox
     auto stamp = [&](int k, uint64_t rt, uint64_t mt) {
