@@ -161,8 +161,8 @@ int nkv_ctx_sync(nkv_ctx *ctx);
                                  and writes its results across PCIe (host-coherent pinned
                                  buffers, no DMA); 2 = one copy to HBM, the launch, one copy
                                  back; 3 = the resident service: one workgroup stays on the GPU
-                                 and serves each call of at most 256 values from a host-coherent
-                                 mailbox as path 1 does, without a launch or the runtime's
+                                 and serves each call of at most 256 values from a mailbox
+                                 (NKV_OPT_SERVICE_MAILBOX) as path 1 does, without a launch or the runtime's
                                  completion (larger calls take path 1; the service leaves
                                  20 ms after its last request, or at nkv_ctx_destroy, and the
                                  next call starts it again; while it runs, a device-wide
