@@ -83,7 +83,7 @@ struct Rec {
     uint64_t req_ticks[kReqs];
 };
 
-template <bool IDLE>
+template <bool IDLE, int LANES, int LEVELS>
 __global__ __launch_bounds__(256) void k_shape(Rec* out) {
     __shared__ uint4 blk[1024];
     __shared__ uint32_t dig[5 * 64];
@@ -101,7 +101,7 @@ __global__ __launch_bounds__(256) void k_shape(Rec* out) {
         }
         __syncthreads();
         const uint64_t r0 = __builtin_amdgcn_s_memrealtime();
-        if (tid < 10) {  // 10 lanes of wave 0, as a 10-value flush
+        if (tid < LANES) {  // 10 lanes of wave 0, as a 10-value flush
             for (int b = 0; b < 8; ++b) {
                 const uint32_t at = ((h[0] + tid + b) & 255u) * 4u;
                 uint32_t m[16];
@@ -118,7 +118,7 @@ __global__ __launch_bounds__(256) void k_shape(Rec* out) {
 #pragma unroll
             for (int k = 0; k < 5; ++k) dig[5 * tid + k] = h[k];
         }
-        for (int lv = 0; lv < 4; ++lv) {  // the levels' barriers
+        for (int lv = 0; lv < LEVELS; ++lv) {  // the levels' barriers
             __syncthreads();
             if (tid < (10u >> lv)) h[0] ^= dig[5 * tid];
         }
@@ -134,31 +134,38 @@ __global__ __launch_bounds__(256) void k_shape(Rec* out) {
     }
 }
 
+template <bool IDLE, int LANES, int LEVELS>
+static int series(const char* name, Rec* d, int launches, unsigned threads) {
+    printf("%s (threads %u, lanes %d, level barriers %d, idle %d)\n", name, threads, LANES, LEVELS, int(IDLE));
+    for (int l = 0; l < launches; ++l) {
+        hipLaunchKernelGGL((k_shape<IDLE, LANES, LEVELS>), dim3(1), dim3(threads), 0, 0, d);
+        CK(hipGetLastError());
+        CK(hipDeviceSynchronize());
+        Rec r;
+        CK(hipMemcpy(&r, d, sizeof r, hipMemcpyDeviceToHost));
+        std::vector<uint64_t> t(r.req_ticks + 4, r.req_ticks + kReqs);
+        std::sort(t.begin(), t.end());
+        printf("  launch %2d: xcc %u se %u cu %2u simd %u: request median %.2f us (min %.2f max %.2f)\n", l,
+               r.xcc & 15, (r.hw >> 13) & 7, (r.hw >> 8) & 15, (r.hw >> 4) & 3, t[t.size() / 2] / 100.0,
+               t.front() / 100.0, t.back() / 100.0);
+        fflush(stdout);
+    }
+    return 0;
+}
+
 int main(int argc, char** argv) {
-    const int launches = argc > 1 ? atoi(argv[1]) : 16;
+    const int launches = argc > 1 ? atoi(argv[1]) : 8;
     CK(hipSetDevice(0));
     Rec* d = nullptr;
     CK(hipMalloc(&d, sizeof(Rec)));
-    for (int idle = 1; idle >= 0; --idle) {
-        printf("IDLE %d (wave 0 sleeps ~20 us between requests: %s)\n", idle, idle ? "yes" : "no");
-        for (int l = 0; l < launches; ++l) {
-            if (idle)
-                hipLaunchKernelGGL(k_shape<true>, dim3(1), dim3(256), 0, 0, d);
-            else
-                hipLaunchKernelGGL(k_shape<false>, dim3(1), dim3(256), 0, 0, d);
-            CK(hipGetLastError());
-            CK(hipDeviceSynchronize());
-            Rec r;
-            CK(hipMemcpy(&r, d, sizeof r, hipMemcpyDeviceToHost));
-            std::vector<uint64_t> t(r.req_ticks + 4, r.req_ticks + kReqs);
-            std::sort(t.begin(), t.end());
-            printf("  launch %2d: xcc %u se %u cu %2u simd %u: request median %.2f us (min %.2f max %.2f)\n", l,
-                   r.xcc & 15, (r.hw >> 13) & 7, (r.hw >> 8) & 15, (r.hw >> 4) & 3, t[t.size() / 2] / 100.0,
-                   t.front() / 100.0, t.back() / 100.0);
-            fflush(stdout);
-        }
-    }
+    int rc = 0;
+    rc |= series<false, 10, 4>("A service shape", d, launches, 256);
+    rc |= series<false, 10, 4>("B one wave", d, launches, 64);
+    rc |= series<false, 64, 4>("C 256 threads, 64 lanes", d, launches, 256);
+    rc |= series<false, 10, 0>("D 256 threads, no level barriers", d, launches, 256);
+    rc |= series<false, 64, 0>("E one wave, 64 lanes, no barriers (cu_speed's shape)", d, launches, 64);
+    rc |= series<false, 10, 0>("F one wave, 10 lanes, no level barriers", d, launches, 64);
     (void)hipFree(d);
-    printf("done\n");
-    return 0;
+    printf("done rc=%d\n", rc);
+    return rc;
 }
