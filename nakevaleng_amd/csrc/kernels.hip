@@ -2044,10 +2044,23 @@ __global__ __launch_bounds__(kBlock) void k_fill(uint8_t* __restrict__ buf, uint
 
 constexpr uint32_t kSmallBlock = 256;
 
-// SHA-1 of p[0, len), p 16-byte aligned, one block of register lookahead
-__device__ __forceinline__ void sha1_value_aligned(const uint8_t* p, uint64_t len, uint32_t h[5]) {
+// SHA-1 of p[0, len), p 16-byte aligned, one block of register lookahead,
+// with every lane of the wave issuing every compression.  A wave runs its VALU work up to 35 % slower on some CUs when fewer than ~48 of
+// its lanes are active than with all of them (one clock, same instructions:
+// tools/svc_shape.hip, profiles/r06_svc_shape_lanes.txt -- 10 active lanes take
+// 11.2-15.1 us by CU for what 48 or 64 lanes do in 11.0 us on every CU), and a
+// small tree's waves have few values.  So the full-block loop runs to the
+// wave's largest block count (a lane past its own blocks compresses its stale
+// block into a copy it drops) and the padding blocks run in every lane; a lane
+// with no value (len 0) hashes the empty value, which its caller drops.  The
+// caller calls it with every lane of the wave active.
+__device__ __forceinline__ void sha1_value_all_lanes(const uint8_t* p, uint32_t len, uint32_t h[5]) {
     sha1_init(h);
-    const uint64_t nfull = len >> 6;
+    const uint32_t nfull = len >> 6;
+    uint32_t most = nfull;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) most = max(most, uint32_t(__shfl_xor(int(most), o)));
+    most = uint32_t(__builtin_amdgcn_readfirstlane(int(most)));  // wave-uniform trip count
     const uint4* q = reinterpret_cast<const uint4*>(p);
     uint4 cur[4], nxt[4];
 #pragma unroll
@@ -2055,14 +2068,19 @@ __device__ __forceinline__ void sha1_value_aligned(const uint8_t* p, uint64_t le
         cur[k] = nfull ? q[k] : make_uint4(0u, 0u, 0u, 0u);
         nxt[k] = make_uint4(0u, 0u, 0u, 0u);
     }
-    for (uint64_t b = 0; b < nfull; ++b) {
+    for (uint32_t b = 0; b < most; ++b) {
         if (b + 1 < nfull) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) nxt[k] = q[4 * (b + 1) + k];
         }
-        uint32_t w[16];
+        uint32_t w[16], t[5];
         be16_from_raw(cur, w);
-        sha1_compress(h, w);
+#pragma unroll
+        for (int i = 0; i < 5; ++i) t[i] = h[i];
+        sha1_compress(t, w);
+        const bool mine = b < nfull;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) h[i] = mine ? t[i] : h[i];
 #pragma unroll
         for (int k = 0; k < 4; ++k) cur[k] = nxt[k];
     }
@@ -2130,13 +2148,20 @@ __device__ __forceinline__ void small_levels_and_image(uint8_t* sm, uint8_t* seg
     int lv = 1;
     do {
         const uint32_t pc = (cnt + 1) >> 1;
-        for (uint32_t j = tid; j < pc; j += B) {
-            const bool lone = 2 * j + 1 >= cnt;
-            uint32_t l[5], r[5] = {0u, 0u, 0u, 0u, 0u}, o[5];
-            load_digest(sm, base + 2 * j, l);
-            if (!lone) load_digest(sm, base + 2 * j + 1, r);
-            sha1_parent(l, r, lone, o);
-            store_digest(sm, base + cnt + j, o);
+        // every lane of a wave that has a parent to build takes part (a lane
+        // past the level's end rebuilds the last parent and drops it): a wave
+        // with few active lanes computes slower on some CUs (sha1_value_all_lanes)
+        for (uint32_t j0 = 0; j0 < pc; j0 += B) {
+            const uint32_t j = j0 + tid;
+            if ((j & ~63u) < pc) {
+                const uint32_t jj = min(j, pc - 1u);
+                const bool lone = 2 * jj + 1 >= cnt;
+                uint32_t l[5], r[5] = {0u, 0u, 0u, 0u, 0u}, o[5];
+                load_digest(sm, base + 2 * jj, l);
+                if (!lone) load_digest(sm, base + 2 * jj + 1, r);
+                sha1_parent(l, r, lone, o);
+                if (j < pc) store_digest(sm, base + cnt + j, o);
+            }
         }
         __syncthreads();
         base += cnt;
@@ -2259,7 +2284,11 @@ __global__ __launch_bounds__(kSmallBlock) void k_small_tree(const uint64_t* __re
     }
     NKV_STAMP(1);
     uint32_t h[5] = {0u, 0u, 0u, 0u, 0u};
-    if (i < n) sha1_value_aligned(vals + desc[2 * i], desc[2 * i + 1], h);  // NewLeaf, merklenode.go:27-34
+    if ((i & ~63u) < n) {  // every lane of a wave with a value (sha1_value_all_lanes)
+        const bool real = i < n;
+        sha1_value_all_lanes(real ? vals + desc[2 * i] : vals, real ? uint32_t(desc[2 * i + 1]) : 0u,
+                             h);  // NewLeaf, merklenode.go:27-34
+    }
     NKV_STAMP(2);
     if (gridDim.x > 1) {
         if (i < n) store_digest(scratch, i, h);
@@ -2408,10 +2437,13 @@ __global__ __launch_bounds__(B) void k_small_service(SmallMailbox* __restrict__ 
                 vals = seg + 16u * n;
             }
             if (traced && tid == 0) stamp(1, __builtin_amdgcn_s_memrealtime(), __builtin_amdgcn_s_memtime());
-            for (uint32_t i = tid; i < n; i += B) {
+            static_assert(kSvcMaxN <= B, "one leaf per thread");
+            if ((tid & ~63u) < n) {  // every lane of a wave with a value (sha1_value_all_lanes)
+                const bool real = tid < n;
                 uint32_t h[5];
-                sha1_value_aligned(vals + desc[2 * i], desc[2 * i + 1], h);  // NewLeaf, merklenode.go:27-34
-                store_digest(sm, i, h);
+                sha1_value_all_lanes(real ? vals + desc[2 * tid] : vals, real ? uint32_t(desc[2 * tid + 1]) : 0u,
+                                     h);  // NewLeaf, merklenode.go:27-34
+                if (real) store_digest(sm, tid, h);
             }
             if (traced) {
                 __syncthreads();

@@ -13,7 +13,7 @@
 // the median request time and the placement.
 //
 //   hipcc --offload-arch=gfx950 -O3 tools/svc_shape.hip -o tools/svc_shape.bin
-//   tools/svc_shape.bin [launches]
+//   tools/svc_shape.bin [launches] [bisect|lanes]
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -83,7 +83,9 @@ struct Rec {
     uint64_t req_ticks[kReqs];
 };
 
-template <bool IDLE, int LANES, int LEVELS>
+// QUARTERS: LANES active lanes in each 16-lane quarter of wave 0 instead of the
+// first LANES lanes
+template <bool IDLE, int LANES, int LEVELS, bool QUARTERS = false>
 __global__ __launch_bounds__(256) void k_shape(Rec* out) {
     __shared__ uint4 blk[1024];
     __shared__ uint32_t dig[5 * 64];
@@ -101,7 +103,7 @@ __global__ __launch_bounds__(256) void k_shape(Rec* out) {
         }
         __syncthreads();
         const uint64_t r0 = __builtin_amdgcn_s_memrealtime();
-        if (tid < LANES) {  // 10 lanes of wave 0, as a 10-value flush
+        if (QUARTERS ? (tid < 64 && (tid & 15u) < uint32_t(LANES)) : tid < uint32_t(LANES)) {  // e.g. 10 lanes: a 10-value flush
             for (int b = 0; b < 8; ++b) {
                 const uint32_t at = ((h[0] + tid + b) & 255u) * 4u;
                 uint32_t m[16];
@@ -134,11 +136,12 @@ __global__ __launch_bounds__(256) void k_shape(Rec* out) {
     }
 }
 
-template <bool IDLE, int LANES, int LEVELS>
+template <bool IDLE, int LANES, int LEVELS, bool QUARTERS = false>
 static int series(const char* name, Rec* d, int launches, unsigned threads) {
-    printf("%s (threads %u, lanes %d, level barriers %d, idle %d)\n", name, threads, LANES, LEVELS, int(IDLE));
+    printf("%s (threads %u, lanes %d%s, level barriers %d, idle %d)\n", name, threads, LANES,
+           QUARTERS ? " per quarter" : "", LEVELS, int(IDLE));
     for (int l = 0; l < launches; ++l) {
-        hipLaunchKernelGGL((k_shape<IDLE, LANES, LEVELS>), dim3(1), dim3(threads), 0, 0, d);
+        hipLaunchKernelGGL((k_shape<IDLE, LANES, LEVELS, QUARTERS>), dim3(1), dim3(threads), 0, 0, d);
         CK(hipGetLastError());
         CK(hipDeviceSynchronize());
         Rec r;
@@ -159,12 +162,24 @@ int main(int argc, char** argv) {
     Rec* d = nullptr;
     CK(hipMalloc(&d, sizeof(Rec)));
     int rc = 0;
-    rc |= series<false, 10, 4>("A service shape", d, launches, 256);
-    rc |= series<false, 10, 4>("B one wave", d, launches, 64);
-    rc |= series<false, 64, 4>("C 256 threads, 64 lanes", d, launches, 256);
-    rc |= series<false, 10, 0>("D 256 threads, no level barriers", d, launches, 256);
-    rc |= series<false, 64, 0>("E one wave, 64 lanes, no barriers (cu_speed's shape)", d, launches, 64);
-    rc |= series<false, 10, 0>("F one wave, 10 lanes, no level barriers", d, launches, 64);
+    const char* which = argc > 2 ? argv[2] : "bisect";
+    if (which[0] == 'b') {  // round 6, first: which ingredient
+        rc |= series<false, 10, 4>("A service shape", d, launches, 256);
+        rc |= series<false, 10, 4>("B one wave", d, launches, 64);
+        rc |= series<false, 64, 4>("C 256 threads, 64 lanes", d, launches, 256);
+        rc |= series<false, 10, 0>("D 256 threads, no level barriers", d, launches, 256);
+        rc |= series<false, 64, 0>("E one wave, 64 lanes, no barriers (cu_speed's shape)", d, launches, 64);
+        rc |= series<false, 10, 0>("F one wave, 10 lanes, no level barriers", d, launches, 64);
+    } else {  // second: which active-lane patterns are slow
+        rc |= series<false, 1, 0>("G 1 lane", d, launches, 64);
+        rc |= series<false, 16, 0>("H lanes 0-15 (one whole quarter)", d, launches, 64);
+        rc |= series<false, 17, 0>("I lanes 0-16", d, launches, 64);
+        rc |= series<false, 32, 0>("J lanes 0-31", d, launches, 64);
+        rc |= series<false, 48, 0>("K lanes 0-47", d, launches, 64);
+        rc |= series<false, 63, 0>("L lanes 0-62", d, launches, 64);
+        rc |= series<false, 1, 0, true>("M one lane in each quarter", d, launches, 64);
+        rc |= series<false, 3, 0, true>("N three lanes in each quarter", d, launches, 64);
+    }
     (void)hipFree(d);
     printf("done rc=%d\n", rc);
     return rc;
