@@ -36,6 +36,9 @@ namespace nkv {
 #ifndef NKV_EXP_NOTAIL
 #define NKV_EXP_NOTAIL 0
 #endif
+#ifndef NKV_EXP_PARTIAL_REDUCE
+#define NKV_EXP_PARTIAL_REDUCE 0  // 1: subtree_reduce with only the live lanes active (the round-5 form)
+#endif
 #ifndef NKV_EXP_FIXEDHDR
 #define NKV_EXP_FIXEDHDR 0
 #endif
@@ -219,16 +222,23 @@ __device__ __forceinline__ void subtree_reduce(uint32_t (*lds)[B], uint64_t n, i
         const uint64_t ncur = ((nprev - 1) >> 1) + 1;
         const uint64_t lo_cur = lo_prev >> 1;
         span >>= 1;
-        const bool act = tid < span && lo_cur + tid < ncur;
+        // lanes [0, live) build this level's parents; every lane of a wave that
+        // has one takes part (a lane past live rebuilds the last parent and
+        // drops it): a wave with few active lanes computes up to 35 % slower on
+        // some CUs, and the narrow top levels are a lone-wave chain
+        // (sha1_value_all_lanes, tools/svc_shape.hip)
+        const int live = ncur > lo_cur ? int(min<uint64_t>(uint64_t(span), ncur - lo_cur)) : 0;
+        const bool act = tid < live;
         uint32_t out[5];
         __syncthreads();
-        if (act) {
+        if (NKV_EXP_PARTIAL_REDUCE ? act : (tid & ~63) < live) {
+            const int t = min(tid, live - 1);
             uint32_t l[5], r[5];
-            const bool lone = (2 * (lo_cur + tid) + 1) >= nprev;
+            const bool lone = (2 * (lo_cur + uint64_t(t)) + 1) >= nprev;
 #pragma unroll
             for (int k = 0; k < 5; ++k) {
-                l[k] = lds[k][2 * tid];
-                r[k] = lone ? 0u : lds[k][2 * tid + 1];
+                l[k] = lds[k][2 * t];
+                r[k] = lone ? 0u : lds[k][2 * t + 1];
             }
             sha1_parent(l, r, lone, out);
         }
