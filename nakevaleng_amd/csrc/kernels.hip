@@ -39,9 +39,6 @@ namespace nkv {
 #ifndef NKV_EXP_PARTIAL_REDUCE
 #define NKV_EXP_PARTIAL_REDUCE 0  // 1: subtree_reduce with only the live lanes active (the round-5 form)
 #endif
-#ifndef NKV_EXP_PARTIAL_RING
-#define NKV_EXP_PARTIAL_RING 0  // 1: the work queue's blocks compressed by the live lanes only (round-5 form)
-#endif
 #ifndef NKV_EXP_FIXEDHDR
 #define NKV_EXP_FIXEDHDR 0
 #endif
@@ -654,20 +651,11 @@ template <int R>
 __device__ __forceinline__ void sha1_blocks_ring_vc(uint8_t* wbuf, const uint8_t* p, uint32_t my_nfull,
                                                     uint32_t h[5]) {
     ring_vc_blocks<R>(wbuf, p, my_nfull, [&](uint32_t b, uint32_t w[16]) {
-#if NKV_EXP_PARTIAL_RING
+        // the live lanes only: compressing in every lane (into a copy a lane
+        // past its value drops) measured no faster on configs[2] and ran the
+        // clock 1-2 % lower (profiles/r06_ab_ring_lanes.txt): its sorted groups
+        // keep waves nearly full, unlike the small trees (sha1_value_all_lanes)
         if (b < my_nfull) sha1_compress(h, w);
-#else
-        // every lane compresses (a lane past its value into a copy it drops):
-        // the wave issues the same instructions either way, and a wave with
-        // few active lanes computes slower on some CUs (sha1_value_all_lanes)
-        uint32_t t[5];
-#pragma unroll
-        for (int i = 0; i < 5; ++i) t[i] = h[i];
-        sha1_compress(t, w);
-        const bool mine = b < my_nfull;
-#pragma unroll
-        for (int i = 0; i < 5; ++i) h[i] = mine ? t[i] : h[i];
-#endif
     });
 }
 

@@ -2,7 +2,8 @@
 # Round 6: the work queue's blocks compressed by every lane (product) against
 # only the live lanes (tools/libnkvmerkle_partialring.so: build_exp.sh
 # partialring -DNKV_EXP_PARTIAL_RING=1), configs[2] (--config mixed) without
-# sub-records, alternating x4 on one box; roots verified each run.
+# sub-records, alternating x4 on one box; roots verified each run.  Reproduces
+# only on commit d4a64e5 (the switch was removed with the change: no gain).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
 export HSA_ENABLE_IPC_MODE_LEGACY=0
