@@ -182,14 +182,15 @@ int nkv_ctx_sync(nkv_ctx *ctx);
 #define NKV_OPT_QUEUE_PAIR 19 /* retired (ABI version 1): 0 is the only value accepted (one wave per
                                  work-queue group; the two-wave pair kernel of round 5 was removed
                                  after failing its first GPU parity run) */
-#define NKV_OPT_SERVICE_MAILBOX 20 /* where the resident service (NKV_OPT_SMALL_PATH 3) takes its
-                                      requests: 0 (default) = the doorbell, the request line and
-                                      the packed input in fine-grained device memory the host
-                                      stores to directly, when the GPU has a large BAR (the service
-                                      polls and reads local memory; else as 1); 1 = in
-                                      host-coherent memory (the service polls across PCIe).
-                                      Answers always land in host memory.  A change stops a
-                                      running service; the next call starts it in the new form */
+#define NKV_OPT_SERVICE_MAILBOX 20 /* where small-tree calls put their input: 0 (default) = in
+                                      fine-grained device memory the host stores to directly,
+                                      when the GPU has a large BAR and the packed input fits
+                                      16 KiB (the kernel stages local memory instead of reading
+                                      across PCIe; for the resident service, NKV_OPT_SMALL_PATH 3,
+                                      its doorbell and request line too, so it polls local
+                                      memory; else as 1); 1 = in host-coherent memory.  Answers
+                                      always land in host memory.  A change stops a running
+                                      service; the next call starts it in the new form */
 int nkv_ctx_set_option(nkv_ctx *ctx, int key, int64_t value);
 /* Which path the latest host-buffer tree call of the context took */
 #define NKV_PATH_GRID 0  /* copies + leaf kernel + per-level reduce launches */

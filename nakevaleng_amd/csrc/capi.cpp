@@ -290,6 +290,28 @@ int svc_buffers(nkv_ctx* c) {
     return NKV_OK;
 }
 
+// The one-launch path's input buffer in device memory the host stores to
+// (made once, on a large-BAR GPU with NKV_OPT_SERVICE_MAILBOX 0), or nullptr:
+// a packed input of at most kSmallSeg bytes is copied there, so the kernel
+// stages it from local memory instead of across PCIe.
+uint8_t* small_input_bar(nkv_ctx* c) {
+    if (c->svc_mailbox != 0) return nullptr;
+    if (!c->d_sin_bar && !c->sin_bar_tried) {
+        c->sin_bar_tried = true;
+        int large = 0;
+        void* d = nullptr;
+        if (hipDeviceGetAttribute(&large, hipDeviceAttributeIsLargeBar, c->device) == hipSuccess && large &&
+            hipExtMallocWithFlags(&d, kSmallSeg, hipDeviceMallocFinegrained) == hipSuccess) {
+            if (host_mapped(d))
+                c->d_sin_bar = static_cast<uint8_t*>(d);
+            else
+                (void)hipFree(d);
+        }
+        (void)hipGetLastError();
+    }
+    return c->d_sin_bar;
+}
+
 // The request side as the host stores to it (the device's address too).
 SmallMailbox* svc_request_side(nkv_ctx* c) {
     return c->svc_box_dev ? reinterpret_cast<SmallMailbox*>(c->d_svc_box) : c->h_mbox;
@@ -499,6 +521,16 @@ int small_tree(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint6
         const uint64_t* d_desc = static_cast<const uint64_t*>(din);
         const uint8_t* d_vals = in_place ? static_cast<const uint8_t*>(dblk) + lo
                                          : reinterpret_cast<const uint8_t*>(d_desc + 2 * n);
+        // a packed input that fits the kernel's LDS stage goes to device memory
+        // over the large BAR (posted writes: they land before the launch's
+        // doorbell), so the kernel stages it without a PCIe read round trip
+        uint8_t* bar = !in_place && in_bytes <= kSmallSeg ? small_input_bar(c) : nullptr;
+        if (bar) {
+            memcpy(bar, c->h_sin, in_bytes);
+            store_fence();
+            d_desc = reinterpret_cast<const uint64_t*>(bar);
+            d_vals = bar + 16 * n;
+        }
         HIPTRY(launch_small_tree(d_desc, d_vals, uint32_t(vext), uint32_t(n), static_cast<uint8_t*>(dout),
                                  uint32_t(img_at), scratch, ticket,
                                  reinterpret_cast<unsigned int*>(static_cast<uint8_t*>(dout) + out_bytes), seq,
@@ -851,6 +883,7 @@ void nkv_ctx_destroy(nkv_ctx* c) {
     if (c->h_stage) (void)hipHostFree(c->h_stage);
     if (c->h_small) (void)hipHostFree(c->h_small);
     if (c->h_sin) (void)hipHostFree(c->h_sin);
+    if (c->d_sin_bar) (void)hipFree(c->d_sin_bar);
     if (c->h_sout) (void)hipHostFree(c->h_sout);
     for (hipEvent_t e : c->ring) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->join_ev) (void)hipEventDestroy(e);

@@ -218,6 +218,10 @@ struct nkv_ctx {
     // the host stores to directly (one block: the mailbox, then kSmallSeg bytes)
     uint8_t* d_svc_box = nullptr;
     int svc_mailbox = 0;      // NKV_OPT_SERVICE_MAILBOX
+    // the one-launch path's packed input in fine-grained device memory the host
+    // stores to (kSmallSeg bytes; NKV_OPT_SERVICE_MAILBOX 0 on a large-BAR GPU)
+    uint8_t* d_sin_bar = nullptr;
+    bool sin_bar_tried = false;
     bool svc_box_dev = false; // the live buffers are d_svc_box's (else h_mbox / h_svc_in)
     hipStream_t svc = nullptr;
     bool svc_live = false;   // a service launch was made and may still run

@@ -2289,6 +2289,9 @@ __global__ __launch_bounds__(kSmallBlock) void k_small_tree(const uint64_t* __re
     const uint32_t tid = threadIdx.x;
     const uint32_t i = blockIdx.x * kSmallBlock + tid;
     NKV_STAMP(0);
+    // the input may lie in fine-grained device memory the host stored to
+    // (NKV_OPT_SERVICE_MAILBOX 0): no stale L2 line of an earlier call's input
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     if (gridDim.x == 1 && 16u * n + vbytes <= kSmallSeg) {
         small_stage_in<kSmallBlock>(reinterpret_cast<const uint8_t*>(desc), seg, 16u * n);
         small_stage_in<kSmallBlock>(vals, seg + 16u * n, vbytes);
