@@ -8,7 +8,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 O=gpurun_out/${OUT:-r06q}
 mkdir -p $O
-timeout -k 10 400 python3 -u -m pytest tests/test_gpu_small.py tests/test_cpp_api.py -x -q --timeout 120 \
+timeout -k 10 400 python3 -u -m pytest tests/test_gpu_small.py tests/test_cpp_api.py -m gpu -x -q --timeout 120 \
     --timeout-method thread > $O/tests.txt 2>&1 || { tail -40 $O/tests.txt; exit 1; }
 tail -1 $O/tests.txt
 for mb in 0 1; do
