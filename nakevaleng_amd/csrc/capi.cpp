@@ -464,6 +464,11 @@ int small_tree(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint6
         in_place = false;
         TRY(svc_buffers(c));
     }
+    // likewise the one-launch path (1): an input that fits 16 KiB is packed and
+    // stored into BAR-mapped device memory (small_input_bar), arena values
+    // included, rather than read across PCIe where it lies
+    uint8_t* const bar = !svc && c->small_path == 1 && 16 * n + vbytes <= kSmallSeg ? small_input_bar(c) : nullptr;
+    if (bar) in_place = false;
     const uint64_t vext = in_place ? align16(hi) - lo : vbytes;  // the values' extent
     const uint64_t in_bytes = 16 * n + (in_place ? 0 : vbytes);
     if (!svc_inline) TRY(grow_coherent(&c->h_sin, &c->h_sin_cap, in_bytes));
@@ -524,7 +529,6 @@ int small_tree(nkv_ctx* c, const uint8_t* base, const uint64_t* off, const uint6
         // a packed input that fits the kernel's LDS stage goes to device memory
         // over the large BAR (posted writes: they land before the launch's
         // doorbell), so the kernel stages it without a PCIe read round trip
-        uint8_t* bar = !in_place && in_bytes <= kSmallSeg ? small_input_bar(c) : nullptr;
         if (bar) {
             memcpy(bar, c->h_sin, in_bytes);
             store_fence();

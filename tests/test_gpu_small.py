@@ -221,9 +221,11 @@ def test_small_flush_tool_roots(oracle, tmp_path):
 def test_small_path_reads_the_arena_in_place(small_ctx, oracle, coherent):
     """Values inside an nkv_host_alloc block (the mirrors' NewLeaf arena) at
     16-byte aligned places: with a host-coherent block (NKV_OPT_ARENA_COHERENT
-    1, the default) the one-launch kernel reads them where they lie; with a
-    default pinned block, or any unaligned place, they are packed first.  Either
-    way bit-exact, and a block rewritten between calls is read afresh."""
+    1, the default) the one-launch kernel reads them where they lie, unless
+    they fit 16 KiB on a large-BAR GPU (then they are packed into device
+    memory); with a default pinned block, or any unaligned place, they are
+    packed first.  Every way bit-exact, and a block rewritten between calls is
+    read afresh."""
     _lib, ctx = small_ctx
     L = _lib.lib()
     ctx.set_option(_lib.NKV_OPT_ARENA_COHERENT, coherent)
