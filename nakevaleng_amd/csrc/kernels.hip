@@ -2260,7 +2260,7 @@ __device__ __forceinline__ void small_levels_and_image(uint8_t* sm, uint8_t* seg
 // per wave (the guide's producer form: every storing wave waits for its own
 // stores, a barrier, then ONE lane's release fence -- a single L2 write-back --
 // its wait, and the flag); a fence in every wave cost each wave an L2
-// write-back (16 of them in the 1024-thread service).
+// write-back (16 of them in the service's first, 1024-thread form).
 __device__ __forceinline__ void small_signal_done(unsigned int* done, uint32_t seq) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's output stores have completed
     __syncthreads();
