@@ -392,3 +392,24 @@ def test_small_path_without_image(small_ctx, oracle, mode):
         _lib.check(L.nkv_tree_from_values(ctx.h, _lib.p8(base), _lib.p64(off), _lib.p64(ln), n, _lib.p8(root2),
                                           None, None))
         assert root2.tobytes() == nodes_w[-1].tobytes(), n
+
+
+@pytest.mark.parametrize("mode", [1, 3])
+def test_small_path_host_input_form(small_ctx, oracle, mode):
+    """NKV_OPT_SERVICE_MAILBOX 1: the one-launch kernel and the service take
+    their packed input from host memory instead of BAR-mapped device memory;
+    back to 0 in the same context, the device form again -- every n = 1..80 and
+    a few larger, bit-exact in both forms, calls alternating between them."""
+    _lib, ctx = small_ctx
+    ctx.set_option(_lib.NKV_OPT_SMALL_PATH, mode)
+    try:
+        for n in list(range(1, 81)) + [255, 256, 300]:
+            base, off, ln = _values(n, 9000 + n, maxlen=300)
+            nodes_w, img_w = _want(oracle, base, off, ln)
+            for mailbox in (1, 0):
+                ctx.set_option(_lib.NKV_OPT_SERVICE_MAILBOX, mailbox)
+                root, nodes, img, path = _run(_lib, ctx, base, off, ln)
+                assert path == _lib.NKV_PATH_SMALL
+                assert np.array_equal(nodes, nodes_w) and img == img_w, (mode, mailbox, n)
+    finally:
+        ctx.set_option(_lib.NKV_OPT_SERVICE_MAILBOX, 0)
